@@ -1,0 +1,72 @@
+/*
+ * lpcnet.h -- drop-in synthesis API of liblpcnet_mi355x.so.
+ *
+ * Each entry point replaces the symbol of the same name in the reference's
+ * include/lpcnet.h (auliaadila/LPCNet, cited as <file>:<line> relative to the
+ * reference root) with identical signature, argument meaning and error
+ * behaviour.  Only the synthesis subset is provided;
+ * encoder / decoder / PLC prototypes of the reference header are out of scope.
+ *
+ * Behavioural notes versus the reference:
+ *  - The reference binds a compiled-in model in lpcnet_init unless built with
+ *    USE_WEIGHTS_FILE (src/lpcnet.c:192-196).  This library has no compiled-in
+ *    model: it always behaves like the USE_WEIGHTS_FILE build, so callers load a
+ *    weight blob with lpcnet_load_model() (as src/lpcnet_demo.c:204-207 does).
+ *  - LPCNetState is a fixed-size host handle; the per-stream synthesis state
+ *    and the model live in MI355X device memory, bound lazily on first use.
+ *  - Output is PCM-identical to the reference's x86 AVX2 (DOT_PROD) build for
+ *    int8 blobs and to its --disable-dot-product build for fp32 blobs.
+ */
+#ifndef LPCNET_H_MI355X
+#define LPCNET_H_MI355X
+
+#ifndef LPCNET_EXPORT
+#if defined(__GNUC__)
+#define LPCNET_EXPORT __attribute__((visibility("default")))
+#else
+#define LPCNET_EXPORT
+#endif
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NB_FEATURES 20        /* include/lpcnet.h:45 */
+#define NB_TOTAL_FEATURES 36  /* include/lpcnet.h:46 */
+#define LPCNET_FRAME_SIZE (160) /* include/lpcnet.h:53 */
+
+typedef struct LPCNetState LPCNetState;
+
+/* include/lpcnet.h:156-160 -- size of an LPCNetState (caller allocation). */
+LPCNET_EXPORT int lpcnet_get_size(void);
+
+/* include/lpcnet.h:162-169 -- placement-initialise st (>= lpcnet_get_size()
+ * bytes).  Returns 0. */
+LPCNET_EXPORT int lpcnet_init(LPCNetState *st);
+
+/* include/lpcnet.h:171-174 -- allocate + initialise. */
+LPCNET_EXPORT LPCNetState *lpcnet_create(void);
+
+/* include/lpcnet.h:176-179 -- free a state from lpcnet_create (also releases
+ * the device resources bound to it). */
+LPCNET_EXPORT void lpcnet_destroy(LPCNetState *st);
+
+/* src/lpcnet.c:174-182 lpcnet_reset (declared at include/lpcnet.h:78 area):
+ * clear the dynamic synthesis state and reseed the RNG with "LPCNet". */
+LPCNET_EXPORT void lpcnet_reset(LPCNetState *st);
+
+/* include/lpcnet.h:181-188 -- synthesise N (<= 160) samples from one frame of
+ * NB_FEATURES features. */
+LPCNET_EXPORT void lpcnet_synthesize(LPCNetState *st, const float *features, short *output, int N);
+
+/* include/lpcnet.h:214 -- bind a weight blob (src/write_lpcnet_weights.c
+ * format).  Returns 0, or -1 if an array is missing or has the wrong size.
+ * Unlike the reference the blob is copied to the device, so the caller may
+ * free it afterwards. */
+LPCNET_EXPORT int lpcnet_load_model(LPCNetState *st, const unsigned char *data, int len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

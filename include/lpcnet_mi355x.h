@@ -1,0 +1,106 @@
+/*
+ * lpcnet_mi355x.h -- batch extension and tooling of liblpcnet_mi355x.so.
+ *
+ * The reference has no batch API (one LPCNetState = one stream on one core,
+ * SURVEY.md section 8b).  A batch owns B independent streams, each with
+ * exactly the semantics of one reference LPCNetState; stream s of a batch is
+ * PCM-identical to the same stream run alone through lpcnet_synthesize().
+ * Streams shard across GPUs with no collective (one batch per device).
+ */
+#ifndef LPCNET_MI355X_H
+#define LPCNET_MI355X_H
+
+#include "lpcnet.h"
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct LPCNetBatch LPCNetBatch;
+
+/* Weight-blob variants (chosen from the array sizes of the blob). */
+#define LPCNET_VARIANT_INT8 0 /* reference AVX2 build: DOT_PROD int8 GRU weights */
+#define LPCNET_VARIANT_FP32 1 /* reference --disable-dot-product build */
+
+typedef struct {
+  int variant;          /* LPCNET_VARIANT_* */
+  int gru_a_blocks;     /* 8x4 blocks in sparse_gru_a_recurrent_weights */
+  int gru_b_blocks;     /* 8x4 blocks in gru_b_weights */
+  int may_saturate;     /* 1 if an int8 pair can saturate the int16 maddubs sum */
+  double bytes_shared_per_frame;  /* algorithmic weight bytes read once per frame step */
+  double bytes_shared_per_sample; /* algorithmic weight bytes read once per sample step */
+  double bytes_per_stream_sample; /* per-stream bytes per sample (gathers, trace-free) */
+  double ops_per_sample;          /* 2*MAC per stream per sample */
+} LPCNetModelInfo;
+
+/* Create a batch of nb_streams streams on HIP device `device`.
+ * Returns NULL if the device is unavailable or nb_streams < 1. */
+LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device);
+LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b);
+/* 0 on success, -1 on a missing / mis-sized array (lpcnet_load_model rules). */
+LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *data, int len);
+LPCNET_EXPORT int lpcnet_batch_model_info(const LPCNetBatch *b, LPCNetModelInfo *info);
+/* lpcnet_reset() on every stream / on one stream. */
+LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b);
+LPCNET_EXPORT int lpcnet_batch_reset_stream(LPCNetBatch *b, int stream);
+LPCNET_EXPORT int lpcnet_batch_nb_streams(const LPCNetBatch *b);
+
+/* One frame for every stream, host buffers: features [B][NB_FEATURES],
+ * pcm [B][N], N <= 160.  Equivalent to lpcnet_synthesize() on each stream.
+ * Returns 0, or -1 on error (no model, bad N). */
+LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features, short *pcm, int N);
+
+/* nframes consecutive frames for every stream with device-resident I/O:
+ * d_features [nframes][B][NB_FEATURES] and d_pcm [nframes][B][N] are device
+ * pointers on the batch's device.  h_features holds the same features on the
+ * host: lpc_from_cepstrum (freq.c:310-320) runs on host threads, pipelined
+ * two frames ahead of its use (FEATURES_DELAY), and uploads 64 B/stream/frame.
+ * Work is enqueued on the batch's HIP stream; the call returns once every
+ * frame has been enqueued (use lpcnet_batch_sync to wait). */
+LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_features, const float *d_features,
+                                                 short *d_pcm, int nframes, int N);
+LPCNET_EXPORT int lpcnet_batch_sync(LPCNetBatch *b);
+
+/* Device memory helpers (so callers need no HIP headers). */
+LPCNET_EXPORT void *lpcnet_batch_device_alloc(LPCNetBatch *b, size_t bytes);
+LPCNET_EXPORT int lpcnet_batch_device_free(LPCNetBatch *b, void *p);
+LPCNET_EXPORT int lpcnet_batch_memcpy_h2d(LPCNetBatch *b, void *dst, const void *src, size_t bytes);
+LPCNET_EXPORT int lpcnet_batch_memcpy_d2h(LPCNetBatch *b, void *dst, const void *src, size_t bytes);
+
+/* Kernel timing (HIP events on the batch's stream, recorded around every
+ * launch since the last reset_timers): which = 0 sample-network kernel,
+ * 1 frame-network kernel.  Returns total ms and the number of launches. */
+LPCNET_EXPORT void lpcnet_batch_reset_timers(LPCNetBatch *b, int enable);
+LPCNET_EXPORT double lpcnet_batch_kernel_ms(LPCNetBatch *b, int which, int *launches);
+
+/* Debug / parity: per-sample trace of the pre-sampling logits (8 per sample,
+ * nnet.c:186-211) and the sampled excitation of the LAST synthesize call.
+ * logits [B][N][8], exc [B][N]. */
+LPCNET_EXPORT int lpcnet_batch_set_trace(LPCNetBatch *b, int enable);
+LPCNET_EXPORT int lpcnet_batch_get_trace(LPCNetBatch *b, float *logits, int *exc);
+/* Per-stream state snapshot: any pointer may be NULL. */
+LPCNET_EXPORT int lpcnet_batch_get_state(LPCNetBatch *b, int stream, float *gru_a_cond /*1152*/, float *gru_b_cond /*48*/,
+                                         float *lpc /*16*/, float *gru_a_state /*384*/, float *gru_b_state /*16*/,
+                                         int *frame_count);
+
+/* ---- tooling (host only, no GPU needed) -------------------------------- */
+/* Deterministic synthetic default-size model in the reference blob format.
+ * flags: bit0 = make some int8 pairs able to saturate maddubs.
+ * Returns the blob size; writes it if buf != NULL and cap is large enough. */
+LPCNET_EXPORT int lpcnet_mi355x_synthetic_model(unsigned seed, int variant, int flags, unsigned char *buf, int cap);
+/* Synthetic feature frames (NB_TOTAL_FEATURES floats each) for stream `stream`. */
+LPCNET_EXPORT void lpcnet_mi355x_synthetic_features(unsigned stream, int nframes, float *out);
+/* Host restatement of freq.c:310-320 lpc_from_cepstrum used by the engine. */
+LPCNET_EXPORT float lpcnet_mi355x_lpc_from_cepstrum(float *lpc, const float *cepstrum);
+/* The rcpps table the device activations use (2048 entries). */
+LPCNET_EXPORT const uint32_t *lpcnet_mi355x_rcp_table(void);
+/* Number of visible HIP devices (0 on a machine without GPU). */
+LPCNET_EXPORT int lpcnet_mi355x_device_count(void);
+/* Last error string of this thread. */
+LPCNET_EXPORT const char *lpcnet_mi355x_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
