@@ -1,0 +1,48 @@
+# Build of liblpcnet_mi355x.so (gfx950) and the CPU checker under oracle/.
+#
+#   make            -> lpcnet_amd/liblpcnet_mi355x.so + oracle/ libraries
+#   make lib        -> the product library only
+#
+# Every translation unit is compiled with -ffp-contract=off: the engine is
+# bit-exact with the reference x86 build only without FMA contraction.
+
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+JOBS ?= 4
+BUILD := build
+LIB := lpcnet_amd/liblpcnet_mi355x.so
+CSRC := lpcnet_amd/csrc
+HDRS := include/lpcnet.h include/lpcnet_mi355x.h $(CSRC)/lpcnet_engine.h $(CSRC)/rcp_table_x86.inc
+COMMON := -O3 -fPIC -ffp-contract=off -fno-fast-math -std=c++17 -Iinclude -I$(CSRC) -fvisibility=hidden -Wall -Wno-unused-function
+OBJS := $(BUILD)/kernels.o $(BUILD)/engine.o $(BUILD)/lpc_host.o $(BUILD)/model_gen.o
+
+all: lib oracle
+
+lib: $(LIB)
+
+$(BUILD):
+	mkdir -p $(BUILD)
+
+$(BUILD)/kernels.o: $(CSRC)/kernels.hip $(HDRS) | $(BUILD)
+	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -c $< -o $@
+
+$(BUILD)/engine.o: $(CSRC)/engine.cpp $(HDRS) | $(BUILD)
+	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -c $< -o $@
+
+$(BUILD)/lpc_host.o: $(CSRC)/lpc_host.cpp $(HDRS) | $(BUILD)
+	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -c $< -o $@
+
+$(BUILD)/model_gen.o: $(CSRC)/model_gen.cpp $(HDRS) | $(BUILD)
+	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(BUILD) $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all lib oracle clean

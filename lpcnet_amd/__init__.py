@@ -1,0 +1,273 @@
+"""lpcnet_amd -- Python mirror of the MI355X LPCNet synthesis engine.
+
+Thin ctypes binding over ``liblpcnet_mi355x.so`` (built in-tree by
+``make lib``).  The class API mirrors the reference C interface of
+``include/lpcnet.h`` (auliaadila/LPCNet):
+
+* :class:`LPCNet` -- one stream: ``lpcnet_create`` / ``lpcnet_load_model`` /
+  ``lpcnet_synthesize`` / ``lpcnet_reset`` / ``lpcnet_destroy``
+  (reference ``src/lpcnet.c:174-281``).
+* :class:`LPCNetBatch` -- B independent streams on one GPU (the batch extension
+  of ``include/lpcnet_mi355x.h``).
+
+There is no CPU fallback: every synthesis call runs the HIP kernels, and
+importing the package raises if the native library is absent.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblpcnet_mi355x.so")
+
+NB_FEATURES = 20
+NB_TOTAL_FEATURES = 36
+FRAME_SIZE = 160
+VARIANT_INT8 = 0
+VARIANT_FP32 = 1
+
+
+class LPCNetError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build it with `make lib` (or __graft_entry__.build()); "
+            "lpcnet_amd has no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    vp, i, f, u = C.c_void_p, C.c_int, C.c_float, C.c_uint
+    sig = {
+        "lpcnet_get_size": (i, []),
+        "lpcnet_init": (i, [vp]),
+        "lpcnet_create": (vp, []),
+        "lpcnet_destroy": (None, [vp]),
+        "lpcnet_reset": (None, [vp]),
+        "lpcnet_synthesize": (None, [vp, vp, vp, i]),
+        "lpcnet_load_model": (i, [vp, C.c_char_p, i]),
+        "lpcnet_batch_create": (vp, [i, i]),
+        "lpcnet_batch_destroy": (None, [vp]),
+        "lpcnet_batch_load_model": (i, [vp, C.c_char_p, i]),
+        "lpcnet_batch_model_info": (i, [vp, vp]),
+        "lpcnet_batch_reset": (None, [vp]),
+        "lpcnet_batch_reset_stream": (i, [vp, i]),
+        "lpcnet_batch_nb_streams": (i, [vp]),
+        "lpcnet_batch_synthesize": (i, [vp, vp, vp, i]),
+        "lpcnet_batch_synthesize_frames": (i, [vp, vp, vp, vp, i, i]),
+        "lpcnet_batch_sync": (i, [vp]),
+        "lpcnet_batch_device_alloc": (vp, [vp, C.c_size_t]),
+        "lpcnet_batch_device_free": (i, [vp, vp]),
+        "lpcnet_batch_memcpy_h2d": (i, [vp, vp, vp, C.c_size_t]),
+        "lpcnet_batch_memcpy_d2h": (i, [vp, vp, vp, C.c_size_t]),
+        "lpcnet_batch_reset_timers": (None, [vp, i]),
+        "lpcnet_batch_kernel_ms": (C.c_double, [vp, i, C.POINTER(C.c_int)]),
+        "lpcnet_batch_set_trace": (i, [vp, i]),
+        "lpcnet_batch_get_trace": (i, [vp, vp, vp]),
+        "lpcnet_batch_get_state": (i, [vp, i, vp, vp, vp, vp, vp, vp]),
+        "lpcnet_mi355x_synthetic_model": (i, [u, i, i, vp, i]),
+        "lpcnet_mi355x_synthetic_features": (None, [u, i, vp]),
+        "lpcnet_mi355x_lpc_from_cepstrum": (f, [vp, vp]),
+        "lpcnet_mi355x_rcp_table": (C.POINTER(C.c_uint32), []),
+        "lpcnet_mi355x_device_count": (i, []),
+        "lpcnet_mi355x_last_error": (C.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class ModelInfo(C.Structure):
+    _fields_ = [("variant", C.c_int), ("gru_a_blocks", C.c_int), ("gru_b_blocks", C.c_int),
+                ("may_saturate", C.c_int), ("bytes_shared_per_frame", C.c_double),
+                ("bytes_shared_per_sample", C.c_double), ("bytes_per_stream_sample", C.c_double),
+                ("ops_per_sample", C.c_double)]
+
+
+def last_error() -> str:
+    return (lib.lpcnet_mi355x_last_error() or b"").decode()
+
+
+def device_count() -> int:
+    return lib.lpcnet_mi355x_device_count()
+
+
+def synthetic_model(seed: int = 1, variant: int = VARIANT_INT8, saturating: bool = False) -> bytes:
+    """Deterministic synthetic default-size model in the reference blob format."""
+    flags = 1 if saturating else 0
+    n = lib.lpcnet_mi355x_synthetic_model(seed, variant, flags, None, 0)
+    buf = C.create_string_buffer(n)
+    lib.lpcnet_mi355x_synthetic_model(seed, variant, flags, buf, n)
+    return buf.raw
+
+
+def synthetic_features(stream: int, nframes: int) -> np.ndarray:
+    """[nframes, 36] float32 synthetic features of stream ``stream``."""
+    out = np.zeros((nframes, NB_TOTAL_FEATURES), np.float32)
+    lib.lpcnet_mi355x_synthetic_features(stream, nframes, out.ctypes.data)
+    return out
+
+
+def lpc_from_cepstrum(cepstrum: np.ndarray) -> np.ndarray:
+    """Host restatement of freq.c:310-320 used by the engine."""
+    c = np.ascontiguousarray(cepstrum, np.float32)
+    out = np.zeros(16, np.float32)
+    lib.lpcnet_mi355x_lpc_from_cepstrum(out.ctypes.data, c.ctypes.data)
+    return out
+
+
+def rcp_table() -> np.ndarray:
+    p = lib.lpcnet_mi355x_rcp_table()
+    return np.ctypeslib.as_array(p, shape=(2048,)).copy()
+
+
+class LPCNet:
+    """One synthesis stream (reference LPCNetState semantics)."""
+
+    def __init__(self, blob: bytes | None = None):
+        self._st = lib.lpcnet_create()
+        if not self._st:
+            raise LPCNetError("lpcnet_create failed")
+        if blob is not None:
+            self.load_model(blob)
+
+    def load_model(self, blob: bytes) -> None:
+        if lib.lpcnet_load_model(self._st, blob, len(blob)) != 0:
+            raise LPCNetError(f"lpcnet_load_model failed: {last_error()}")
+
+    def reset(self) -> None:
+        lib.lpcnet_reset(self._st)
+
+    def synthesize(self, features: np.ndarray, n: int = FRAME_SIZE) -> np.ndarray:
+        f = np.ascontiguousarray(features[:NB_FEATURES], np.float32)
+        out = np.zeros(n, np.int16)
+        lib.lpcnet_synthesize(self._st, f.ctypes.data, out.ctypes.data, n)
+        return out
+
+    def close(self) -> None:
+        if self._st:
+            lib.lpcnet_destroy(self._st)
+            self._st = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class LPCNetBatch:
+    """B independent streams on one MI355X (include/lpcnet_mi355x.h)."""
+
+    def __init__(self, nb_streams: int, device: int = 0, blob: bytes | None = None):
+        self._b = lib.lpcnet_batch_create(nb_streams, device)
+        if not self._b:
+            raise LPCNetError(f"lpcnet_batch_create failed: {last_error()}")
+        self.B = nb_streams
+        if blob is not None:
+            self.load_model(blob)
+
+    def load_model(self, blob: bytes) -> None:
+        if lib.lpcnet_batch_load_model(self._b, blob, len(blob)) != 0:
+            raise LPCNetError(f"lpcnet_batch_load_model failed: {last_error()}")
+
+    def info(self) -> ModelInfo:
+        mi = ModelInfo()
+        if lib.lpcnet_batch_model_info(self._b, C.byref(mi)) != 0:
+            raise LPCNetError("no model loaded")
+        return mi
+
+    def reset(self, stream: int | None = None) -> None:
+        if stream is None:
+            lib.lpcnet_batch_reset(self._b)
+        elif lib.lpcnet_batch_reset_stream(self._b, stream) != 0:
+            raise LPCNetError(last_error())
+
+    def synthesize(self, features: np.ndarray, n: int = FRAME_SIZE) -> np.ndarray:
+        """features [B, >=20] -> pcm [B, n] int16 (one frame per stream)."""
+        f = np.ascontiguousarray(np.asarray(features, np.float32)[:, :NB_FEATURES])
+        assert f.shape[0] == self.B
+        out = np.zeros((self.B, n), np.int16)
+        if lib.lpcnet_batch_synthesize(self._b, f.ctypes.data, out.ctypes.data, n) != 0:
+            raise LPCNetError(last_error())
+        return out
+
+    # -- device-resident path (benchmarks) ---------------------------------
+    def device_alloc(self, nbytes: int) -> int:
+        p = lib.lpcnet_batch_device_alloc(self._b, nbytes)
+        if not p:
+            raise LPCNetError(last_error())
+        return p
+
+    def device_free(self, p: int) -> None:
+        lib.lpcnet_batch_device_free(self._b, p)
+
+    def h2d(self, dst: int, arr: np.ndarray) -> None:
+        a = np.ascontiguousarray(arr)
+        if lib.lpcnet_batch_memcpy_h2d(self._b, dst, a.ctypes.data, a.nbytes) != 0:
+            raise LPCNetError(last_error())
+
+    def d2h(self, arr: np.ndarray, src: int) -> None:
+        if lib.lpcnet_batch_memcpy_d2h(self._b, arr.ctypes.data, src, arr.nbytes) != 0:
+            raise LPCNetError(last_error())
+
+    def synthesize_frames(self, h_features: np.ndarray, d_features: int, d_pcm: int, nframes: int,
+                          n: int = FRAME_SIZE) -> None:
+        """Enqueue ``nframes`` frames; h_features [nframes, B, 20] (host copy for LPC)."""
+        assert h_features.dtype == np.float32 and h_features.flags.c_contiguous
+        if lib.lpcnet_batch_synthesize_frames(self._b, h_features.ctypes.data, d_features, d_pcm, nframes, n) != 0:
+            raise LPCNetError(last_error())
+
+    def sync(self) -> None:
+        if lib.lpcnet_batch_sync(self._b) != 0:
+            raise LPCNetError(last_error())
+
+    def reset_timers(self, enable: bool = True) -> None:
+        lib.lpcnet_batch_reset_timers(self._b, 1 if enable else 0)
+
+    def kernel_ms(self, which: int = 0) -> tuple[float, int]:
+        n = C.c_int(0)
+        ms = lib.lpcnet_batch_kernel_ms(self._b, which, C.byref(n))
+        return ms, n.value
+
+    def set_trace(self, enable: bool = True) -> None:
+        lib.lpcnet_batch_set_trace(self._b, 1 if enable else 0)
+
+    def get_trace(self, n: int) -> tuple[np.ndarray, np.ndarray]:
+        logits = np.zeros((self.B, n, 8), np.float32)
+        exc = np.zeros((self.B, n), np.int32)
+        if lib.lpcnet_batch_get_trace(self._b, logits.ctypes.data, exc.ctypes.data) != 0:
+            raise LPCNetError("trace not enabled")
+        return logits, exc
+
+    def get_state(self, stream: int) -> dict:
+        a = np.zeros(1152, np.float32)
+        b = np.zeros(48, np.float32)
+        lpc = np.zeros(16, np.float32)
+        sa = np.zeros(384, np.float32)
+        sb = np.zeros(16, np.float32)
+        fc = C.c_int(0)
+        if lib.lpcnet_batch_get_state(self._b, stream, a.ctypes.data, b.ctypes.data, lpc.ctypes.data,
+                                      sa.ctypes.data, sb.ctypes.data, C.byref(fc)) != 0:
+            raise LPCNetError(last_error())
+        return {"gru_a_cond": a, "gru_b_cond": b, "lpc": lpc, "gru_a_state": sa, "gru_b_state": sb,
+                "frame_count": fc.value}
+
+    def close(self) -> None:
+        if self._b:
+            lib.lpcnet_batch_destroy(self._b)
+            self._b = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

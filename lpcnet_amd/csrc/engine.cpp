@@ -1,0 +1,988 @@
+/*
+ * engine.cpp -- host side of the MI355X LPCNet synthesis engine and the
+ * C-ABI entry points declared in include/lpcnet.h and include/lpcnet_mi355x.h.
+ *
+ * Responsibilities
+ *  - weight-blob ingest with the reference's validation rules
+ *    (parse_lpcnet_weights.c:36-113, 115-221) and re-tiling of the
+ *    block-sparse GRU weights into the sample kernel's LDS image;
+ *  - per-stream device state (lpcnet_private.h:28-48) and reset semantics
+ *    (lpcnet.c:174-182);
+ *  - per-frame scheduling: lpc_from_cepstrum on a host thread pool, pipelined
+ *    one frame ahead, then frame_kernel + sample_kernel on one HIP stream.
+ * Compile with -ffp-contract=off (the u-law / logit tables are computed here
+ * with the reference's exact expressions).
+ */
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "lpcnet_engine.h"
+#include "lpcnet_mi355x.h"
+
+using namespace lpcnet_mi355x;
+
+namespace {
+
+thread_local std::string g_err;
+void set_err(const std::string &e) { g_err = e; }
+
+const uint32_t kRcpTable[2048] = {
+#include "rcp_table_x86.inc"
+};
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) {                                                                \
+      set_err(std::string(#x) + ": " + hipGetErrorString(e_));                            \
+      return -1;                                                                           \
+    }                                                                                      \
+  } while (0)
+
+/* ---- host restatements of the scalar helpers used at init/reset -------- */
+
+/* common.h:18-33 + 47-58 */
+int host_lin2ulaw(float x)
+{
+  float scale = 255.f / 32768.f;
+  int s = x >= 0 ? 1 : -1;
+  x = fabsf(x);
+  float y = 1 + scale * x;
+  uint32_t bits;
+  memcpy(&bits, &y, 4);
+  int integer = (int)(bits >> 23) - 127;
+  bits -= (uint32_t)integer << 23;
+  float m;
+  memcpy(&m, &bits, 4);
+  float frac = m - 1.5f;
+  frac = -0.41445418f + frac * (0.95909232f + frac * (-0.33951290f + frac * 0.16541097f));
+  float l2 = 1 + integer + frac;
+  float u = (s * (128 * (0.69315f * l2) / 5.5451774445f));
+  u = 128 + u;
+  if (u < 0) u = 0;
+  if (u > 255) u = 255;
+  return (int)floor(.5 + u);
+}
+
+/* common.h:37-45 */
+float host_ulaw2lin(float u)
+{
+  float scale_1 = 32768.f / 255.f;
+  u = u - 128.f;
+  float s = u >= 0.f ? 1.f : -1.f;
+  u = fabsf(u);
+  return s * scale_1 * (exp(u / 128. * 5.5451774445f) - 1);
+}
+
+/* kiss99.c:32-81 */
+struct Kiss {
+  uint32_t z, w, jsr, jcong;
+  uint32_t next()
+  {
+    uint32_t znew = 36969 * (z & 0xFFFF) + (z >> 16);
+    uint32_t wnew = 18000 * (w & 0xFFFF) + (w >> 16);
+    uint32_t mwc = (znew << 16) + wnew;
+    uint32_t shr3 = jsr ^ (jsr << 13);
+    shr3 ^= shr3 >> 17;
+    shr3 ^= shr3 << 5;
+    uint32_t cong = 69069 * jcong + 1234567;
+    z = znew; w = wnew; jsr = shr3; jcong = cong;
+    return (mwc ^ cong) + shr3;
+  }
+  void srand(const unsigned char *d, int n)
+  {
+    int i;
+    z = 362436069; w = 521288629; jsr = 123456789; jcong = 380116160;
+    for (i = 3; i < n; i += 4) {
+      z ^= d[i - 3]; w ^= d[i - 2]; jsr ^= d[i - 1]; jcong ^= d[i];
+      next();
+    }
+    if (i - 3 < n) z ^= d[i - 3];
+    if (i - 2 < n) w ^= d[i - 2];
+    if (i - 1 < n) jsr ^= d[i - 1];
+    if (z == 0 || z == 0x9068FFFF) z++;
+    if (w == 0 || w == 0x464FFFFF) w++;
+    if (jsr == 0) jsr++;
+  }
+};
+
+/* ---- blob parsing (parse_lpcnet_weights.c:36-113) ---------------------- */
+struct Arr {
+  std::string name;
+  int size;
+  const unsigned char *data;
+};
+
+bool parse_blob(std::vector<Arr> &out, const unsigned char *data, int len)
+{
+  while (len > 0) {
+    if (len < 64) return false;
+    int size, block;
+    memcpy(&size, data + 12, 4);
+    memcpy(&block, data + 16, 4);
+    if (block < size || block > len - 64 || data[63] != 0 || size <= 0) return false;
+    out.push_back(Arr{std::string((const char *)data + 20), size, data + 64});
+    data += block + 64;
+    len -= block + 64;
+  }
+  return true;
+}
+
+const Arr *find(const std::vector<Arr> &l, const char *name)
+{
+  for (const Arr &a : l)
+    if (a.name == name) return &a;
+  return nullptr;
+}
+
+const void *find_check(const std::vector<Arr> &l, const char *name, int size)
+{
+  const Arr *a = find(l, name);
+  if (!a || a->size != size) {
+    set_err(std::string("weight array missing or mis-sized: ") + name);
+    return nullptr;
+  }
+  return a->data;
+}
+
+/* find_idx_check: per 8-row block [nb, pos...], pos 4-aligned and < nb_in-3 */
+bool parse_idx(const std::vector<Arr> &l, const char *name, int nb_in, int nb_out, std::vector<std::vector<int>> &blocks)
+{
+  const Arr *a = find(l, name);
+  if (!a) { set_err(std::string("missing ") + name); return false; }
+  std::vector<int> idx(a->size / 4);
+  memcpy(idx.data(), a->data, idx.size() * 4);
+  size_t p = 0;
+  int remain = (int)idx.size();
+  blocks.clear();
+  while (remain > 0) {
+    int nb = idx[p++];
+    if (nb < 0 || remain < nb + 1) { set_err(std::string("bad idx ") + name); return false; }
+    std::vector<int> pos(nb);
+    for (int k = 0; k < nb; k++) {
+      pos[k] = idx[p++];
+      if (pos[k] + 3 >= nb_in || (pos[k] & 3) || pos[k] < 0) { set_err(std::string("bad idx pos ") + name); return false; }
+    }
+    blocks.push_back(pos);
+    nb_out -= 8;
+    remain -= nb + 1;
+  }
+  if (nb_out != 0) { set_err(std::string("idx rows mismatch ") + name); return false; }
+  return true;
+}
+
+int total_blocks(const std::vector<std::vector<int>> &b)
+{
+  int t = 0;
+  for (auto &v : b) t += (int)v.size();
+  return t;
+}
+
+/* ---- small persistent thread pool for lpc_from_cepstrum ---------------- */
+class Pool {
+ public:
+  explicit Pool(int n)
+  {
+    for (int i = 0; i < n; i++) th_.emplace_back([this] { worker(); });
+  }
+  ~Pool()
+  {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  /* run f(chunk) for chunk in [0, n) on the workers and the calling thread */
+  void parallel_for(int n, const std::function<void(int)> &f)
+  {
+    if (n <= 0) return;
+    if (th_.empty() || n == 1) {
+      for (int i = 0; i < n; i++) f(i);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &f;
+      n_ = n;
+      next_.store(0);
+      left_.store(n);
+      gen_++;
+    }
+    cv_.notify_all();
+    drain();
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return left_.load() == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void drain()
+  {
+    for (;;) {
+      int i = next_.fetch_add(1);
+      if (i >= n_) break;
+      (*job_)(i);
+      if (left_.fetch_sub(1) == 1) {
+        std::lock_guard<std::mutex> g(m_);
+        done_.notify_all();
+      }
+    }
+  }
+  void worker()
+  {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || (gen_ != seen && job_ != nullptr); });
+        if (stop_) return;
+        seen = gen_;
+      }
+      drain();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)> *job_ = nullptr;
+  int n_ = 0;
+  std::atomic<int> next_{0}, left_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+int pool_threads()
+{
+  const char *e = getenv("LPCNET_LPC_THREADS");
+  if (e) return std::max(0, atoi(e));
+  int hc = (int)std::thread::hardware_concurrency();
+  return std::max(0, std::min(hc, 16) - 1);
+}
+
+}  // namespace
+
+/* ------------------------------------------------------------------------ */
+struct LPCNetBatch {
+  int device = 0;
+  int B = 0;
+  int S = 1;
+  hipStream_t stream = nullptr;
+  /* model */
+  bool have_model = false;
+  int variant = 0;
+  bool sat = false;
+  LPCNetModelInfo info{};
+  std::vector<void *> model_bufs;
+  FrameArgs fa{};
+  SampleArgs sa{};
+  int lds_bytes = 0;
+  /* streams */
+  StreamState *d_state = nullptr;
+  float *d_feat = nullptr;
+  short *d_pcm = nullptr;
+  float *d_lpc[2] = {nullptr, nullptr};
+  float *h_lpc[2] = {nullptr, nullptr};
+  hipEvent_t ev_lpc[2] = {nullptr, nullptr};
+  bool ev_lpc_used[2] = {false, false};
+  /* trace */
+  bool trace = false;
+  float *d_trace_logits = nullptr;
+  int *d_trace_exc = nullptr;
+  int trace_N = 0;
+  /* timing */
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pairs[2];
+  std::vector<hipEvent_t> ev_free;
+  Pool *pool = nullptr;
+
+  int set_device() { return hipSetDevice(device) == hipSuccess ? 0 : -1; }
+};
+
+namespace {
+
+template <typename T>
+T *dev_upload(LPCNetBatch *b, const void *src, size_t bytes)
+{
+  void *p = nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+  if (bytes && hipMemcpy(p, src, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  b->model_bufs.push_back(p);
+  return (T *)p;
+}
+
+void free_model(LPCNetBatch *b)
+{
+  for (void *p : b->model_bufs) (void)hipFree(p);
+  b->model_bufs.clear();
+  b->have_model = false;
+}
+
+hipEvent_t get_event(LPCNetBatch *b)
+{
+  if (!b->ev_free.empty()) {
+    hipEvent_t e = b->ev_free.back();
+    b->ev_free.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+/* pair sums of an int8 8x4 block that could saturate maddubs (x in [0,255]) */
+bool block_may_saturate(const int8_t *w)
+{
+  for (int r = 0; r < 8; r++)
+    for (int c = 0; c < 4; c += 2) {
+      int a = w[r * 4 + c], bb = w[r * 4 + c + 1];
+      int pos = std::max(a, 0) + std::max(bb, 0), neg = std::max(-a, 0) + std::max(-bb, 0);
+      if (255 * pos > 32767 || 255 * neg > 32768) return true;
+    }
+  return false;
+}
+
+int load_model(LPCNetBatch *b, const unsigned char *data, int len)
+{
+  std::vector<Arr> L;
+  if (!data || len <= 0 || !parse_blob(L, data, len)) {
+    set_err("malformed weight blob");
+    return -1;
+  }
+  std::vector<std::vector<int>> ga_blocks, gb_blocks;
+  if (!parse_idx(L, "sparse_gru_a_recurrent_weights_idx", NA, GA_ROWS, ga_blocks)) return -1;
+  if (!parse_idx(L, "gru_b_weights_idx", NA, GB_ROWS, gb_blocks)) return -1;
+  const int nba = total_blocks(ga_blocks), nbb = total_blocks(gb_blocks);
+  const Arr *gaw = find(L, "sparse_gru_a_recurrent_weights");
+  if (!gaw) { set_err("missing sparse_gru_a_recurrent_weights"); return -1; }
+  int variant;
+  if (gaw->size == 32 * nba) variant = LPCNET_VARIANT_INT8;
+  else if (gaw->size == 32 * nba * 4) variant = LPCNET_VARIANT_FP32;
+  else { set_err("sparse_gru_a_recurrent_weights size matches neither int8 nor fp32"); return -1; }
+  const int q = variant == LPCNET_VARIANT_FP32 ? 4 : 1;
+
+#define F(var, name, cnt) const float *var = (const float *)find_check(L, name, (cnt)*4); if (!var) return -1
+  F(conv1_w, "feature_conv1_weights", 3 * FIN * COND);
+  F(conv1_b, "feature_conv1_bias", COND);
+  F(conv2_w, "feature_conv2_weights", 3 * COND * COND);
+  F(conv2_b, "feature_conv2_bias", COND);
+  F(dense1_w, "feature_dense1_weights", COND * COND);
+  F(dense1_b, "feature_dense1_bias", COND);
+  F(dense2_w, "feature_dense2_weights", COND * COND);
+  F(dense2_b, "feature_dense2_bias", COND);
+  F(gadf_w, "gru_a_dense_feature_weights", COND * GA_ROWS);
+  F(gadf_b, "gru_a_dense_feature_bias", GA_ROWS);
+  F(gbdf_w, "gru_b_dense_feature_weights", COND * GB_ROWS);
+  F(gbdf_b, "gru_b_dense_feature_bias", GB_ROWS);
+  F(embed_pitch, "embed_pitch_weights", 256 * EP);
+  F(embed_sig, "embed_sig_weights", 256 * 128);
+  F(emb_sig, "gru_a_embed_sig_weights", 256 * GA_ROWS);
+  F(emb_pred, "gru_a_embed_pred_weights", 256 * GA_ROWS);
+  F(emb_exc, "gru_a_embed_exc_weights", 256 * GA_ROWS);
+  F(ga_bias, "sparse_gru_a_bias", 6 * NA);
+  F(ga_subias, "sparse_gru_a_subias", 6 * NA);
+  F(ga_diag, "sparse_gru_a_recurrent_weights_diag", 3 * NA);
+  F(gb_bias, "gru_b_bias", 6 * NB);
+  F(gb_subias, "gru_b_subias", 6 * NB);
+  F(fc_b, "dual_fc_bias", 512);
+  F(fc_w, "dual_fc_weights", 256 * 32);
+  F(fc_f, "dual_fc_factor", 512);
+#undef F
+  (void)embed_sig;
+  const void *gbw = find_check(L, "gru_b_weights", 32 * nbb * q);
+  const void *gbrec = find_check(L, "gru_b_recurrent_weights", 3 * NB * NB * q);
+  if (!gbw || !gbrec) return -1;
+
+  /* ---- derived host layouts ---- */
+  const bool int8 = variant == LPCNET_VARIANT_INT8;
+  bool sat = false;
+  if (int8) {
+    const int8_t *wa = (const int8_t *)gaw->data, *wb = (const int8_t *)gbw, *wr = (const int8_t *)gbrec;
+    for (int k = 0; k < nba && !sat; k++) sat |= block_may_saturate(wa + 32 * k);
+    for (int k = 0; k < nbb && !sat; k++) sat |= block_may_saturate(wb + 32 * k);
+    for (int k = 0; k < 3 * NB * NB / 32 && !sat; k++) sat |= block_may_saturate(wr + 32 * k);
+  }
+  const float *abias = int8 ? ga_subias : ga_bias; /* USE_SU_BIAS only with DOT_PROD */
+  const float *bbias = int8 ? gb_subias : gb_bias;
+  std::vector<float> ga_par(6 * NA), gb_par(2 * GB_ROWS);
+  std::vector<int> ga_wsum(3 * NA, 0), gb_wsum(2 * GB_ROWS, 0);
+  for (int g = 0; g < 3; g++)
+    for (int i = 0; i < NA; i++) {
+      ga_par[g * NA + i] = abias[3 * NA + g * NA + i];
+      ga_par[(3 + g) * NA + i] = ga_diag[g * NA + i];
+    }
+  for (int r = 0; r < GB_ROWS; r++) {
+    gb_par[r] = bbias[r];
+    gb_par[GB_ROWS + r] = bbias[GB_ROWS + r];
+  }
+
+  /* per-block offsets into the blob weights */
+  std::vector<int> ga_first(ga_blocks.size() + 1, 0), gb_first(gb_blocks.size() + 1, 0);
+  for (size_t r = 0; r < ga_blocks.size(); r++) ga_first[r + 1] = ga_first[r] + (int)ga_blocks[r].size();
+  for (size_t r = 0; r < gb_blocks.size(); r++) gb_first[r + 1] = gb_first[r] + (int)gb_blocks[r].size();
+
+  if (int8 && !sat) {
+    const int8_t *wa = (const int8_t *)gaw->data, *wb = (const int8_t *)gbw, *wr = (const int8_t *)gbrec;
+    for (int rb = 0; rb < GA_ROWS / 8; rb++)
+      for (int k = ga_first[rb]; k < ga_first[rb + 1]; k++)
+        for (int r = 0; r < 8; r++)
+          for (int c = 0; c < 4; c++) ga_wsum[rb * 8 + r] += 128 * wa[32 * k + r * 4 + c];
+    for (int rb = 0; rb < GB_ROWS / 8; rb++)
+      for (int k = gb_first[rb]; k < gb_first[rb + 1]; k++)
+        for (int r = 0; r < 8; r++)
+          for (int c = 0; c < 4; c++) gb_wsum[rb * 8 + r] += 128 * wb[32 * k + r * 4 + c];
+    for (int rb = 0; rb < GB_ROWS / 8; rb++)
+      for (int cb = 0; cb < NB / 4; cb++)
+        for (int r = 0; r < 8; r++)
+          for (int c = 0; c < 4; c++) gb_wsum[GB_ROWS + rb * 8 + r] += 128 * wr[32 * (rb * (NB / 4) + cb) + r * 4 + c];
+  }
+
+  /* ---- LDS image ---- */
+  std::vector<unsigned char> img(IMG_VAR, 0);
+  memcpy(&img[IMG_RCP], kRcpTable, sizeof(kRcpTable));
+  for (int i = 0; i < 256; i++) {
+    float u = host_ulaw2lin((float)i);
+    memcpy(&img[IMG_ULAW + 4 * i], &u, 4);
+    /* lpcnet.c:188-191 */
+    float prob = .025f + .95f * i / 255.f;
+    float lg = (float)-log((double)((1 - prob) / prob)); /* C double log, not logf */
+    memcpy(&img[IMG_LOGIT + 4 * i], &lg, 4);
+  }
+  memcpy(&img[IMG_FCW], fc_w, 256 * 32 * 4);
+  memcpy(&img[IMG_FCB], fc_b, 512 * 4);
+  memcpy(&img[IMG_FCF], fc_f, 512 * 4);
+  auto align16 = [&]() { img.resize((img.size() + 15) / 16 * 16, 0); };
+  auto put = [&](const void *p, size_t n) -> size_t {
+    align16();
+    size_t off = img.size();
+    img.resize(off + n);
+    memcpy(&img[off], p, n);
+    return off;
+  };
+  SampleArgs &sa = b->sa;
+  memset(&sa, 0, sizeof(sa));
+  std::vector<float4> ga_wf, gb_wf_unused;
+  if (int8) sa.gb_rec_off = (int)put(gbrec, 3 * NB * NB);
+  /* GRU_B input blocks: [rb][k][row] (u32 int8 row quads | float4 fp32 rows) */
+  for (int rb = 0; rb < GB_ROWS / 8; rb++) {
+    int nb = (int)gb_blocks[rb].size();
+    sa.gb_nb[rb] = nb;
+    if (int8) {
+      std::vector<uint32_t> w(nb * 8);
+      for (int k = 0; k < nb; k++)
+        for (int r = 0; r < 8; r++) memcpy(&w[k * 8 + r], (const int8_t *)gbw + 32 * (gb_first[rb] + k) + 4 * r, 4);
+      sa.gb_woff[rb] = (int)(put(w.data(), w.size() * 4) / 4);
+    } else {
+      std::vector<float> w(nb * 8 * 4);
+      const float *src = (const float *)gbw;
+      for (int k = 0; k < nb; k++)
+        for (int r = 0; r < 8; r++)
+          for (int c = 0; c < 4; c++) w[(k * 8 + r) * 4 + c] = src[32 * (gb_first[rb] + k) + c * 8 + r];
+      sa.gb_woff[rb] = (int)(put(w.data(), w.size() * 4) / 4);
+    }
+    std::vector<uint16_t> cbs(nb);
+    for (int k = 0; k < nb; k++) cbs[k] = (uint16_t)(gb_blocks[rb][k] / 4);
+    sa.gb_coff[rb] = (int)(put(cbs.data(), cbs.size() * 2) / 2);
+  }
+  /* GRU_A blocks: per (wave, gate) chunk [k][64 lanes], lane = 8*(row block in wave) + row */
+  size_t ga_slots = 0;
+  for (int w = 0; w < SAMPLE_WAVES; w++)
+    for (int g = 0; g < 3; g++) {
+      int K = 0;
+      for (int j = 0; j < 8; j++) K = std::max(K, (int)ga_blocks[g * (NA / 8) + w * 8 + j].size());
+      sa.ga_K[w][g] = K;
+      std::vector<uint16_t> cbs(K * 8, int8 ? 0 : 0xFFFF);
+      std::vector<uint32_t> wq(int8 ? K * 64 : 0, 0);
+      size_t fbase = ga_wf.size();
+      if (!int8) ga_wf.resize(fbase + (size_t)K * 64, make_float4(0, 0, 0, 0));
+      for (int j = 0; j < 8; j++) {
+        int rb = g * (NA / 8) + w * 8 + j;
+        for (int k = 0; k < (int)ga_blocks[rb].size(); k++) {
+          cbs[k * 8 + j] = (uint16_t)(ga_blocks[rb][k] / 4);
+          for (int r = 0; r < 8; r++) {
+            int blk = ga_first[rb] + k;
+            if (int8) {
+              memcpy(&wq[k * 64 + j * 8 + r], (const int8_t *)gaw->data + 32 * blk + 4 * r, 4);
+            } else {
+              const float *src = (const float *)gaw->data + 32 * blk;
+              ga_wf[fbase + k * 64 + j * 8 + r] = make_float4(src[0 * 8 + r], src[1 * 8 + r], src[2 * 8 + r], src[3 * 8 + r]);
+            }
+          }
+        }
+      }
+      if (int8) sa.ga_woff[w][g] = (int)(put(wq.data(), wq.size() * 4) / 4);
+      else sa.ga_woff[w][g] = (int)fbase;
+      sa.ga_coff[w][g] = (int)(put(cbs.data(), cbs.size() * 2) / 2);
+      ga_slots += K;
+    }
+  align16();
+
+  /* choose streams per workgroup and check the LDS budget */
+  int S = b->B >= 1024 ? 4 : (b->B >= 512 ? 2 : 1);
+  int lds = sample_lds_bytes(S, variant, (int)img.size());
+  while (lds > 160 * 1024 && S > 1) {
+    S /= 2;
+    lds = sample_lds_bytes(S, variant, (int)img.size());
+  }
+  if (lds > 160 * 1024) {
+    set_err("model does not fit the 160 KiB LDS budget");
+    return -1;
+  }
+
+  if (b->set_device()) { set_err("hipSetDevice failed"); return -1; }
+  free_model(b);
+  FrameArgs &fa = b->fa;
+#define UP(dst, src, n) if (!(dst = dev_upload<std::remove_const<std::remove_pointer<decltype(dst)>::type>::type>(b, src, n))) { set_err("device upload failed"); free_model(b); return -1; }
+  UP(fa.conv1_w, conv1_w, 3 * FIN * COND * 4);
+  UP(fa.conv1_b, conv1_b, COND * 4);
+  UP(fa.conv2_w, conv2_w, 3 * COND * COND * 4);
+  UP(fa.conv2_b, conv2_b, COND * 4);
+  UP(fa.dense1_w, dense1_w, COND * COND * 4);
+  UP(fa.dense1_b, dense1_b, COND * 4);
+  UP(fa.dense2_w, dense2_w, COND * COND * 4);
+  UP(fa.dense2_b, dense2_b, COND * 4);
+  UP(fa.gadf_w, gadf_w, COND * GA_ROWS * 4);
+  UP(fa.gadf_b, gadf_b, GA_ROWS * 4);
+  UP(fa.gbdf_w, gbdf_w, COND * GB_ROWS * 4);
+  UP(fa.gbdf_b, gbdf_b, GB_ROWS * 4);
+  UP(fa.embed_pitch, embed_pitch, 256 * EP * 4);
+  UP(fa.rcp, kRcpTable, sizeof(kRcpTable));
+  UP(sa.emb_sig, emb_sig, 256 * GA_ROWS * 4);
+  UP(sa.emb_pred, emb_pred, 256 * GA_ROWS * 4);
+  UP(sa.emb_exc, emb_exc, 256 * GA_ROWS * 4);
+  UP(sa.ga_par, ga_par.data(), ga_par.size() * 4);
+  UP(sa.ga_wsum, ga_wsum.data(), ga_wsum.size() * 4);
+  UP(sa.gb_par, gb_par.data(), gb_par.size() * 4);
+  UP(sa.gb_wsum, gb_wsum.data(), gb_wsum.size() * 4);
+  UP(sa.image, img.data(), img.size());
+  if (!int8) {
+    UP(sa.ga_wf, ga_wf.data(), ga_wf.size() * sizeof(float4));
+    UP(sa.gb_recf, gbrec, 3 * NB * NB * 4);
+  }
+#undef UP
+  sa.image_bytes = (int)img.size();
+  b->variant = variant;
+  b->sat = sat;
+  b->S = S;
+  b->lds_bytes = lds;
+  b->have_model = true;
+
+  /* algorithmic work, recomputed from the loaded index */
+  LPCNetModelInfo &in = b->info;
+  in.variant = variant;
+  in.gru_a_blocks = nba;
+  in.gru_b_blocks = nbb;
+  in.may_saturate = sat ? 1 : 0;
+  double frame_w = (3.0 * FIN * COND + 3.0 * COND * COND + 2.0 * COND * COND + COND * GA_ROWS + COND * GB_ROWS) * 4 +
+                   (2.0 * COND + 2 * COND + GA_ROWS + GB_ROWS) * 4 + EP * 4;
+  double wbytes = int8 ? 1 : 4;
+  in.bytes_shared_per_frame = frame_w;
+  in.bytes_shared_per_sample = 32.0 * nba * wbytes + 4.0 * (nba + GA_ROWS / 8) /* idx */ + 6.0 * NA * 4 /* bias+diag */ +
+                               32.0 * nbb * wbytes + 4.0 * (nbb + GB_ROWS / 8) + 3.0 * NB * NB * wbytes + 2.0 * GB_ROWS * 4;
+  in.bytes_per_stream_sample = 3.0 * GA_ROWS * 4 /* embedding rows */ + 8 * (32 + 2 * 4 + 2 * 4) /* dual_fc path */ + 2;
+  in.ops_per_sample = 2.0 * (32.0 * nba + 32.0 * nbb + 3 * NB * NB + 8 * 2 * NB + NLPC) +
+                      2.0 * (3.0 * FIN * COND + 3.0 * COND * COND + 2.0 * COND * COND + COND * GA_ROWS + COND * GB_ROWS) / FRAME;
+  (void)ga_slots;
+  return 0;
+}
+
+void host_reset_state(StreamState &s)
+{
+  memset(&s, 0, sizeof(s));
+  s.last_exc = host_lin2ulaw(0.f);
+  Kiss k;
+  k.srand((const unsigned char *)"LPCNet", 6);
+  s.rng[0] = k.z; s.rng[1] = k.w; s.rng[2] = k.jsr; s.rng[3] = k.jcong;
+}
+
+int ensure_trace(LPCNetBatch *b, int N)
+{
+  if (!b->trace) {
+    b->sa.trace_logits = nullptr;
+    b->sa.trace_exc = nullptr;
+    return 0;
+  }
+  if (!b->d_trace_logits) {
+    HIPCHK(hipMalloc(&b->d_trace_logits, (size_t)b->B * FRAME * 8 * 4));
+    HIPCHK(hipMalloc(&b->d_trace_exc, (size_t)b->B * FRAME * 4));
+  }
+  b->sa.trace_logits = b->d_trace_logits;
+  b->sa.trace_exc = b->d_trace_exc;
+  b->trace_N = N;
+  return 0;
+}
+
+int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lpc, short *d_pcm, int N)
+{
+  FrameArgs fa = b->fa;
+  fa.st = b->d_state;
+  fa.nstreams = b->B;
+  fa.features = d_features;
+  fa.lpc_new = d_lpc;
+  SampleArgs sa = b->sa;
+  sa.st = b->d_state;
+  sa.nstreams = b->B;
+  sa.N = N;
+  sa.pcm = d_pcm;
+  hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
+  if (b->timing)
+    for (int i = 0; i < 4; i++) e[i] = get_event(b);
+  if (e[0]) HIPCHK(hipEventRecord(e[0], b->stream));
+  if (launch_frame(fa, b->stream)) { set_err("frame kernel launch failed"); return -1; }
+  if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
+  if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
+  if (launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->lds_bytes, b->stream)) {
+    set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return -1;
+  }
+  if (e[3]) HIPCHK(hipEventRecord(e[3], b->stream));
+  if (b->timing) {
+    b->ev_pairs[1].push_back(e[0]);
+    b->ev_pairs[1].push_back(e[1]);
+    b->ev_pairs[0].push_back(e[2]);
+    b->ev_pairs[0].push_back(e[3]);
+  }
+  return 0;
+}
+
+void compute_lpc(LPCNetBatch *b, const float *feat, int feat_stride, float *out)
+{
+  const int chunk = 32;
+  int nchunks = (b->B + chunk - 1) / chunk;
+  b->pool->parallel_for(nchunks, [&](int c) {
+    int e = std::min(b->B, (c + 1) * chunk);
+    for (int s = c * chunk; s < e; s++) lpc_from_cepstrum_host(out + (size_t)s * NLPC, feat + (size_t)s * feat_stride);
+  });
+}
+
+}  // namespace
+
+/* ======================================================================== */
+/* batch API                                                                 */
+
+extern "C" {
+
+LPCNET_EXPORT const char *lpcnet_mi355x_last_error(void) { return g_err.c_str(); }
+
+LPCNET_EXPORT int lpcnet_mi355x_device_count(void)
+{
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+LPCNET_EXPORT const uint32_t *lpcnet_mi355x_rcp_table(void) { return kRcpTable; }
+
+LPCNET_EXPORT float lpcnet_mi355x_lpc_from_cepstrum(float *lpc, const float *cepstrum)
+{
+  return lpc_from_cepstrum_host(lpc, cepstrum);
+}
+
+LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
+{
+  if (nb_streams < 1) { set_err("nb_streams < 1"); return nullptr; }
+  int ndev = lpcnet_mi355x_device_count();
+  if (device < 0 || device >= ndev) { set_err("no such HIP device"); return nullptr; }
+  LPCNetBatch *b = new LPCNetBatch();
+  b->device = device;
+  b->B = nb_streams;
+  bool ok = b->set_device() == 0;
+  ok = ok && hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) == hipSuccess;
+  ok = ok && hipMalloc(&b->d_state, sizeof(StreamState) * (size_t)nb_streams) == hipSuccess;
+  ok = ok && hipMalloc(&b->d_feat, sizeof(float) * NF * (size_t)nb_streams) == hipSuccess;
+  ok = ok && hipMalloc(&b->d_pcm, sizeof(short) * FRAME * (size_t)nb_streams) == hipSuccess;
+  for (int i = 0; i < 2 && ok; i++) {
+    ok = ok && hipMalloc(&b->d_lpc[i], sizeof(float) * NLPC * (size_t)nb_streams) == hipSuccess;
+    ok = ok && hipHostMalloc(&b->h_lpc[i], sizeof(float) * NLPC * (size_t)nb_streams, hipHostMallocDefault) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&b->ev_lpc[i], hipEventDisableTiming) == hipSuccess;
+  }
+  if (!ok) {
+    set_err("device allocation failed");
+    lpcnet_batch_destroy(b);
+    return nullptr;
+  }
+  b->pool = new Pool(std::min(pool_threads(), std::max(0, nb_streams / 32)));
+  lpcnet_batch_reset(b);
+  return b;
+}
+
+LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
+{
+  if (!b) return;
+  b->set_device();
+  if (b->stream) (void)hipStreamSynchronize(b->stream);
+  free_model(b);
+  (void)hipFree(b->d_state);
+  (void)hipFree(b->d_feat);
+  (void)hipFree(b->d_pcm);
+  (void)hipFree(b->d_trace_logits);
+  (void)hipFree(b->d_trace_exc);
+  for (int i = 0; i < 2; i++) {
+    (void)hipFree(b->d_lpc[i]);
+    if (b->h_lpc[i]) (void)hipHostFree(b->h_lpc[i]);
+    if (b->ev_lpc[i]) (void)hipEventDestroy(b->ev_lpc[i]);
+  }
+  for (int k = 0; k < 2; k++)
+    for (hipEvent_t e : b->ev_pairs[k]) (void)hipEventDestroy(e);
+  for (hipEvent_t e : b->ev_free) (void)hipEventDestroy(e);
+  if (b->stream) (void)hipStreamDestroy(b->stream);
+  delete b->pool;
+  delete b;
+}
+
+LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *data, int len)
+{
+  if (!b) return -1;
+  if (b->set_device()) return -1;
+  (void)hipStreamSynchronize(b->stream);
+  return load_model(b, data, len);
+}
+
+LPCNET_EXPORT int lpcnet_batch_model_info(const LPCNetBatch *b, LPCNetModelInfo *info)
+{
+  if (!b || !b->have_model || !info) return -1;
+  *info = b->info;
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_nb_streams(const LPCNetBatch *b) { return b ? b->B : 0; }
+
+LPCNET_EXPORT int lpcnet_batch_reset_stream(LPCNetBatch *b, int stream)
+{
+  if (!b || stream < 0 || stream >= b->B) return -1;
+  if (b->set_device()) return -1;
+  StreamState s;
+  host_reset_state(s);
+  HIPCHK(hipMemcpyAsync(&b->d_state[stream], &s, sizeof(s), hipMemcpyHostToDevice, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
+LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b)
+{
+  if (!b || b->set_device()) return;
+  std::vector<StreamState> v(b->B);
+  host_reset_state(v[0]);
+  for (int i = 1; i < b->B; i++) v[i] = v[0];
+  (void)hipMemcpyAsync(b->d_state, v.data(), sizeof(StreamState) * v.size(), hipMemcpyHostToDevice, b->stream);
+  (void)hipStreamSynchronize(b->stream);
+}
+
+LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features, short *pcm, int N)
+{
+  if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
+  if (N < 0 || N > FRAME || !features || !pcm) { set_err("bad arguments"); return -1; }
+  if (b->set_device()) return -1;
+  if (ensure_trace(b, N)) return -1;
+  compute_lpc(b, features, NF, b->h_lpc[0]);
+  HIPCHK(hipMemcpyAsync(b->d_lpc[0], b->h_lpc[0], sizeof(float) * NLPC * b->B, hipMemcpyHostToDevice, b->stream));
+  HIPCHK(hipMemcpyAsync(b->d_feat, features, sizeof(float) * NF * b->B, hipMemcpyHostToDevice, b->stream));
+  if (launch_frame_step(b, b->d_feat, b->d_lpc[0], b->d_pcm, N)) return -1;
+  if (N > 0) HIPCHK(hipMemcpyAsync(pcm, b->d_pcm, sizeof(short) * N * b->B, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_features, const float *d_features,
+                                                 short *d_pcm, int nframes, int N)
+{
+  if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
+  if (N < 0 || N > FRAME || nframes < 0 || !h_features || !d_features || !d_pcm) { set_err("bad arguments"); return -1; }
+  if (b->set_device()) return -1;
+  if (ensure_trace(b, N)) return -1;
+  const size_t fstride = (size_t)b->B * NF;
+  if (nframes == 0) return 0;
+  int slot = 0;
+  auto wait_slot = [&](int sl) -> int {
+    if (b->ev_lpc_used[sl]) HIPCHK(hipEventSynchronize(b->ev_lpc[sl]));
+    return 0;
+  };
+  if (wait_slot(0)) return -1;
+  compute_lpc(b, h_features, NF, b->h_lpc[0]);
+  for (int f = 0; f < nframes; f++) {
+    slot = f & 1;
+    HIPCHK(hipMemcpyAsync(b->d_lpc[slot], b->h_lpc[slot], sizeof(float) * NLPC * b->B, hipMemcpyHostToDevice, b->stream));
+    HIPCHK(hipEventRecord(b->ev_lpc[slot], b->stream));
+    b->ev_lpc_used[slot] = true;
+    if (launch_frame_step(b, d_features + f * fstride, b->d_lpc[slot], d_pcm + (size_t)f * b->B * N, N)) return -1;
+    if (f + 1 < nframes) {
+      /* host LPC of the next frame overlaps this frame's kernels */
+      if (wait_slot(slot ^ 1)) return -1;
+      compute_lpc(b, h_features + (f + 1) * fstride, NF, b->h_lpc[slot ^ 1]);
+    }
+  }
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_sync(LPCNetBatch *b)
+{
+  if (!b || b->set_device()) return -1;
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
+LPCNET_EXPORT void *lpcnet_batch_device_alloc(LPCNetBatch *b, size_t bytes)
+{
+  if (!b || b->set_device()) return nullptr;
+  void *p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) { set_err("hipMalloc failed"); return nullptr; }
+  return p;
+}
+
+LPCNET_EXPORT int lpcnet_batch_device_free(LPCNetBatch *b, void *p)
+{
+  if (!b || b->set_device()) return -1;
+  HIPCHK(hipFree(p));
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_memcpy_h2d(LPCNetBatch *b, void *dst, const void *src, size_t bytes)
+{
+  if (!b || b->set_device()) return -1;
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_memcpy_d2h(LPCNetBatch *b, void *dst, const void *src, size_t bytes)
+{
+  if (!b || b->set_device()) return -1;
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
+LPCNET_EXPORT void lpcnet_batch_reset_timers(LPCNetBatch *b, int enable)
+{
+  if (!b) return;
+  b->set_device();
+  (void)hipStreamSynchronize(b->stream);
+  for (int k = 0; k < 2; k++) {
+    for (hipEvent_t e : b->ev_pairs[k]) b->ev_free.push_back(e);
+    b->ev_pairs[k].clear();
+  }
+  b->timing = enable != 0;
+}
+
+LPCNET_EXPORT double lpcnet_batch_kernel_ms(LPCNetBatch *b, int which, int *launches)
+{
+  if (!b || which < 0 || which > 1) return -1;
+  b->set_device();
+  (void)hipStreamSynchronize(b->stream);
+  double tot = 0;
+  const std::vector<hipEvent_t> &v = b->ev_pairs[which];
+  for (size_t i = 0; i + 1 < v.size(); i += 2) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, v[i], v[i + 1]) == hipSuccess) tot += ms;
+  }
+  if (launches) *launches = (int)(v.size() / 2);
+  return tot;
+}
+
+LPCNET_EXPORT int lpcnet_batch_set_trace(LPCNetBatch *b, int enable)
+{
+  if (!b) return -1;
+  b->trace = enable != 0;
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_get_trace(LPCNetBatch *b, float *logits, int *exc)
+{
+  if (!b || !b->trace || !b->d_trace_logits || b->set_device()) return -1;
+  HIPCHK(hipStreamSynchronize(b->stream));
+  int N = b->trace_N;
+  if (logits) HIPCHK(hipMemcpy(logits, b->d_trace_logits, sizeof(float) * 8 * N * b->B, hipMemcpyDeviceToHost));
+  if (exc) HIPCHK(hipMemcpy(exc, b->d_trace_exc, sizeof(int) * N * b->B, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_get_state(LPCNetBatch *b, int stream, float *gru_a_cond, float *gru_b_cond, float *lpc,
+                                         float *gru_a_state, float *gru_b_state, int *frame_count)
+{
+  if (!b || stream < 0 || stream >= b->B || b->set_device()) return -1;
+  StreamState s;
+  HIPCHK(hipStreamSynchronize(b->stream));
+  HIPCHK(hipMemcpy(&s, &b->d_state[stream], sizeof(s), hipMemcpyDeviceToHost));
+  if (gru_a_cond) memcpy(gru_a_cond, s.gru_a_cond, sizeof(s.gru_a_cond));
+  if (gru_b_cond) memcpy(gru_b_cond, s.gru_b_cond, sizeof(s.gru_b_cond));
+  if (lpc) memcpy(lpc, s.lpc, sizeof(s.lpc));
+  if (gru_a_state) memcpy(gru_a_state, s.gru_a_state, sizeof(s.gru_a_state));
+  if (gru_b_state) memcpy(gru_b_state, s.gru_b_state, sizeof(s.gru_b_state));
+  if (frame_count) *frame_count = s.frame_count;
+  return 0;
+}
+
+/* ======================================================================== */
+/* drop-in single-stream API (include/lpcnet.h)                              */
+
+struct LPCNetState {
+  uint32_t magic;
+  int device;
+  LPCNetBatch *batch;
+};
+static const uint32_t kMagic = 0x4c50434eu; /* "LPCN" */
+
+LPCNET_EXPORT int lpcnet_get_size(void) { return (int)sizeof(LPCNetState); }
+
+LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
+{
+  st->magic = kMagic;
+  const char *d = getenv("LPCNET_DEVICE");
+  st->device = d ? atoi(d) : 0;
+  st->batch = nullptr;
+  return 0;
+}
+
+LPCNET_EXPORT LPCNetState *lpcnet_create(void)
+{
+  LPCNetState *st = (LPCNetState *)calloc(1, sizeof(LPCNetState));
+  if (st) lpcnet_init(st);
+  return st;
+}
+
+LPCNET_EXPORT void lpcnet_destroy(LPCNetState *st)
+{
+  if (!st) return;
+  if (st->magic == kMagic && st->batch) lpcnet_batch_destroy(st->batch);
+  free(st);
+}
+
+LPCNET_EXPORT void lpcnet_reset(LPCNetState *st)
+{
+  if (st && st->batch) lpcnet_batch_reset(st->batch);
+}
+
+LPCNET_EXPORT int lpcnet_load_model(LPCNetState *st, const unsigned char *data, int len)
+{
+  if (!st) return -1;
+  if (!st->batch) {
+    st->batch = lpcnet_batch_create(1, st->device);
+    if (!st->batch) return -1;
+  }
+  return lpcnet_batch_load_model(st->batch, data, len) == 0 ? 0 : -1;
+}
+
+LPCNET_EXPORT void lpcnet_synthesize(LPCNetState *st, const float *features, short *output, int N)
+{
+  if (!st || !st->batch || lpcnet_batch_synthesize(st->batch, features, output, N) != 0) {
+    if (output && N > 0) memset(output, 0, sizeof(short) * N);
+  }
+}
+
+}  // extern "C"

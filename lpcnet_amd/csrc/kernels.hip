@@ -1,0 +1,765 @@
+/*
+ * kernels.hip -- CDNA4 (gfx950) kernels of the LPCNet synthesis engine.
+ *
+ * Numerics contract: every float operation reproduces
+ * the reference x86 AVX2 build bit for bit.  This file MUST be compiled with
+ * -ffp-contract=off; explicit __builtin_fmaf appears exactly where the
+ * reference issues _mm256_fmadd_ps, and _mm256_rcp_ps is emulated through the
+ * 2048-entry table (rcp_x86 below).
+ *
+ * Kernels
+ *   frame_kernel  -- run_frame_network (lpcnet.c:82-120) for 4 streams per
+ *                    256-thread workgroup: conv1d x2, dense x2, the GRU_A/GRU_B
+ *                    conditioning projections and the LPC ring.
+ *   sample_kernel -- lpcnet_synthesize_tail_impl (lpcnet.c:235-271) for one
+ *                    frame: S streams per 384-thread workgroup, persistent over
+ *                    the N samples.  Thread i owns GRU_A unit i (its z, r and h
+ *                    rows) for all S streams; wave w owns GRU_B row block w;
+ *                    wave s runs stream s's GRU_B update, dual-FC tree sampling
+ *                    and the LPC/de-emphasis output.  GRU_A/GRU_B int8 blocks,
+ *                    dual_fc weights and all tables live in LDS for the whole
+ *                    frame; three workgroup barriers per sample.
+ */
+#include <hip/hip_runtime.h>
+
+#include "lpcnet_engine.h"
+
+namespace lpcnet_mi355x {
+
+/* ------------------------------------------------------------------------ */
+/* numerics helpers                                                          */
+
+__device__ __forceinline__ float rcp_x86(float x, const uint32_t *tab)
+{
+  /* _mm256_rcp_ps: table of the top 11 mantissa bits, exponent invariant,
+   * denormal results flushed to zero (probe: SURVEY.md 7 hard part 1). */
+  uint32_t u = __float_as_uint(x), sign = u & 0x80000000u;
+  int e = (int)((u >> 23) & 0xff);
+  uint32_t t = tab[(u >> 12) & 0x7ff];
+  int te = (int)((t >> 23) & 0xff) - (e - 127);
+  uint32_t r = te < 1 ? sign : (sign | (t & 0x007fffffu) | ((uint32_t)te << 23));
+  r = e == 0 ? (sign | 0x7f800000u) : r;
+  r = e == 255 ? ((u & 0x7fffffu) ? (u | 0x00400000u) : sign) : r;
+  return __uint_as_float(r);
+}
+
+/* _mm256_min_ps / _mm256_max_ps return the second operand when unordered */
+__device__ __forceinline__ float mm_min(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float mm_max(float a, float b) { return a > b ? a : b; }
+
+/* vec_avx.h:393-411 tanh8_approx */
+__device__ __forceinline__ float tanh_x86(float X, const uint32_t *tab)
+{
+  float X2 = X * X;
+  float num = __builtin_fmaf(__builtin_fmaf(0.60863042f, X2, 96.39235687f), X2, 952.52801514f);
+  float den = __builtin_fmaf(__builtin_fmaf(11.88600922f, X2, 413.36801147f), X2, 952.72399902f);
+  num = num * X;
+  den = rcp_x86(den, tab);
+  num = num * den;
+  return mm_max(-1.f, mm_min(1.f, num));
+}
+
+/* vec_avx.h:421-440 sigmoid8_approx */
+__device__ __forceinline__ float sigmoid_x86(float X, const uint32_t *tab)
+{
+  float X2 = X * X;
+  float num = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
+  float den = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
+  num = num * X;
+  den = rcp_x86(den, tab);
+  num = __builtin_fmaf(num, den, 0.5f);
+  return mm_max(0.f, mm_min(1.f, num));
+}
+
+/* _mm256_cvtps_epi32: round to nearest even, out of range / NaN -> INT_MIN */
+__device__ __forceinline__ int cvt_rne(float v)
+{
+  float r = __builtin_rintf(v);
+  return (r >= -2147483648.f && r < 2147483648.f) ? (int)r : (int)0x80000000u;
+}
+
+/* vector_ps_to_epi8 (vec_avx.h:321-336) -> u8, returned XOR 0x80 (= u8-128,
+ * the signed form the dot4 path consumes) */
+__device__ __forceinline__ uint32_t quant_s8(float x)
+{
+  float r = __builtin_rintf(__builtin_fmaf(x, 127.f, 127.f));
+  uint32_t q = (r > 0.f && r < 2147483648.f) ? (uint32_t)fminf(r, 255.f) : 0u;
+  return q ^ 0x80u;
+}
+
+constexpr float kScale = 128.f * 127.f;          /* vec_avx.h:686 */
+constexpr float kScale1 = 1.f / 128.f / 127.f;   /* vec_avx.h:687 */
+constexpr float kLog256 = 5.5451774445f;         /* common.h:17 */
+constexpr float kPreemph = 0.85f;                /* lpcnet.c:40 */
+
+/* common.h:18-33, 47-58 lin2ulaw */
+__device__ __forceinline__ int lin2ulaw_x86(float x)
+{
+  const float scale = 255.f / 32768.f;
+  int s = x >= 0 ? 1 : -1;
+  x = fabsf(x);
+  float y = 1 + scale * x;
+  uint32_t bits = __float_as_uint(y);
+  int integer = (int)(bits >> 23) - 127;
+  bits -= (uint32_t)integer << 23;
+  float frac = __uint_as_float(bits) - 1.5f;
+  frac = -0.41445418f + frac * (0.95909232f + frac * (-0.33951290f + frac * 0.16541097f));
+  float l2 = (float)(1 + integer) + frac;
+  float u = (float)s * ((128.f * (0.69315f * l2)) / kLog256);
+  u = 128.f + u;
+  if (u < 0) u = 0;
+  if (u > 255) u = 255;
+  return (int)floor(.5 + (double)u);
+}
+
+/* kiss99.c:59-81 */
+__device__ __forceinline__ uint32_t kiss99_next(uint32_t &z, uint32_t &w, uint32_t &jsr, uint32_t &jcong)
+{
+  uint32_t znew = 36969u * (z & 0xFFFF) + (z >> 16);
+  uint32_t wnew = 18000u * (w & 0xFFFF) + (w >> 16);
+  uint32_t mwc = (znew << 16) + wnew;
+  uint32_t shr3 = jsr ^ (jsr << 13);
+  shr3 ^= shr3 >> 17;
+  shr3 ^= shr3 << 5;
+  uint32_t cong = 69069u * jcong + 1234567u;
+  z = znew; w = wnew; jsr = shr3; jcong = cong;
+  return (mwc ^ cong) + shr3;
+}
+
+/* maddubs(u8 x, s8 w) pair sums with int16 saturation + madd(ones) for one
+ * 4-input group; x given in the XOR-0x80 signed form. */
+__device__ __forceinline__ int dot4_sat(uint32_t w, uint32_t xs)
+{
+  uint32_t xu = xs ^ 0x80808080u;
+  int x0 = xu & 0xff, x1 = (xu >> 8) & 0xff, x2 = (xu >> 16) & 0xff, x3 = xu >> 24;
+  int w0 = (int)(int8_t)(w & 0xff), w1 = (int)(int8_t)((w >> 8) & 0xff);
+  int w2 = (int)(int8_t)((w >> 16) & 0xff), w3 = (int)(int8_t)(w >> 24);
+  int p0 = min(max(x0 * w0 + x1 * w1, -32768), 32767);
+  int p1 = min(max(x2 * w2 + x3 * w3, -32768), 32767);
+  return p0 + p1;
+}
+
+template <bool SAT>
+__device__ __forceinline__ int dot4(uint32_t w, uint32_t xs, int acc)
+{
+  if constexpr (SAT) return acc + dot4_sat(w, xs);
+  else return __builtin_amdgcn_sdot4((int)w, (int)xs, acc, false);
+}
+
+/* ------------------------------------------------------------------------ */
+/* frame network                                                             */
+
+/* out[i] = act(bias[i] + sum_j W[j*nout+i] x[j]) for a pair of streams, with
+ * the per-row sequential FMA chain of sgemv_accum16 (vec_avx.h:618-643). */
+__device__ __forceinline__ float2 chain2(const float *__restrict__ W, float b, int nout, int i, const float4 *x, int nin,
+                                         int half)
+{
+  float a0 = b, a1 = b;
+  const float *wp = W + i;
+  int j = 0;
+  for (; j + 4 <= nin; j += 4) {
+    float w0 = wp[(j + 0) * nout], w1 = wp[(j + 1) * nout], w2 = wp[(j + 2) * nout], w3 = wp[(j + 3) * nout];
+    float4 x0 = x[j], x1 = x[j + 1], x2 = x[j + 2], x3 = x[j + 3];
+    float2 y0 = half ? make_float2(x0.z, x0.w) : make_float2(x0.x, x0.y);
+    float2 y1 = half ? make_float2(x1.z, x1.w) : make_float2(x1.x, x1.y);
+    float2 y2 = half ? make_float2(x2.z, x2.w) : make_float2(x2.x, x2.y);
+    float2 y3 = half ? make_float2(x3.z, x3.w) : make_float2(x3.x, x3.y);
+    a0 = __builtin_fmaf(w0, y0.x, a0); a1 = __builtin_fmaf(w0, y0.y, a1);
+    a0 = __builtin_fmaf(w1, y1.x, a0); a1 = __builtin_fmaf(w1, y1.y, a1);
+    a0 = __builtin_fmaf(w2, y2.x, a0); a1 = __builtin_fmaf(w2, y2.y, a1);
+    a0 = __builtin_fmaf(w3, y3.x, a0); a1 = __builtin_fmaf(w3, y3.y, a1);
+  }
+  for (; j < nin; j++) {
+    float w0 = wp[j * nout];
+    float4 x0 = x[j];
+    float2 y0 = half ? make_float2(x0.z, x0.w) : make_float2(x0.x, x0.y);
+    a0 = __builtin_fmaf(w0, y0.x, a0); a1 = __builtin_fmaf(w0, y0.y, a1);
+  }
+  return make_float2(a0, a1);
+}
+
+__device__ __forceinline__ float4 chain4(const float *__restrict__ W, float b, int nout, int i, const float4 *x, int nin)
+{
+  float4 a = make_float4(b, b, b, b);
+  const float *wp = W + i;
+  for (int j = 0; j < nin; j += 4) {
+    float w0 = wp[(j + 0) * nout], w1 = wp[(j + 1) * nout], w2 = wp[(j + 2) * nout], w3 = wp[(j + 3) * nout];
+    float4 x0 = x[j], x1 = x[j + 1], x2 = x[j + 2], x3 = x[j + 3];
+    a.x = __builtin_fmaf(w0, x0.x, a.x); a.y = __builtin_fmaf(w0, x0.y, a.y); a.z = __builtin_fmaf(w0, x0.z, a.z); a.w = __builtin_fmaf(w0, x0.w, a.w);
+    a.x = __builtin_fmaf(w1, x1.x, a.x); a.y = __builtin_fmaf(w1, x1.y, a.y); a.z = __builtin_fmaf(w1, x1.z, a.z); a.w = __builtin_fmaf(w1, x1.w, a.w);
+    a.x = __builtin_fmaf(w2, x2.x, a.x); a.y = __builtin_fmaf(w2, x2.y, a.y); a.z = __builtin_fmaf(w2, x2.z, a.z); a.w = __builtin_fmaf(w2, x2.w, a.w);
+    a.x = __builtin_fmaf(w3, x3.x, a.x); a.y = __builtin_fmaf(w3, x3.y, a.y); a.z = __builtin_fmaf(w3, x3.z, a.z); a.w = __builtin_fmaf(w3, x3.w, a.w);
+  }
+  return a;
+}
+
+__device__ __forceinline__ float get4(const float4 &v, int s) { return s == 0 ? v.x : (s == 1 ? v.y : (s == 2 ? v.z : v.w)); }
+__device__ __forceinline__ void set4(float4 &v, int s, float x)
+{
+  if (s == 0) v.x = x; else if (s == 1) v.y = x; else if (s == 2) v.z = x; else v.w = x;
+}
+
+__global__ __launch_bounds__(FRAME_THREADS) void frame_kernel(FrameArgs A)
+{
+  /* activations stored [input j][stream 0..3] so one ds_read_b128 feeds 4 chains */
+  __shared__ float4 x1[3 * FIN];    /* conv1 input window: mem (2 frames) + current */
+  __shared__ float4 x2[3 * COND];   /* conv2 input window */
+  __shared__ float4 ya[COND], yb[COND];
+  __shared__ int fc[FRAME_STREAMS];
+  const int tid = threadIdx.x;
+  const int s0 = blockIdx.x * FRAME_STREAMS;
+  const uint32_t *rcp = A.rcp;
+
+  if (tid < FRAME_STREAMS) {
+    int sid = s0 + tid;
+    fc[tid] = sid < A.nstreams ? A.st[sid].frame_count : 1000;
+  }
+  for (int e = tid; e < FRAME_STREAMS * 3 * FIN; e += FRAME_THREADS) {
+    int s = e / (3 * FIN), j = e % (3 * FIN);
+    int sid = min(s0 + s, A.nstreams - 1);
+    const StreamState *p = &A.st[sid];
+    float v;
+    if (j < 2 * FIN) {
+      v = p->conv1_mem[j];
+    } else if (j < 2 * FIN + NF) {
+      v = A.features[sid * NF + (j - 2 * FIN)];
+    } else {
+      /* lpcnet.c:93-94: the 0.1 avoids rounding issues */
+      float f18 = A.features[sid * NF + 18];
+      int pitch = (int)floor(.1 + (double)(50.f * f18) + 100);
+      pitch = min(255, max(33, pitch));
+      v = A.embed_pitch[pitch * EP + (j - 2 * FIN - NF)];
+    }
+    set4(x1[j], s, v);
+  }
+  for (int e = tid; e < FRAME_STREAMS * 2 * COND; e += FRAME_THREADS) {
+    int s = e / (2 * COND), j = e % (2 * COND);
+    int sid = min(s0 + s, A.nstreams - 1);
+    set4(x2[j], s, A.st[sid].conv2_mem[j]);
+  }
+  __syncthreads();
+
+  const int i = tid & (COND - 1), half = tid >> 7;
+  /* conv1 (nnet.c:452-470): 252 inputs -> 128, tanh; cleared while frame_count < 1 */
+  {
+    float2 a = chain2(A.conv1_w, A.conv1_b[i], COND, i, x1, 3 * FIN, half);
+    a.x = tanh_x86(a.x, rcp);
+    a.y = tanh_x86(a.y, rcp);
+    if (fc[2 * half] < 1) a.x = 0.f;
+    if (fc[2 * half + 1] < 1) a.y = 0.f;
+    set4(x2[2 * COND + i], 2 * half, a.x);
+    set4(x2[2 * COND + i], 2 * half + 1, a.y);
+  }
+  __syncthreads();
+  /* conv2: 384 inputs -> 128, tanh; cleared while frame_count < FEATURES_DELAY */
+  {
+    float2 a = chain2(A.conv2_w, A.conv2_b[i], COND, i, x2, 3 * COND, half);
+    a.x = tanh_x86(a.x, rcp);
+    a.y = tanh_x86(a.y, rcp);
+    if (fc[2 * half] < FEATURES_DELAY) a.x = 0.f;
+    if (fc[2 * half + 1] < FEATURES_DELAY) a.y = 0.f;
+    set4(ya[i], 2 * half, a.x);
+    set4(ya[i], 2 * half + 1, a.y);
+  }
+  __syncthreads();
+  {
+    float2 a = chain2(A.dense1_w, A.dense1_b[i], COND, i, ya, COND, half);
+    set4(yb[i], 2 * half, tanh_x86(a.x, rcp));
+    set4(yb[i], 2 * half + 1, tanh_x86(a.y, rcp));
+  }
+  __syncthreads();
+  {
+    float2 a = chain2(A.dense2_w, A.dense2_b[i], COND, i, yb, COND, half);
+    set4(ya[i], 2 * half, tanh_x86(a.x, rcp));
+    set4(ya[i], 2 * half + 1, tanh_x86(a.y, rcp));
+  }
+  __syncthreads();
+  /* conditioning projections (linear) */
+  for (int o = tid; o < GA_ROWS + GB_ROWS; o += FRAME_THREADS) {
+    float4 a = o < GA_ROWS ? chain4(A.gadf_w, A.gadf_b[o], GA_ROWS, o, ya, COND)
+                           : chain4(A.gbdf_w, A.gbdf_b[o - GA_ROWS], GB_ROWS, o - GA_ROWS, ya, COND);
+    for (int s = 0; s < FRAME_STREAMS; s++) {
+      int sid = s0 + s;
+      if (sid >= A.nstreams) break;
+      if (o < GA_ROWS) A.st[sid].gru_a_cond[o] = get4(a, s);
+      else A.st[sid].gru_b_cond[o - GA_ROWS] = get4(a, s);
+    }
+  }
+  /* conv memories (nnet.c:469) */
+  for (int e = tid; e < FRAME_STREAMS * 2 * FIN; e += FRAME_THREADS) {
+    int s = e / (2 * FIN), j = e % (2 * FIN);
+    if (s0 + s < A.nstreams) A.st[s0 + s].conv1_mem[j] = get4(x1[FIN + j], s);
+  }
+  for (int e = tid; e < FRAME_STREAMS * 2 * COND; e += FRAME_THREADS) {
+    int s = e / (2 * COND), j = e % (2 * COND);
+    if (s0 + s < A.nstreams) A.st[s0 + s].conv2_mem[j] = get4(x2[COND + j], s);
+  }
+  /* LPC ring (lpcnet.c:110-118; LPC_GAMMA = 1 -> lpc_weighting multiplies by 1.0f) */
+  if (tid < FRAME_STREAMS * NLPC) {
+    int s = tid / NLPC, k = tid % NLPC, sid = s0 + s;
+    if (sid < A.nstreams) {
+      StreamState *p = &A.st[sid];
+      float cur = p->old_lpc[FEATURES_DELAY - 1][k];
+      float nxt = p->old_lpc[0][k];
+      float g = 1.0f, gi = g;
+      for (int q = 0; q < k; q++) gi *= g;
+      p->lpc[k] = cur * gi;
+      p->old_lpc[1][k] = nxt;
+      p->old_lpc[0][k] = A.lpc_new[sid * NLPC + k];
+    }
+  }
+  __syncthreads();
+  if (tid < FRAME_STREAMS) {
+    int sid = s0 + tid;
+    if (sid < A.nstreams && fc[tid] < 1000) A.st[sid].frame_count = fc[tid] + 1;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* sample network                                                            */
+
+/* LDS areas after the image (byte sizes for S streams). */
+template <int S, int V>
+struct SampleLds {
+  static constexpr int xa = V == 0 ? 2 * (NA / 4) * S * 4 : 2 * (NA / 4) * S * 16; /* double-buffered GRU_A input */
+  static constexpr int xb = V == 0 ? (NB / 4) * S * 4 : 0;                          /* quantized GRU_B state */
+  static constexpr int sb = S * NB * 4;                                             /* float GRU_B state */
+  static constexpr int zr = S * 2 * GB_ROWS * 4;                                    /* GRU_B gate sums, input|recurrent */
+  static constexpr int cb = S * GB_ROWS * 4;                                        /* GRU_B conditioning */
+  static constexpr int ix = S * 4 * 4;                                              /* sig/pred/exc indices */
+  static constexpr int pcm = S * FRAME * 2;
+  static constexpr int total = xa + xb + sb + zr + cb + ix + ((pcm + 15) / 16) * 16;
+};
+
+int sample_lds_bytes(int S, int variant, int image_bytes)
+{
+  int extra = 0;
+#define CASE(s, v) if (S == s && variant == v) extra = SampleLds<s, v>::total;
+  CASE(1, 0) CASE(2, 0) CASE(4, 0) CASE(1, 1) CASE(2, 1) CASE(4, 1)
+#undef CASE
+  return image_bytes + extra;
+}
+
+template <int S, int V, bool SAT>
+__global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
+{
+  extern __shared__ uint4 lds4[];
+  unsigned char *lds = (unsigned char *)lds4;
+  using L = SampleLds<S, V>;
+  unsigned char *xa_base = lds + A.image_bytes;
+  unsigned char *xb = xa_base + L::xa;
+  float *sbuf = (float *)(xb + L::xb);
+  float *zr = sbuf + S * NB;
+  float *condb = zr + S * 2 * GB_ROWS;
+  int *ix = (int *)(condb + S * GB_ROWS);
+  short *pcmbuf = (short *)(ix + S * 4);
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int s0 = blockIdx.x * S;
+  const uint32_t *rcp = (const uint32_t *)(lds + IMG_RCP);
+  const float *ulaw = (const float *)(lds + IMG_ULAW);
+  const float *logit_tab = (const float *)(lds + IMG_LOGIT);
+  const float *fcw = (const float *)(lds + IMG_FCW);
+  const float *fcb = (const float *)(lds + IMG_FCB);
+  const float *fcf = (const float *)(lds + IMG_FCF);
+
+  /* Which streams of this group synthesise this frame (lpcnet.c:239-243). */
+  bool active[S];
+  bool any = false;
+  for (int s = 0; s < S; s++) {
+    int sid = s0 + s;
+    active[s] = sid < A.nstreams && A.st[sid].frame_count > FEATURES_DELAY;
+    any |= active[s];
+  }
+  if (!any) {
+    for (int e = tid; e < S * A.N; e += SAMPLE_THREADS) {
+      int s = e / A.N, n = e % A.N;
+      if (s0 + s < A.nstreams) A.pcm[(size_t)(s0 + s) * A.N + n] = 0;
+    }
+    return;
+  }
+
+  /* weights and tables -> LDS */
+  for (int o = tid; o < A.image_bytes / 16; o += SAMPLE_THREADS) lds4[o] = A.image[o];
+
+  /* GRU_A unit state and constants: thread tid owns unit i = tid */
+  const int i = tid;
+  const float bz = A.ga_par[i], br = A.ga_par[NA + i], bh = A.ga_par[2 * NA + i];
+  const float dz = A.ga_par[3 * NA + i], dr = A.ga_par[4 * NA + i], dh = A.ga_par[5 * NA + i];
+  const int wsz = A.ga_wsum[i], wsr = A.ga_wsum[NA + i], wsh = A.ga_wsum[2 * NA + i];
+  float st[S], cz[S], cr[S], ch[S];
+  for (int s = 0; s < S; s++) {
+    const StreamState *p = &A.st[min(s0 + s, A.nstreams - 1)];
+    st[s] = p->gru_a_state[i];
+    cz[s] = p->gru_a_cond[i];
+    cr[s] = p->gru_a_cond[NA + i];
+    ch[s] = p->gru_a_cond[2 * NA + i];
+  }
+  /* stream-serial state: wave s owns stream s (lanes 0..15 hold last_sig/lpc/GRU_B units) */
+  float ls = 0.f, lp = 0.f, sbv = 0.f, pred = 0.f, deemph = 0.f;
+  uint32_t rz = 0, rw = 0, rj = 0, rc = 0, r0 = 0, r1 = 0;
+  int last_exc = 0;
+  const int my_s = wv;
+  const bool stream_wave = my_s < S;
+  if (stream_wave) {
+    const StreamState *p = &A.st[min(s0 + my_s, A.nstreams - 1)];
+    if (lane < NLPC) {
+      ls = p->last_sig[lane];
+      lp = p->lpc[lane];
+      sbv = p->gru_b_state[lane];
+    }
+    for (int k = lane; k < GB_ROWS; k += 64) condb[my_s * GB_ROWS + k] = p->gru_b_cond[k];
+    deemph = p->deemph_mem;
+    last_exc = p->last_exc;
+    rz = p->rng[0]; rw = p->rng[1]; rj = p->rng[2]; rc = p->rng[3];
+  }
+  __syncthreads(); /* image in LDS */
+
+  /* initial quantized inputs: GRU_A state (buffer 0) and GRU_B state */
+  if constexpr (V == 0) {
+    for (int s = 0; s < S; s++) xa_base[(i >> 2) * S * 4 + s * 4 + (i & 3)] = (unsigned char)quant_s8(st[s]);
+    if (stream_wave && lane < NB) {
+      xb[(lane >> 2) * S * 4 + my_s * 4 + (lane & 3)] = (unsigned char)quant_s8(sbv);
+      sbuf[my_s * NB + lane] = sbv;
+    }
+  } else {
+    float *xf = (float *)xa_base;
+    for (int s = 0; s < S; s++) xf[((i >> 2) * S + s) * 4 + (i & 3)] = st[s];
+    if (stream_wave && lane < NB) sbuf[my_s * NB + lane] = sbv;
+  }
+
+  /* per-stream scalar step that precedes every sample: pred, u-law indices, RNG */
+  auto pre_sample = [&]() {
+    /* pred = -sum last_sig[j]*lpc[j], sequential (lpcnet.c:252); lane j holds the j-th product */
+    float prod = ls * lp;
+    float p2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NLPC; j++) p2 = p2 - __int_as_float(__builtin_amdgcn_readlane(__float_as_int(prod), j));
+    pred = p2;
+    float ls0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ls), 0));
+    if (lane == 0) {
+      ix[my_s * 4 + 0] = lin2ulaw_x86(ls0);
+      ix[my_s * 4 + 1] = lin2ulaw_x86(pred);
+      ix[my_s * 4 + 2] = last_exc;
+    }
+    r0 = kiss99_next(rz, rw, rj, rc);
+    r1 = kiss99_next(rz, rw, rj, rc);
+  };
+  if (stream_wave) pre_sample();
+  __syncthreads();
+
+  /* GRU_A per-gate LDS chunks for this wave */
+  const uint32_t *lds32 = (const uint32_t *)lds;
+  const uint16_t *lds16 = (const uint16_t *)lds;
+  const int j8 = lane >> 3;
+
+  for (int n = 0; n < A.N; n++) {
+    const int cur = n & 1;
+    /* ---- phase B: GRU_A (nnet.c:484-491 + 410-448) ---------------------- */
+    {
+      float inz[S], inr[S], inh[S];
+      for (int s = 0; s < S; s++) {
+        const int sig = ix[s * 4 + 0], prd = ix[s * 4 + 1], exc = ix[s * 4 + 2];
+        const float *e1 = A.emb_sig + sig * GA_ROWS, *e2 = A.emb_pred + prd * GA_ROWS, *e3 = A.emb_exc + exc * GA_ROWS;
+        inz[s] = ((cz[s] + e1[i]) + e2[i]) + e3[i];
+        inr[s] = ((cr[s] + e1[NA + i]) + e2[NA + i]) + e3[NA + i];
+        inh[s] = ((ch[s] + e1[2 * NA + i]) + e2[2 * NA + i]) + e3[2 * NA + i];
+      }
+      float gz[S], gr[S], gh[S];
+      if constexpr (V == 0) {
+        int az[S], ar[S], ah[S];
+        for (int s = 0; s < S; s++) {
+          az[s] = cvt_rne(((bz + dz * st[s]) + inz[s]) * kScale) + (SAT ? 0 : wsz);
+          ar[s] = cvt_rne(((br + dr * st[s]) + inr[s]) * kScale) + (SAT ? 0 : wsr);
+          ah[s] = cvt_rne((bh + dh * st[s]) * kScale) + (SAT ? 0 : wsh);
+        }
+        const unsigned char *xa = xa_base + cur * (NA / 4) * S * 4;
+        auto run_gate = [&](int g, int *acc) {
+          const uint32_t *wp = lds32 + A.ga_woff[wv][g] + lane;
+          const uint16_t *cp = lds16 + A.ga_coff[wv][g] + j8;
+          const int K = A.ga_K[wv][g];
+#pragma unroll 4
+          for (int k = 0; k < K; k++) {
+            uint32_t w = wp[k * 64];
+            int off = cp[k * 8] * (S * 4);
+            if constexpr (S == 4) {
+              uint4 xv = *(const uint4 *)(xa + off);
+              acc[0] = dot4<SAT>(w, xv.x, acc[0]);
+              acc[1] = dot4<SAT>(w, xv.y, acc[1]);
+              acc[2] = dot4<SAT>(w, xv.z, acc[2]);
+              acc[3] = dot4<SAT>(w, xv.w, acc[3]);
+            } else if constexpr (S == 2) {
+              uint2 xv = *(const uint2 *)(xa + off);
+              acc[0] = dot4<SAT>(w, xv.x, acc[0]);
+              acc[1] = dot4<SAT>(w, xv.y, acc[1]);
+            } else {
+              acc[0] = dot4<SAT>(w, *(const uint32_t *)(xa + off), acc[0]);
+            }
+          }
+        };
+        run_gate(0, az);
+        run_gate(1, ar);
+        run_gate(2, ah);
+        for (int s = 0; s < S; s++) {
+          gz[s] = (float)az[s] * kScale1;
+          gr[s] = (float)ar[s] * kScale1;
+          gh[s] = (float)ah[s] * kScale1;
+        }
+      } else {
+        for (int s = 0; s < S; s++) {
+          gz[s] = (bz + dz * st[s]) + inz[s];
+          gr[s] = (br + dr * st[s]) + inr[s];
+          gh[s] = bh + dh * st[s];
+        }
+        const float4 *xf = (const float4 *)(xa_base + cur * (NA / 4) * S * 16);
+        auto run_gate_f = [&](int g, float *y) {
+          const float4 *wp = A.ga_wf + A.ga_woff[wv][g] + lane;
+          const uint16_t *cp = lds16 + A.ga_coff[wv][g] + j8;
+          const int K = A.ga_K[wv][g];
+          for (int k = 0; k < K; k++) {
+            int c = cp[k * 8];
+            float4 w = wp[k * 64];
+            if (c != 0xFFFF) {
+              for (int s = 0; s < S; s++) {
+                float4 x = xf[c * S + s];
+                y[s] = __builtin_fmaf(w.x, x.x, y[s]);
+                y[s] = __builtin_fmaf(w.y, x.y, y[s]);
+                y[s] = __builtin_fmaf(w.z, x.z, y[s]);
+                y[s] = __builtin_fmaf(w.w, x.w, y[s]);
+              }
+            }
+          }
+        };
+        run_gate_f(0, gz);
+        run_gate_f(1, gr);
+        run_gate_f(2, gh);
+      }
+      const int nxt = cur ^ 1;
+      for (int s = 0; s < S; s++) {
+        float z = sigmoid_x86(gz[s], rcp);
+        float r = sigmoid_x86(gr[s], rcp);
+        float h = gh[s] * r + inh[s];
+        h = tanh_x86(h, rcp);
+        st[s] = z * st[s] + (1.f - z) * h;
+        if constexpr (V == 0)
+          xa_base[nxt * (NA / 4) * S * 4 + (i >> 2) * S * 4 + s * 4 + (i & 3)] = (unsigned char)quant_s8(st[s]);
+        else
+          ((float *)(xa_base + nxt * (NA / 4) * S * 16))[((i >> 2) * S + s) * 4 + (i & 3)] = st[s];
+      }
+    }
+    __syncthreads();
+
+    /* ---- phase C: GRU_B gate sums, wave w = row block w (nnet.c:345-361) --- */
+    {
+      const int nxt = cur ^ 1;
+      const int rb = wv, r = lane & 7, ks = lane >> 3, row = rb * 8 + r;
+      if constexpr (V == 0) {
+        const unsigned char *xa = xa_base + nxt * (NA / 4) * S * 4;
+        int acc[S], accr[S];
+        for (int s = 0; s < S; s++) { acc[s] = 0; accr[s] = 0; }
+        const uint32_t *wp = lds32 + A.gb_woff[rb];
+        const uint16_t *cp = lds16 + A.gb_coff[rb];
+        const int nb = A.gb_nb[rb];
+        for (int k = ks; k < nb; k += 8) {
+          uint32_t w = wp[k * 8 + r];
+          int off = cp[k] * (S * 4);
+          for (int s = 0; s < S; s++) acc[s] = dot4<SAT>(w, *(const uint32_t *)(xa + off + s * 4), acc[s]);
+        }
+        if (ks < NB / 4) {
+          uint32_t w = ((const uint32_t *)(lds + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r];
+          for (int s = 0; s < S; s++) accr[s] = dot4<SAT>(w, *(const uint32_t *)(xb + ks * S * 4 + s * 4), accr[s]);
+        }
+        for (int s = 0; s < S; s++) {
+          acc[s] += __shfl_xor(acc[s], 8);
+          acc[s] += __shfl_xor(acc[s], 16);
+          acc[s] += __shfl_xor(acc[s], 32);
+          accr[s] += __shfl_xor(accr[s], 8);
+          accr[s] += __shfl_xor(accr[s], 16);
+          accr[s] += __shfl_xor(accr[s], 32);
+        }
+        if (ks == 0) {
+          for (int s = 0; s < S; s++) {
+            int seed = cvt_rne((A.gb_par[row] + condb[s * GB_ROWS + row]) * kScale) + (SAT ? 0 : A.gb_wsum[row]);
+            int seedr = cvt_rne(A.gb_par[GB_ROWS + row] * kScale) + (SAT ? 0 : A.gb_wsum[GB_ROWS + row]);
+            zr[s * 2 * GB_ROWS + row] = (float)(seed + acc[s]) * kScale1;
+            zr[s * 2 * GB_ROWS + GB_ROWS + row] = (float)(seedr + accr[s]) * kScale1;
+          }
+        }
+      } else {
+        /* fp32: one sequential FMA chain per (row, stream) in block order */
+        const int s = lane >> 3;
+        if (s < S) {
+          const float4 *xf = (const float4 *)(xa_base + nxt * (NA / 4) * S * 16);
+          const float4 *wp = (const float4 *)(lds + A.gb_woff[rb] * 4);
+          const uint16_t *cp = lds16 + A.gb_coff[rb];
+          const int nb = A.gb_nb[rb];
+          float y = A.gb_par[row] + condb[s * GB_ROWS + row];
+          for (int k = 0; k < nb; k++) {
+            float4 w = wp[k * 8 + r];
+            float4 x = xf[cp[k] * S + s];
+            y = __builtin_fmaf(w.x, x.x, y);
+            y = __builtin_fmaf(w.y, x.y, y);
+            y = __builtin_fmaf(w.z, x.z, y);
+            y = __builtin_fmaf(w.w, x.w, y);
+          }
+          float y2 = A.gb_par[GB_ROWS + row];
+          for (int j = 0; j < NB; j++) y2 = __builtin_fmaf(A.gb_recf[j * GB_ROWS + row], sbuf[s * NB + j], y2);
+          zr[s * 2 * GB_ROWS + row] = y;
+          zr[s * 2 * GB_ROWS + GB_ROWS + row] = y2;
+        }
+      }
+    }
+    __syncthreads();
+
+    /* ---- phase F: per-stream GRU_B update, dual-FC sampling, output -------- */
+    if (stream_wave) {
+      const int s = my_s;
+      const float *zs = zr + s * 2 * GB_ROWS;
+      /* GRU_B elementwise (nnet.c:362-371) */
+      if (lane < NB) {
+        float z = sigmoid_x86(zs[lane] + zs[GB_ROWS + lane], rcp);
+        float r = sigmoid_x86(zs[NB + lane] + zs[GB_ROWS + NB + lane], rcp);
+        float h = zs[2 * NB + lane] + zs[GB_ROWS + 2 * NB + lane] * r;
+        h = tanh_x86(h, rcp);
+        sbv = z * sbv + (1.f - z) * h;
+      }
+      float xv[NB];
+#pragma unroll
+      for (int j = 0; j < NB; j++) xv[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sbv), j));
+      /* dual_fc tree sampling (nnet.c:163-214), 30 (node, channel) chains at a time */
+      float thr[8];
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        thr[b] = logit_tab[(r0 >> (8 * b)) & 0xFF];
+        thr[b + 4] = logit_tab[(r1 >> (8 * b)) & 0xFF];
+      }
+      const int q = lane >> 1, ch2 = lane & 1;
+      auto node_logit = [&](int node) -> float {
+        float sum = fcb[ch2 * 256 + node];
+        const float *w = fcw + node * 32 + ch2 * 16;
+#pragma unroll
+        for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
+        float v = fcf[ch2 * 256 + node] * tanh_x86(sum, rcp);
+        return v + __shfl_xor(v, 1);
+      };
+      float lg[8];
+      int val = 0;
+      {
+        int node = q < 15 ? q + 1 : 1; /* levels 0..3: nodes 1..15 */
+        float l = node_logit(node);
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          int nd = (1 << b) | val;
+          float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), 2 * (nd - 1)));
+          lg[b] = v;
+          val = (val << 1) | (thr[b] < v ? 1 : 0);
+        }
+      }
+      {
+        /* levels 4..7 under the chosen prefix: 1 + 2 + 4 + 8 nodes */
+        int qq = q < 15 ? q : 0;
+        int lvl = qq == 0 ? 4 : (qq < 3 ? 5 : (qq < 7 ? 6 : 7));
+        int off = qq + 1 - (1 << (lvl - 4));
+        int node = (1 << lvl) | (val << (lvl - 4)) | off;
+        float l = node_logit(node);
+        const int base = val;
+#pragma unroll
+        for (int b = 4; b < 8; b++) {
+          int o = val & ((1 << (b - 4)) - 1);
+          (void)base;
+          int qi = (1 << (b - 4)) - 1 + o;
+          float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), 2 * qi));
+          lg[b] = v;
+          val = (val << 1) | (thr[b] < v ? 1 : 0);
+        }
+      }
+      const int exc = val;
+      /* output sample (lpcnet.c:260-269) */
+      float pcm = pred + ulaw[exc];
+      float up = __shfl_up(ls, 1);
+      ls = lane == 0 ? pcm : up;
+      last_exc = exc;
+      float o = pcm + kPreemph * deemph;
+      deemph = o;
+      if (o < -32767) o = -32767;
+      if (o > 32767) o = 32767;
+      if (lane == 0) pcmbuf[s * FRAME + n] = (short)(int)floor(.5 + (double)o);
+      if (A.trace_logits && lane < 8 && active[s]) {
+        float v = lg[0];
+#pragma unroll
+        for (int b = 1; b < 8; b++) v = lane == b ? lg[b] : v;
+        A.trace_logits[((size_t)(s0 + s) * A.N + n) * 8 + lane] = v;
+      }
+      if (A.trace_exc && lane == 0 && active[s]) A.trace_exc[(size_t)(s0 + s) * A.N + n] = exc;
+      if constexpr (V == 0) {
+        if (lane < NB) xb[(lane >> 2) * S * 4 + s * 4 + (lane & 3)] = (unsigned char)quant_s8(sbv);
+      }
+      if (lane < NB) sbuf[s * NB + lane] = sbv;
+      if (n + 1 < A.N) pre_sample(); /* exactly two kiss99 draws per sample */
+    }
+    __syncthreads();
+  }
+
+  /* ---- write back (only streams that synthesised this frame) ------------- */
+  for (int s = 0; s < S; s++)
+    if (active[s]) A.st[s0 + s].gru_a_state[i] = st[s];
+  if (stream_wave && active[my_s]) {
+    StreamState *p = &A.st[s0 + my_s];
+    if (lane < NLPC) {
+      p->last_sig[lane] = ls;
+      p->gru_b_state[lane] = sbv;
+    }
+    if (lane == 0) {
+      p->deemph_mem = deemph;
+      p->last_exc = last_exc;
+      p->rng[0] = rz; p->rng[1] = rw; p->rng[2] = rj; p->rng[3] = rc;
+    }
+  }
+  for (int e = tid; e < S * A.N; e += SAMPLE_THREADS) {
+    int s = e / A.N, n = e % A.N;
+    if (s0 + s < A.nstreams) A.pcm[(size_t)(s0 + s) * A.N + n] = active[s] ? pcmbuf[s * FRAME + n] : (short)0;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+int launch_frame(const FrameArgs &a, void *stream)
+{
+  int grid = (a.nstreams + FRAME_STREAMS - 1) / FRAME_STREAMS;
+  hipLaunchKernelGGL(frame_kernel, dim3(grid), dim3(FRAME_THREADS), 0, (hipStream_t)stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <int S, int V, bool SAT>
+static int launch_sample_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
+{
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void *)sample_kernel<S, V, SAT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+        hipSuccess)
+      return -1;
+    attr_set = true;
+  }
+  int grid = (a.nstreams + S - 1) / S;
+  hipLaunchKernelGGL((sample_kernel<S, V, SAT>), dim3(grid), dim3(SAMPLE_THREADS), lds_bytes, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_sample(const SampleArgs &a, int S, int variant, int sat, int lds_bytes, void *stream)
+{
+  hipStream_t st = (hipStream_t)stream;
+  if (variant == 0) {
+    if (sat) {
+      if (S == 4) return launch_sample_t<4, 0, true>(a, lds_bytes, st);
+      if (S == 2) return launch_sample_t<2, 0, true>(a, lds_bytes, st);
+      return launch_sample_t<1, 0, true>(a, lds_bytes, st);
+    }
+    if (S == 4) return launch_sample_t<4, 0, false>(a, lds_bytes, st);
+    if (S == 2) return launch_sample_t<2, 0, false>(a, lds_bytes, st);
+    return launch_sample_t<1, 0, false>(a, lds_bytes, st);
+  }
+  if (S == 4) return launch_sample_t<4, 1, false>(a, lds_bytes, st);
+  if (S == 2) return launch_sample_t<2, 1, false>(a, lds_bytes, st);
+  return launch_sample_t<1, 1, false>(a, lds_bytes, st);
+}
+
+}  // namespace lpcnet_mi355x

@@ -1,0 +1,107 @@
+/*
+ * lpcnet_engine.h -- internal declarations of the MI355X LPCNet engine.
+ * Shared by the host engine (engine.cpp) and the HIP kernels (kernels.hip).
+ */
+#ifndef LPCNET_ENGINE_H
+#define LPCNET_ENGINE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lpcnet_mi355x {
+
+/* Default model dimensions (training_tf2/lpcnet.py:312-325; the reference
+ * bakes them into the generated nnet_data.h). */
+constexpr int NA = 384;        /* GRU_A units */
+constexpr int NB = 16;         /* GRU_B units */
+constexpr int COND = 128;      /* conditioning size */
+constexpr int NF = 20;         /* NB_FEATURES */
+constexpr int EP = 64;         /* pitch embedding */
+constexpr int FIN = NF + EP;   /* lpcnet.c:44 FRAME_INPUT_SIZE */
+constexpr int NLPC = 16;       /* LPC_ORDER */
+constexpr int FRAME = 160;     /* samples per frame */
+constexpr int GA_ROWS = 3 * NA;
+constexpr int GB_ROWS = 3 * NB;
+constexpr int FEATURES_DELAY = 2;
+constexpr int SAMPLE_THREADS = 384; /* one thread per GRU_A unit */
+constexpr int SAMPLE_WAVES = SAMPLE_THREADS / 64;
+constexpr int FRAME_THREADS = 256;
+constexpr int FRAME_STREAMS = 4;    /* streams per frame-network workgroup */
+
+/* Per-stream synthesis state in device memory (lpcnet_private.h:28-48). */
+struct alignas(16) StreamState {
+  float gru_a_state[NA];
+  float gru_a_cond[GA_ROWS];
+  float gru_b_cond[GB_ROWS];
+  float gru_b_state[NB];
+  float last_sig[NLPC];
+  float lpc[NLPC];
+  float old_lpc[FEATURES_DELAY][NLPC];
+  float conv1_mem[FIN * 2];
+  float conv2_mem[COND * 2];
+  float deemph_mem;
+  int last_exc;
+  int frame_count;
+  uint32_t rng[4];
+  int pad[1];
+};
+
+/* Fixed sections of the sample kernel's LDS image (byte offsets). */
+constexpr int IMG_RCP = 0;                       /* 2048 u32 rcpps table */
+constexpr int IMG_ULAW = IMG_RCP + 2048 * 4;     /* 256 f32 ulaw2lin */
+constexpr int IMG_LOGIT = IMG_ULAW + 256 * 4;    /* 256 f32 sampling logit table */
+constexpr int IMG_FCW = IMG_LOGIT + 256 * 4;     /* dual_fc weights [256][2][16] f32 */
+constexpr int IMG_FCB = IMG_FCW + 256 * 32 * 4;  /* dual_fc bias [2][256] */
+constexpr int IMG_FCF = IMG_FCB + 512 * 4;       /* dual_fc factor [2][256] */
+constexpr int IMG_VAR = IMG_FCF + 512 * 4;       /* start of the variable sections */
+
+struct FrameArgs {
+  StreamState *st;
+  int nstreams;
+  const float *features; /* [B][NF] for this frame */
+  const float *lpc_new;  /* [B][NLPC] lpc_from_cepstrum(features) (host) */
+  const float *conv1_w, *conv1_b, *conv2_w, *conv2_b;
+  const float *dense1_w, *dense1_b, *dense2_w, *dense2_b;
+  const float *gadf_w, *gadf_b, *gbdf_w, *gbdf_b;
+  const float *embed_pitch;
+  const uint32_t *rcp; /* 2048-entry table in global memory */
+};
+
+struct SampleArgs {
+  StreamState *st;
+  int nstreams;
+  int N;                 /* samples to produce (<= FRAME) */
+  short *pcm;            /* [B][N] */
+  const float *emb_sig, *emb_pred, *emb_exc; /* [256][GA_ROWS] */
+  const float *ga_par;   /* [6][NA]: recurrent bias z,r,h then diag z,r,h */
+  const int *ga_wsum;    /* [3][NA]: 128*rowsum(int8 w) (non-saturating int8 path) */
+  const float *gb_par;   /* [2][GB_ROWS]: input bias, recurrent bias */
+  const int *gb_wsum;    /* [2][GB_ROWS] */
+  const uint4 *image;    /* LDS image */
+  int image_bytes;
+  int ga_K[SAMPLE_WAVES][3];   /* blocks per lane for wave w, gate g (padded) */
+  int ga_woff[SAMPLE_WAVES][3];/* weight chunk offset (u32 units in image / float4 units in ga_wf) */
+  int ga_coff[SAMPLE_WAVES][3];/* column-block index chunk offset (u16 units in image) */
+  int gb_nb[GB_ROWS / 8];      /* blocks per GRU_B row block */
+  int gb_woff[GB_ROWS / 8];    /* u32 units in image [k][8] / float4 [k][8][2] in gb_wf */
+  int gb_coff[GB_ROWS / 8];    /* u16 units in image */
+  int gb_rec_off;              /* byte offset of GRU_B recurrent int8 weights in image */
+  const float4 *ga_wf;   /* fp32 variant: GRU_A blocks [chunk][k][64] float4 */
+  const float4 *gb_wf;   /* fp32 variant: GRU_B blocks [rb][k][8 rows][2] float4 (in c) */
+  const float *gb_recf;  /* fp32 variant: GRU_B recurrent [NB][GB_ROWS] */
+  float *trace_logits;   /* optional [B][N][8] */
+  int *trace_exc;        /* optional [B][N] */
+};
+
+/* Kernel launchers (kernels.hip).  variant: 0 int8, 1 fp32. sat: int8 pairs
+ * may saturate. lds_bytes from sample_lds_bytes(). */
+int sample_lds_bytes(int S, int variant, int image_bytes);
+int launch_frame(const FrameArgs &a, void *stream);
+int launch_sample(const SampleArgs &a, int S, int variant, int sat, int lds_bytes, void *stream);
+
+/* Host LPC (lpc_host.cpp). */
+float lpc_from_cepstrum_host(float *lpc, const float *ceps);
+
+}  // namespace lpcnet_mi355x
+
+#endif

@@ -1,0 +1,181 @@
+"""ctypes wrapper of the CPU checker (oracle/liblpcnet_oracle.so and, when
+built, oracle/_ref/libref_kernels.so).  TEST INFRASTRUCTURE ONLY."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liblpcnet_oracle.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref_kernels.so")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def ensure_built():
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+
+
+ensure_built()
+_ora = C.CDLL(ORACLE_SO)
+_vp, _i = C.c_void_p, C.c_int
+for name, res, args in [
+    ("oracle_port_kernels", _vp, []),
+    ("oracle_set_rcp_table", None, [_vp]),
+    ("oracle_rcp", C.c_float, [C.c_float]),
+    ("oracle_tanh", C.c_float, [C.c_float]),
+    ("oracle_sigmoid", C.c_float, [C.c_float]),
+    ("oracle_quantize_u8", None, [_vp, _vp, _i]),
+    ("oracle_create", _vp, [C.c_char_p, _i, _i, _vp]),
+    ("oracle_destroy", None, [_vp]),
+    ("oracle_reset", None, [_vp]),
+    ("oracle_synthesize", None, [_vp, _vp, _vp, _i, _i]),
+    ("oracle_set_trace", None, [_vp, _vp, _vp, _vp]),
+    ("oracle_get_frame", None, [_vp, _vp, _vp, _vp]),
+    ("oracle_frame_count", _i, [_vp]),
+    ("oracle_get_state", None, [_vp, _vp, _vp]),
+]:
+    fn = getattr(_ora, name)
+    fn.restype = res
+    fn.argtypes = args
+
+RCP_TABLE = np.fromfile(os.path.join(GOLDEN, "rcp_x86.bin"), dtype=np.uint32)
+assert RCP_TABLE.size == 2048
+_ora.oracle_set_rcp_table(RCP_TABLE.ctypes.data)
+
+_ref = None
+if os.path.exists(REF_SO):
+    try:
+        _ref = C.CDLL(REF_SO)
+        _ref.ref_kernels.restype = _vp
+        _ref.ref_rcp_table.restype = _i
+        _ref.ref_rcp_table.argtypes = [_vp]
+        _ref.ref_rcp.restype = C.c_float
+        _ref.ref_rcp.argtypes = [C.c_float]
+        _ref.ref_quantize_u8.argtypes = [_vp, _vp, _i]
+    except OSError:
+        _ref = None
+
+
+def have_ref() -> bool:
+    return _ref is not None
+
+
+def port_kernels():
+    return _ora.oracle_port_kernels()
+
+
+def ref_kernels():
+    return _ref.ref_kernels() if _ref is not None else None
+
+
+def kernel_table(k: C.c_void_p):
+    """Calls into an oracle_kernels table (struct of function pointers)."""
+    FT = C.CFUNCTYPE
+    vp, i = C.c_void_p, C.c_int
+
+    class K(C.Structure):
+        _fields_ = [
+            ("vec_tanh", FT(None, vp, vp, i)),
+            ("vec_sigmoid", FT(None, vp, vp, i)),
+            ("tanh1", FT(C.c_float, C.c_float)),
+            ("sgemv16", FT(None, vp, vp, i, i, i, vp)),
+            ("sparse8x4_i8", FT(None, vp, vp, i, i, vp, vp)),
+            ("dense8x4_i8", FT(None, vp, vp, i, i, vp)),
+            ("sparse8x4_f32", FT(None, vp, vp, i, vp, vp)),
+            ("lin2ulaw", FT(i, C.c_float)),
+            ("ulaw2lin", FT(C.c_float, C.c_float)),
+            ("rng_srand", FT(None, vp, vp, i)),
+            ("rng_rand", FT(C.c_uint32, vp)),
+            ("lpc_from_cepstrum", FT(C.c_float, vp, vp)),
+            ("lpc_weighting", FT(None, vp, C.c_float)),
+        ]
+
+    return K.from_address(k)
+
+
+class Oracle:
+    """One reference-semantics synthesis stream on the CPU."""
+
+    def __init__(self, blob: bytes, variant: int = 0, kernels=None):
+        self._st = _ora.oracle_create(blob, len(blob), variant, kernels or port_kernels())
+        if not self._st:
+            raise ValueError("oracle_create: blob rejected")
+
+    def synthesize(self, features: np.ndarray, n: int = 160, preload: np.ndarray | None = None,
+                   trace: bool = False):
+        f = np.ascontiguousarray(np.asarray(features, np.float32)[:20])
+        out = np.zeros(n, np.int16) if preload is None else np.ascontiguousarray(preload, np.int16).copy()
+        npre = 0 if preload is None else len(preload)
+        if trace:
+            lg = np.zeros((n, 8), np.float32)
+            ex = np.zeros(n, np.int32)
+            rw = np.zeros((n, 2), np.uint32)
+            _ora.oracle_set_trace(self._st, lg.ctypes.data, ex.ctypes.data, rw.ctypes.data)
+        _ora.oracle_synthesize(self._st, f.ctypes.data, out.ctypes.data, n, npre)
+        if trace:
+            _ora.oracle_set_trace(self._st, None, None, None)
+            return out, lg, ex, rw
+        return out
+
+    def frame(self):
+        a = np.zeros(1152, np.float32)
+        b = np.zeros(48, np.float32)
+        lpc = np.zeros(16, np.float32)
+        _ora.oracle_get_frame(self._st, a.ctypes.data, b.ctypes.data, lpc.ctypes.data)
+        return a, b, lpc
+
+    def state(self):
+        a = np.zeros(384, np.float32)
+        b = np.zeros(16, np.float32)
+        _ora.oracle_get_state(self._st, a.ctypes.data, b.ctypes.data)
+        return a, b
+
+    def frame_count(self) -> int:
+        return _ora.oracle_frame_count(self._st)
+
+    def reset(self):
+        _ora.oracle_reset(self._st)
+
+    def __del__(self):
+        try:
+            _ora.oracle_destroy(self._st)
+        except Exception:
+            pass
+
+
+def synth_stream(blob: bytes, feats: np.ndarray, variant: int = 0, kernels=None, n: int = 160) -> np.ndarray:
+    o = Oracle(blob, variant, kernels)
+    return np.stack([o.synthesize(feats[f], n) for f in range(len(feats))])
+
+
+def oracle_tanh(x: float) -> float:
+    return _ora.oracle_tanh(x)
+
+
+def oracle_sigmoid(x: float) -> float:
+    return _ora.oracle_sigmoid(x)
+
+
+def oracle_rcp(x: float) -> float:
+    return _ora.oracle_rcp(x)
+
+
+def ref_rcp(x: float) -> float:
+    return _ref.ref_rcp(x)
+
+
+def ref_rcp_table() -> tuple[np.ndarray, int]:
+    t = np.zeros(2048, np.uint32)
+    bad = _ref.ref_rcp_table(t.ctypes.data)
+    return t, bad
+
+
+def quantize_u8(x: np.ndarray, ref: bool = False) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.zeros(len(x) + 32, np.uint8)
+    (_ref.ref_quantize_u8 if ref else _ora.oracle_quantize_u8)(out.ctypes.data, x.ctypes.data, len(x))
+    return out[:len(x)]

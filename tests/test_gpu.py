@@ -1,0 +1,145 @@
+"""Parity of the HIP path (through the C-ABI) with the golden fixtures made
+from the reference's own kernels and with the CPU oracle.  Integer outputs
+(PCM, excitation) must be identical; the pre-sampling logits and every float
+state are compared bit for bit (tolerance 0 ulp: north_star asks for PCM
+identity under identical kiss99 seeding, which requires bit-exact floats)."""
+import os
+
+import numpy as np
+import pytest
+
+import lpcnet_amd as L
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+GOLD = O.GOLDEN
+
+
+def feats(stream, nframes):
+    return L.synthetic_features(stream, nframes)[:, :20]
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def blobs():
+    return {"streams_int8": L.synthetic_model(1, 0), "streams_fp32": L.synthetic_model(1, 1),
+            "streams_int8_sat": L.synthetic_model(1, 0, True)}
+
+
+@pytest.mark.parametrize("name", ["streams_int8", "streams_fp32", "streams_int8_sat"])
+def test_batch_matches_golden(require_gpu, blobs, name):
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    streams = list(G["streams"])
+    F = G["pcm"].shape[1]
+    b = L.LPCNetBatch(len(streams), 0, blobs[name])
+    info = b.info()
+    assert info.variant == int(G["variant"])
+    if name.endswith("_sat"):
+        assert info.may_saturate == 1
+    b.set_trace(True)
+    for fr in range(F):
+        pcm = b.synthesize(G["features"][:, fr, :20])
+        assert np.array_equal(pcm, G["pcm"][:, fr]), f"frame {fr}: first diff stream/sample " \
+            f"{np.argwhere(pcm != G['pcm'][:, fr])[:3].tolist()}"
+        if 2 <= fr < 6:
+            lg, ex = b.get_trace(160)
+            assert np.array_equal(ex[0], G["trace_exc"][fr - 2])
+            assert np.array_equal(bits(lg[0]), bits(G["trace_logits"][fr - 2]))
+        if fr < 6:
+            st = b.get_state(0)
+            got = np.concatenate([st["gru_a_cond"], st["gru_b_cond"], st["lpc"]])
+            assert np.array_equal(bits(got), bits(G["frame_cond"][fr])), f"frame {fr} conditioning"
+    st = b.get_state(0)
+    assert np.array_equal(bits(st["gru_a_state"]), bits(G["final_gru_a_state"]))
+    assert np.array_equal(bits(st["gru_b_state"]), bits(G["final_gru_b_state"]))
+
+
+def test_single_stream_api_matches_golden(require_gpu, blobs):
+    """lpcnet_create / lpcnet_load_model / lpcnet_synthesize (include/lpcnet.h)."""
+    G = np.load(os.path.join(GOLD, "streams_int8.npz"))
+    net = L.LPCNet(blobs["streams_int8"])
+    for fr in range(G["pcm"].shape[1]):
+        assert np.array_equal(net.synthesize(G["features"][0, fr]), G["pcm"][0, fr]), fr
+    net.reset()
+    assert np.array_equal(net.synthesize(G["features"][0, 0]), G["pcm"][0, 0])
+
+
+@pytest.mark.parametrize("B,check", [(512, (0, 255, 511)), (1024, (0, 3, 517, 1023)), (1100, (1099, 1024, 5))])
+def test_large_batch_streams_match_oracle(require_gpu, blobs, B, check):
+    """Streams-per-workgroup 2 and 4 (and a ragged last workgroup) against the oracle."""
+    F = 5
+    blob = blobs["streams_int8"]
+    b = L.LPCNetBatch(B, 0, blob)
+    allf = np.stack([feats(s, F) for s in range(B)], 1)  # [F][B][20]
+    out = np.stack([b.synthesize(allf[f]) for f in range(F)], 1)  # [B][F][160]
+    for s in check:
+        ref = O.synth_stream(blob, allf[:, s], 0)
+        assert np.array_equal(out[s], ref), s
+    assert np.all(out[:, :2] == 0)  # FEATURES_DELAY silent frames
+    assert np.abs(out[:, 2:]).mean() > 100
+
+
+def test_device_resident_frames_equal_host_path(require_gpu, blobs):
+    """lpcnet_batch_synthesize_frames (pipelined host LPC) == frame-by-frame host API."""
+    B, F = 64, 6
+    blob = blobs["streams_int8"]
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    a = L.LPCNetBatch(B, 0, blob)
+    ref = np.stack([a.synthesize(allf[f]) for f in range(F)], 0)
+    b = L.LPCNetBatch(B, 0, blob)
+    df = b.device_alloc(allf.nbytes)
+    dp = b.device_alloc(F * B * 160 * 2)
+    b.h2d(df, allf)
+    b.synthesize_frames(allf, df, dp, F)
+    b.sync()
+    got = np.zeros((F, B, 160), np.int16)
+    b.d2h(got, dp)
+    b.device_free(df)
+    b.device_free(dp)
+    assert np.array_equal(got, ref)
+
+
+def test_partial_frame_and_reset_stream(require_gpu, blobs):
+    """N < 160 (lpcnet_synthesize with N=80) and a per-stream reset mid-run."""
+    blob = blobs["streams_int8"]
+    B, F = 4, 8
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    b = L.LPCNetBatch(B, 0, blob)
+    ref = [O.Oracle(blob, 0) for _ in range(B)]
+    for f in range(F):
+        if f == 4:
+            b.reset(2)
+            ref[2] = O.Oracle(blob, 0)
+        n = 80 if f % 2 else 160
+        out = b.synthesize(allf[f], n)
+        for s in range(B):
+            assert np.array_equal(out[s], ref[s].synthesize(allf[f, s], n)), (f, s)
+
+
+def test_rejects_bad_blob(require_gpu, blobs):
+    b = L.LPCNetBatch(2, 0)
+    with pytest.raises(L.LPCNetError):
+        b.load_model(blobs["streams_int8"][:-64])
+    with pytest.raises(L.LPCNetError):
+        b.synthesize(np.zeros((2, 20), np.float32))  # no model bound
+
+
+def test_full_size_properties(require_gpu, blobs):
+    """At the bench size (1024 streams): determinism across runs, stream
+    independence (permuting the batch permutes the output), sane PCM."""
+    B, F = 1024, 4
+    blob = blobs["streams_int8"]
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    perm = np.random.default_rng(3).permutation(B)
+    b1 = L.LPCNetBatch(B, 0, blob)
+    o1 = np.stack([b1.synthesize(allf[f]) for f in range(F)], 1)
+    b2 = L.LPCNetBatch(B, 0, blob)
+    o2 = np.stack([b2.synthesize(allf[f][perm]) for f in range(F)], 1)
+    assert np.array_equal(o1[perm], o2)
+    b1.reset()
+    o3 = np.stack([b1.synthesize(allf[f]) for f in range(F)], 1)
+    assert np.array_equal(o1, o3)
+    assert np.abs(o1[:, 2:].astype(np.float64)).mean() > 100

@@ -1,0 +1,80 @@
+"""Host-side checks that need no GPU: the C-ABI library loads and exports every
+symbol declared in include/*.h, the engine's host LPC matches the reference's
+lpc_from_cepstrum golden vectors, the rcpps table, and the synthetic
+generator's determinism."""
+import hashlib
+import os
+import re
+
+import numpy as np
+
+import lpcnet_amd as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+K = np.load(os.path.join(ROOT, "tests", "golden", "kernels.npz"))
+
+
+def declared_symbols():
+    syms = []
+    for h in ("lpcnet.h", "lpcnet_mi355x.h"):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        syms += re.findall(r"^LPCNET_EXPORT[^;(]*?\b(\w+)\s*\(", txt, re.M)
+    return syms
+
+
+def test_library_exports_every_declared_symbol():
+    syms = declared_symbols()
+    assert len(syms) >= 30
+    for s in syms:
+        assert hasattr(L.lib, s), s
+
+
+def test_reference_api_subset_present():
+    for s in ("lpcnet_get_size", "lpcnet_init", "lpcnet_create", "lpcnet_destroy", "lpcnet_reset",
+              "lpcnet_synthesize", "lpcnet_load_model"):
+        assert s in declared_symbols()
+
+
+def test_host_lpc_bit_exact_vs_reference():
+    ceps = np.ascontiguousarray(K["lpc_ceps"], np.float32)
+    for k in range(len(ceps)):
+        got = L.lpc_from_cepstrum(ceps[k])
+        assert np.array_equal(got.view(np.uint32), K["lpc_out"][k].view(np.uint32)), k
+
+
+def test_rcp_table_matches_fixture():
+    tab = np.fromfile(os.path.join(ROOT, "tests", "golden", "rcp_x86.bin"), np.uint32)
+    assert np.array_equal(L.rcp_table(), tab)
+
+
+def test_synthetic_model_deterministic_and_layout():
+    a = L.synthetic_model(1, L.VARIANT_INT8)
+    b = L.synthetic_model(1, L.VARIANT_INT8)
+    c = L.synthetic_model(2, L.VARIANT_INT8)
+    assert a == b and a != c
+    G = np.load(os.path.join(ROOT, "tests", "golden", "streams_int8.npz"))
+    assert hashlib.sha256(a).digest() == G["blob_sha256"].tobytes()
+    # every record: 64-byte WeightHead, 64-aligned payload (nnet.h:54-61)
+    off, names = 0, []
+    while off < len(a):
+        assert a[off:off + 4] == b"DNNw"
+        size, block = np.frombuffer(a[off + 12:off + 20], np.int32)
+        assert block % 64 == 0 and block >= size
+        names.append(a[off + 20:off + 64].split(b"\0")[0].decode())
+        off += 64 + int(block)
+    assert off == len(a)
+    assert "sparse_gru_a_recurrent_weights_idx" in names and "dual_fc_factor" in names
+
+
+def test_synthetic_features_shape():
+    f = L.synthetic_features(3, 5)
+    assert f.shape == (5, 36) and np.all(f[:, 20:] == 0)
+    assert np.all((f[:, 18] >= -1.3) & (f[:, 18] <= 1.5))
+
+
+def test_batch_create_fails_cleanly_without_device():
+    if L.device_count() > 0:
+        return
+    import pytest
+    with pytest.raises(L.LPCNetError):
+        L.LPCNetBatch(4)
