@@ -459,7 +459,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
     {
       float inz[S], inr[S], inh[S];
       for (int s = 0; s < S; s++) {
-        const int sig = ix[s * 4 + 0], prd = ix[s * 4 + 1], exc = ix[s * 4 + 2];
+        const int sig = ix[s * 4 + 0] & 0xFF, prd = ix[s * 4 + 1] & 0xFF, exc = ix[s * 4 + 2] & 0xFF;
         const float *e1 = A.emb_sig + sig * GA_ROWS, *e2 = A.emb_pred + prd * GA_ROWS, *e3 = A.emb_exc + exc * GA_ROWS;
         inz[s] = ((cz[s] + e1[i]) + e2[i]) + e3[i];
         inr[s] = ((cr[s] + e1[NA + i]) + e2[NA + i]) + e3[NA + i];
