@@ -183,6 +183,8 @@ def main():
                      "kernel": "sample_kernel", "avg_launch_ms": sample_ms, "launches": kn,
                      "algorithmic_bytes_per_launch": bytes_launch},
         "frame_kernel_avg_ms": fs / max(fn, 1),
+        "kernel_config": {"streams_per_workgroup": info.streams_per_workgroup, "quad_path": info.quad_path,
+                          "lds_bytes": info.lds_bytes, "gru_a_blocks": info.gru_a_blocks},
         "pcm_checksum": int(np.abs(pcm[-1].astype(np.int64)).sum()),
     }
     if rank == 0 and world == 1 and not args.no_batch1:

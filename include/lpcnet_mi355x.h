@@ -32,6 +32,9 @@ typedef struct {
   double bytes_shared_per_sample; /* algorithmic weight bytes read once per sample step */
   double bytes_per_stream_sample; /* per-stream bytes per sample (gathers, trace-free) */
   double ops_per_sample;          /* 2*MAC per stream per sample */
+  int streams_per_workgroup;      /* S of the sample kernel */
+  int quad_path;                  /* 1: int8 weights as per-lane uint4 quads in LDS */
+  int lds_bytes;                  /* dynamic LDS of the sample kernel */
 } LPCNetModelInfo;
 
 /* Create a batch of nb_streams streams on HIP device `device`.

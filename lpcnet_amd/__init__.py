@@ -89,7 +89,8 @@ class ModelInfo(C.Structure):
     _fields_ = [("variant", C.c_int), ("gru_a_blocks", C.c_int), ("gru_b_blocks", C.c_int),
                 ("may_saturate", C.c_int), ("bytes_shared_per_frame", C.c_double),
                 ("bytes_shared_per_sample", C.c_double), ("bytes_per_stream_sample", C.c_double),
-                ("ops_per_sample", C.c_double)]
+                ("ops_per_sample", C.c_double), ("streams_per_workgroup", C.c_int), ("quad_path", C.c_int),
+                ("lds_bytes", C.c_int)]
 
 
 def last_error() -> str:

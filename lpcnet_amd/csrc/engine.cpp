@@ -285,6 +285,7 @@ struct LPCNetBatch {
   bool have_model = false;
   int variant = 0;
   bool sat = false;
+  bool reg = false;
   LPCNetModelInfo info{};
   std::vector<void *> model_bufs;
   FrameArgs fa{};
@@ -479,10 +480,56 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   memset(&sa, 0, sizeof(sa));
   std::vector<float4> ga_wf, gb_wf_unused;
   if (int8) sa.gb_rec_off = (int)put(gbrec, 3 * NB * NB);
+  /* blocks per lane for each (wave, gate) of the GRU_A layout */
+  int gaK[SAMPLE_WAVES][3];
+  bool reg = int8;
+  for (int w = 0; w < SAMPLE_WAVES; w++)
+    for (int g = 0; g < 3; g++) {
+      int K = 0;
+      for (int j = 0; j < 8; j++) K = std::max(K, (int)ga_blocks[g * (NA / 8) + w * 8 + j].size());
+      gaK[w][g] = K;
+      if (K > 96) reg = false;
+    }
+  for (int rb = 0; rb < GB_ROWS / 8; rb++)
+    if ((int)gb_blocks[rb].size() > 8 * REG_GB) reg = false;
+  if (getenv("LPCNET_NO_QUAD")) reg = false; /* A/B switch: per-slot LDS layout */
+  if (reg) {
+    /* quad layout: wave w, gate g, group gi of 4 slots, lane l = 8*(row block in wave) + row */
+    for (int w = 0; w < SAMPLE_WAVES; w++)
+      for (int g = 0; g < 3; g++) {
+        const int K4 = (gaK[w][g] + 3) / 4;
+        sa.ga_K4[w][g] = K4;
+        std::vector<uint32_t> q((size_t)std::max(K4, 1) * 64 * 4, 0), c((size_t)std::max(K4, 1) * 8, 0);
+        for (int l = 0; l < 64; l++) {
+          const int j = l >> 3, r = l & 7, rb = g * (NA / 8) + w * 8 + j;
+          for (int k = 0; k < (int)ga_blocks[rb].size(); k++) {
+            memcpy(&q[((size_t)(k / 4) * 64 + l) * 4 + (k & 3)], (const int8_t *)gaw->data + 32 * (ga_first[rb] + k) + 4 * r, 4);
+            if (r == 0) c[(k / 4) * 8 + j] |= (uint32_t)(ga_blocks[rb][k] / 4) << (8 * (k & 3));
+          }
+        }
+        sa.ga_qoff[w][g] = (int)(put(q.data(), q.size() * 4) / 16);
+        sa.ga_coff[w][g] = (int)(put(c.data(), c.size() * 4) / 4);
+      }
+    for (int rb = 0; rb < GB_ROWS / 8; rb++) {
+      std::vector<uint32_t> q((size_t)(REG_GB / 4) * 64 * 4, 0), c((size_t)(REG_GB / 4) * 8, 0);
+      for (int l = 0; l < 64; l++) {
+        const int r = l & 7, ks = l >> 3;
+        for (int j = 0; j < REG_GB; j++) {
+          const int k = ks + 8 * j;
+          if (k >= (int)gb_blocks[rb].size()) continue;
+          memcpy(&q[((size_t)(j / 4) * 64 + l) * 4 + (j & 3)], (const int8_t *)gbw + 32 * (gb_first[rb] + k) + 4 * r, 4);
+          if (r == 0) c[(j / 4) * 8 + ks] |= (uint32_t)(gb_blocks[rb][k] / 4) << (8 * (j & 3));
+        }
+      }
+      sa.gb_qoff[rb] = (int)(put(q.data(), q.size() * 4) / 16);
+      sa.gb_coff[rb] = (int)(put(c.data(), c.size() * 4) / 4);
+    }
+  }
   /* GRU_B input blocks: [rb][k][row] (u32 int8 row quads | float4 fp32 rows) */
   for (int rb = 0; rb < GB_ROWS / 8; rb++) {
     int nb = (int)gb_blocks[rb].size();
     sa.gb_nb[rb] = nb;
+    if (reg) continue;
     if (int8) {
       std::vector<uint32_t> w(nb * 8);
       for (int k = 0; k < nb; k++)
@@ -500,12 +547,10 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
     for (int k = 0; k < nb; k++) cbs[k] = (uint16_t)(gb_blocks[rb][k] / 4);
     sa.gb_coff[rb] = (int)(put(cbs.data(), cbs.size() * 2) / 2);
   }
-  /* GRU_A blocks: per (wave, gate) chunk [k][64 lanes], lane = 8*(row block in wave) + row */
-  size_t ga_slots = 0;
-  for (int w = 0; w < SAMPLE_WAVES; w++)
+  /* GRU_A blocks (LDS / fp32 global path): per (wave, gate) chunk [k][64 lanes] */
+  for (int w = 0; w < SAMPLE_WAVES && !reg; w++)
     for (int g = 0; g < 3; g++) {
-      int K = 0;
-      for (int j = 0; j < 8; j++) K = std::max(K, (int)ga_blocks[g * (NA / 8) + w * 8 + j].size());
+      int K = gaK[w][g];
       sa.ga_K[w][g] = K;
       std::vector<uint16_t> cbs(K * 8, int8 ? 0 : 0xFFFF);
       std::vector<uint32_t> wq(int8 ? K * 64 : 0, 0);
@@ -529,7 +574,6 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
       if (int8) sa.ga_woff[w][g] = (int)(put(wq.data(), wq.size() * 4) / 4);
       else sa.ga_woff[w][g] = (int)fbase;
       sa.ga_coff[w][g] = (int)(put(cbs.data(), cbs.size() * 2) / 2);
-      ga_slots += K;
     }
   align16();
 
@@ -579,6 +623,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   sa.image_bytes = (int)img.size();
   b->variant = variant;
   b->sat = sat;
+  b->reg = reg;
   b->S = S;
   b->lds_bytes = lds;
   b->have_model = true;
@@ -589,6 +634,9 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   in.gru_a_blocks = nba;
   in.gru_b_blocks = nbb;
   in.may_saturate = sat ? 1 : 0;
+  in.streams_per_workgroup = S;
+  in.quad_path = reg ? 1 : 0;
+  in.lds_bytes = lds;
   double frame_w = (3.0 * FIN * COND + 3.0 * COND * COND + 2.0 * COND * COND + COND * GA_ROWS + COND * GB_ROWS) * 4 +
                    (2.0 * COND + 2 * COND + GA_ROWS + GB_ROWS) * 4 + EP * 4;
   double wbytes = int8 ? 1 : 4;
@@ -598,7 +646,6 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   in.bytes_per_stream_sample = 3.0 * GA_ROWS * 4 /* embedding rows */ + 8 * (32 + 2 * 4 + 2 * 4) /* dual_fc path */ + 2;
   in.ops_per_sample = 2.0 * (32.0 * nba + 32.0 * nbb + 3 * NB * NB + 8 * 2 * NB + NLPC) +
                       2.0 * (3.0 * FIN * COND + 3.0 * COND * COND + 2.0 * COND * COND + COND * GA_ROWS + COND * GB_ROWS) / FRAME;
-  (void)ga_slots;
   return 0;
 }
 
@@ -647,7 +694,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   if (launch_frame(fa, b->stream)) { set_err("frame kernel launch failed"); return -1; }
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
-  if (launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->lds_bytes, b->stream)) {
+  if (launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream)) {
     set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     return -1;
   }

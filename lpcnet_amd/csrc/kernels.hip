@@ -340,7 +340,73 @@ int sample_lds_bytes(int S, int variant, int image_bytes)
   return image_bytes + extra;
 }
 
-template <int S, int V, bool SAT>
+/* x quads of the S streams for one column block: S dot4 accumulations */
+template <int S, bool SAT>
+__device__ __forceinline__ void dot_streams(const unsigned char *xa, int off, uint32_t w, int *acc)
+{
+  if constexpr (S == 4) {
+    uint4 xv = *(const uint4 *)(xa + off);
+    acc[0] = dot4<SAT>(w, xv.x, acc[0]);
+    acc[1] = dot4<SAT>(w, xv.y, acc[1]);
+    acc[2] = dot4<SAT>(w, xv.z, acc[2]);
+    acc[3] = dot4<SAT>(w, xv.w, acc[3]);
+  } else if constexpr (S == 2) {
+    uint2 xv = *(const uint2 *)(xa + off);
+    acc[0] = dot4<SAT>(w, xv.x, acc[0]);
+    acc[1] = dot4<SAT>(w, xv.y, acc[1]);
+  } else {
+    acc[0] = dot4<SAT>(w, *(const uint32_t *)(xa + off), acc[0]);
+  }
+}
+
+/* x quad type for S streams of one column block */
+template <int S> struct XQ { using T = uint32_t; };
+template <> struct XQ<2> { using T = uint2; };
+template <> struct XQ<4> { using T = uint4; };
+
+template <int S, bool SAT>
+__device__ __forceinline__ void dot_x(const typename XQ<S>::T &x, uint32_t w, int *acc)
+{
+  if constexpr (S == 4) {
+    acc[0] = dot4<SAT>(w, x.x, acc[0]);
+    acc[1] = dot4<SAT>(w, x.y, acc[1]);
+    acc[2] = dot4<SAT>(w, x.z, acc[2]);
+    acc[3] = dot4<SAT>(w, x.w, acc[3]);
+  } else if constexpr (S == 2) {
+    acc[0] = dot4<SAT>(w, x.x, acc[0]);
+    acc[1] = dot4<SAT>(w, x.y, acc[1]);
+  } else {
+    acc[0] = dot4<SAT>(w, x, acc[0]);
+  }
+}
+
+/* Quad-path gate: K4 groups of 4 slots.  Group g of this lane: its four
+ * weight quads are one uint4 (wq[qoff + g*64 + lane]) and the four column
+ * blocks one u32 shared by the 8 lanes of a row block (cq[coff + g*8 + rb]),
+ * so the dependent LDS round trip (index -> x) is paid once per 4 slots. */
+template <int S, bool SAT>
+__device__ __forceinline__ void gate_quad(const unsigned char *xa, const uint4 *wq, const uint32_t *cq, int qoff,
+                                          int coff, int K4, int lane, int *acc)
+{
+  using X = typename XQ<S>::T;
+  const uint4 *wp = wq + qoff + lane;
+  const uint32_t *cp = cq + coff + (lane >> 3);
+#pragma unroll 2
+  for (int g = 0; g < K4; g++) {
+    const uint4 w = wp[g * 64];
+    const uint32_t c = cp[g * 8];
+    const X x0 = *(const X *)(xa + (c & 0xFF) * (S * 4));
+    const X x1 = *(const X *)(xa + ((c >> 8) & 0xFF) * (S * 4));
+    const X x2 = *(const X *)(xa + ((c >> 16) & 0xFF) * (S * 4));
+    const X x3 = *(const X *)(xa + (c >> 24) * (S * 4));
+    dot_x<S, SAT>(x0, w.x, acc);
+    dot_x<S, SAT>(x1, w.y, acc);
+    dot_x<S, SAT>(x2, w.z, acc);
+    dot_x<S, SAT>(x3, w.w, acc);
+  }
+}
+
+template <int S, int V, bool SAT, bool REG>
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
 {
   extern __shared__ uint4 lds4[];
@@ -381,6 +447,10 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
 
   /* weights and tables -> LDS */
   for (int o = tid; o < A.image_bytes / 16; o += SAMPLE_THREADS) lds4[o] = A.image[o];
+
+  const int K4z = REG ? A.ga_K4[wv][0] : 0, K4r = REG ? A.ga_K4[wv][1] : 0, K4h = REG ? A.ga_K4[wv][2] : 0;
+  const uint4 *wq = (const uint4 *)lds;
+  const uint32_t *cq = (const uint32_t *)lds;
 
   /* GRU_A unit state and constants: thread tid owns unit i = tid */
   const int i = tid;
@@ -428,9 +498,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
     if (stream_wave && lane < NB) sbuf[my_s * NB + lane] = sbv;
   }
 
-  /* per-stream scalar step that precedes every sample: pred, u-law indices, RNG */
+  /* per-stream step between samples: pred and the u-law indices (lpcnet.c:252-254) */
   auto pre_sample = [&]() {
-    /* pred = -sum last_sig[j]*lpc[j], sequential (lpcnet.c:252); lane j holds the j-th product */
+    /* pred = -sum last_sig[j]*lpc[j], sequential; lane j holds the j-th product */
     float prod = ls * lp;
     float p2 = 0.f;
 #pragma unroll
@@ -442,13 +512,10 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
       ix[my_s * 4 + 1] = lin2ulaw_x86(pred);
       ix[my_s * 4 + 2] = last_exc;
     }
-    r0 = kiss99_next(rz, rw, rj, rc);
-    r1 = kiss99_next(rz, rw, rj, rc);
   };
   if (stream_wave) pre_sample();
   __syncthreads();
 
-  /* GRU_A per-gate LDS chunks for this wave */
   const uint32_t *lds32 = (const uint32_t *)lds;
   const uint16_t *lds16 = (const uint16_t *)lds;
   const int j8 = lane >> 3;
@@ -457,58 +524,62 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
     const int cur = n & 1;
     /* ---- phase B: GRU_A (nnet.c:484-491 + 410-448) ---------------------- */
     {
-      float inz[S], inr[S], inh[S];
+      /* the two kiss99 draws of this sample (sample_mdense, nnet.c:178-184) */
+      if (stream_wave) {
+        r0 = kiss99_next(rz, rw, rj, rc);
+        r1 = kiss99_next(rz, rw, rj, rc);
+      }
+      /* embedding gathers issued first; consumed after the recurrent matvec */
+      float e1z[S], e1r[S], e1h[S], e2z[S], e2r[S], e2h[S], e3z[S], e3r[S], e3h[S];
       for (int s = 0; s < S; s++) {
         const int sig = ix[s * 4 + 0] & 0xFF, prd = ix[s * 4 + 1] & 0xFF, exc = ix[s * 4 + 2] & 0xFF;
         const float *e1 = A.emb_sig + sig * GA_ROWS, *e2 = A.emb_pred + prd * GA_ROWS, *e3 = A.emb_exc + exc * GA_ROWS;
-        inz[s] = ((cz[s] + e1[i]) + e2[i]) + e3[i];
-        inr[s] = ((cr[s] + e1[NA + i]) + e2[NA + i]) + e3[NA + i];
-        inh[s] = ((ch[s] + e1[2 * NA + i]) + e2[2 * NA + i]) + e3[2 * NA + i];
+        e1z[s] = e1[i]; e1r[s] = e1[NA + i]; e1h[s] = e1[2 * NA + i];
+        e2z[s] = e2[i]; e2r[s] = e2[NA + i]; e2h[s] = e2[2 * NA + i];
+        e3z[s] = e3[i]; e3r[s] = e3[NA + i]; e3h[s] = e3[2 * NA + i];
       }
-      float gz[S], gr[S], gh[S];
+      float gz[S], gr[S], gh[S], inh[S];
       if constexpr (V == 0) {
+        /* integer part first: the seed (which needs the gathers) is added after,
+         * int32 addition being associative */
         int az[S], ar[S], ah[S];
         for (int s = 0; s < S; s++) {
-          az[s] = cvt_rne(((bz + dz * st[s]) + inz[s]) * kScale) + (SAT ? 0 : wsz);
-          ar[s] = cvt_rne(((br + dr * st[s]) + inr[s]) * kScale) + (SAT ? 0 : wsr);
-          ah[s] = cvt_rne((bh + dh * st[s]) * kScale) + (SAT ? 0 : wsh);
+          az[s] = SAT ? 0 : wsz;
+          ar[s] = SAT ? 0 : wsr;
+          ah[s] = SAT ? 0 : wsh;
         }
         const unsigned char *xa = xa_base + cur * (NA / 4) * S * 4;
-        auto run_gate = [&](int g, int *acc) {
-          const uint32_t *wp = lds32 + A.ga_woff[wv][g] + lane;
-          const uint16_t *cp = lds16 + A.ga_coff[wv][g] + j8;
-          const int K = A.ga_K[wv][g];
+        if constexpr (REG) {
+          gate_quad<S, SAT>(xa, wq, cq, A.ga_qoff[wv][0], A.ga_coff[wv][0], K4z, lane, az);
+          gate_quad<S, SAT>(xa, wq, cq, A.ga_qoff[wv][1], A.ga_coff[wv][1], K4r, lane, ar);
+          gate_quad<S, SAT>(xa, wq, cq, A.ga_qoff[wv][2], A.ga_coff[wv][2], K4h, lane, ah);
+        } else {
+          auto run_gate = [&](int g, int *acc) {
+            const uint32_t *wp = lds32 + A.ga_woff[wv][g] + lane;
+            const uint16_t *cp = lds16 + A.ga_coff[wv][g] + j8;
+            const int K = A.ga_K[wv][g];
 #pragma unroll 4
-          for (int k = 0; k < K; k++) {
-            uint32_t w = wp[k * 64];
-            int off = cp[k * 8] * (S * 4);
-            if constexpr (S == 4) {
-              uint4 xv = *(const uint4 *)(xa + off);
-              acc[0] = dot4<SAT>(w, xv.x, acc[0]);
-              acc[1] = dot4<SAT>(w, xv.y, acc[1]);
-              acc[2] = dot4<SAT>(w, xv.z, acc[2]);
-              acc[3] = dot4<SAT>(w, xv.w, acc[3]);
-            } else if constexpr (S == 2) {
-              uint2 xv = *(const uint2 *)(xa + off);
-              acc[0] = dot4<SAT>(w, xv.x, acc[0]);
-              acc[1] = dot4<SAT>(w, xv.y, acc[1]);
-            } else {
-              acc[0] = dot4<SAT>(w, *(const uint32_t *)(xa + off), acc[0]);
-            }
-          }
-        };
-        run_gate(0, az);
-        run_gate(1, ar);
-        run_gate(2, ah);
+            for (int k = 0; k < K; k++) dot_streams<S, SAT>(xa, cp[k * 8] * (S * 4), wp[k * 64], acc);
+          };
+          run_gate(0, az);
+          run_gate(1, ar);
+          run_gate(2, ah);
+        }
         for (int s = 0; s < S; s++) {
-          gz[s] = (float)az[s] * kScale1;
-          gr[s] = (float)ar[s] * kScale1;
-          gh[s] = (float)ah[s] * kScale1;
+          const float inz = ((cz[s] + e1z[s]) + e2z[s]) + e3z[s];
+          const float inr = ((cr[s] + e1r[s]) + e2r[s]) + e3r[s];
+          inh[s] = ((ch[s] + e1h[s]) + e2h[s]) + e3h[s];
+          gz[s] = (float)(az[s] + cvt_rne(((bz + dz * st[s]) + inz) * kScale)) * kScale1;
+          gr[s] = (float)(ar[s] + cvt_rne(((br + dr * st[s]) + inr) * kScale)) * kScale1;
+          gh[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
         }
       } else {
         for (int s = 0; s < S; s++) {
-          gz[s] = (bz + dz * st[s]) + inz[s];
-          gr[s] = (br + dr * st[s]) + inr[s];
+          const float inz = ((cz[s] + e1z[s]) + e2z[s]) + e3z[s];
+          const float inr = ((cr[s] + e1r[s]) + e2r[s]) + e3r[s];
+          inh[s] = ((ch[s] + e1h[s]) + e2h[s]) + e3h[s];
+          gz[s] = (bz + dz * st[s]) + inz;
+          gr[s] = (br + dr * st[s]) + inr;
           gh[s] = bh + dh * st[s];
         }
         const float4 *xf = (const float4 *)(xa_base + cur * (NA / 4) * S * 16);
@@ -557,17 +628,18 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
         const unsigned char *xa = xa_base + nxt * (NA / 4) * S * 4;
         int acc[S], accr[S];
         for (int s = 0; s < S; s++) { acc[s] = 0; accr[s] = 0; }
-        const uint32_t *wp = lds32 + A.gb_woff[rb];
-        const uint16_t *cp = lds16 + A.gb_coff[rb];
-        const int nb = A.gb_nb[rb];
-        for (int k = ks; k < nb; k += 8) {
-          uint32_t w = wp[k * 8 + r];
-          int off = cp[k] * (S * 4);
-          for (int s = 0; s < S; s++) acc[s] = dot4<SAT>(w, *(const uint32_t *)(xa + off + s * 4), acc[s]);
+        if constexpr (REG) {
+          gate_quad<S, SAT>(xa, wq, cq, A.gb_qoff[rb], A.gb_coff[rb], REG_GB / 4, lane, acc);
+        } else {
+          const uint32_t *wp = lds32 + A.gb_woff[rb];
+          const uint16_t *cp = lds16 + A.gb_coff[rb];
+          const int nb = A.gb_nb[rb];
+#pragma unroll 4
+          for (int k = ks; k < nb; k += 8) dot_streams<S, SAT>(xa, cp[k] * (S * 4), wp[k * 8 + r], acc);
         }
         if (ks < NB / 4) {
           uint32_t w = ((const uint32_t *)(lds + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r];
-          for (int s = 0; s < S; s++) accr[s] = dot4<SAT>(w, *(const uint32_t *)(xb + ks * S * 4 + s * 4), accr[s]);
+          dot_streams<S, SAT>(xb, ks * S * 4, w, accr);
         }
         for (int s = 0; s < S; s++) {
           acc[s] += __shfl_xor(acc[s], 8);
@@ -656,17 +728,15 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
         }
       }
       {
-        /* levels 4..7 under the chosen prefix: 1 + 2 + 4 + 8 nodes */
+        /* levels 4..7 under the chosen 4-bit prefix: 1 + 2 + 4 + 8 nodes */
         int qq = q < 15 ? q : 0;
         int lvl = qq == 0 ? 4 : (qq < 3 ? 5 : (qq < 7 ? 6 : 7));
         int off = qq + 1 - (1 << (lvl - 4));
         int node = (1 << lvl) | (val << (lvl - 4)) | off;
         float l = node_logit(node);
-        const int base = val;
 #pragma unroll
         for (int b = 4; b < 8; b++) {
           int o = val & ((1 << (b - 4)) - 1);
-          (void)base;
           int qi = (1 << (b - 4)) - 1 + o;
           float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), 2 * qi));
           lg[b] = v;
@@ -695,7 +765,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
         if (lane < NB) xb[(lane >> 2) * S * 4 + s * 4 + (lane & 3)] = (unsigned char)quant_s8(sbv);
       }
       if (lane < NB) sbuf[s * NB + lane] = sbv;
-      if (n + 1 < A.N) pre_sample(); /* exactly two kiss99 draws per sample */
+      if (n + 1 < A.N) pre_sample();
     }
     __syncthreads();
   }
@@ -729,37 +799,35 @@ int launch_frame(const FrameArgs &a, void *stream)
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int S, int V, bool SAT>
+template <int S, int V, bool SAT, bool REG>
 static int launch_sample_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
 {
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)sample_kernel<S, V, SAT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-        hipSuccess)
+    if (hipFuncSetAttribute((const void *)sample_kernel<S, V, SAT, REG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
       return -1;
     attr_set = true;
   }
   int grid = (a.nstreams + S - 1) / S;
-  hipLaunchKernelGGL((sample_kernel<S, V, SAT>), dim3(grid), dim3(SAMPLE_THREADS), lds_bytes, stream, a);
+  hipLaunchKernelGGL((sample_kernel<S, V, SAT, REG>), dim3(grid), dim3(SAMPLE_THREADS), lds_bytes, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_sample(const SampleArgs &a, int S, int variant, int sat, int lds_bytes, void *stream)
+template <int S>
+static int launch_s(const SampleArgs &a, int variant, int sat, int reg, int lds_bytes, hipStream_t st)
+{
+  if (variant == 1) return launch_sample_t<S, 1, false, false>(a, lds_bytes, st);
+  if (sat) return reg ? launch_sample_t<S, 0, true, true>(a, lds_bytes, st) : launch_sample_t<S, 0, true, false>(a, lds_bytes, st);
+  return reg ? launch_sample_t<S, 0, false, true>(a, lds_bytes, st) : launch_sample_t<S, 0, false, false>(a, lds_bytes, st);
+}
+
+int launch_sample(const SampleArgs &a, int S, int variant, int sat, int reg, int lds_bytes, void *stream)
 {
   hipStream_t st = (hipStream_t)stream;
-  if (variant == 0) {
-    if (sat) {
-      if (S == 4) return launch_sample_t<4, 0, true>(a, lds_bytes, st);
-      if (S == 2) return launch_sample_t<2, 0, true>(a, lds_bytes, st);
-      return launch_sample_t<1, 0, true>(a, lds_bytes, st);
-    }
-    if (S == 4) return launch_sample_t<4, 0, false>(a, lds_bytes, st);
-    if (S == 2) return launch_sample_t<2, 0, false>(a, lds_bytes, st);
-    return launch_sample_t<1, 0, false>(a, lds_bytes, st);
-  }
-  if (S == 4) return launch_sample_t<4, 1, false>(a, lds_bytes, st);
-  if (S == 2) return launch_sample_t<2, 1, false>(a, lds_bytes, st);
-  return launch_sample_t<1, 1, false>(a, lds_bytes, st);
+  if (S == 4) return launch_s<4>(a, variant, sat, reg, lds_bytes, st);
+  if (S == 2) return launch_s<2>(a, variant, sat, reg, lds_bytes, st);
+  return launch_s<1>(a, variant, sat, reg, lds_bytes, st);
 }
 
 }  // namespace lpcnet_mi355x

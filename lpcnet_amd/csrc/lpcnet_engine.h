@@ -27,6 +27,7 @@ constexpr int SAMPLE_THREADS = 384; /* one thread per GRU_A unit */
 constexpr int SAMPLE_WAVES = SAMPLE_THREADS / 64;
 constexpr int FRAME_THREADS = 256;
 constexpr int FRAME_STREAMS = 4;    /* streams per frame-network workgroup */
+constexpr int REG_GB = 12;          /* GRU_B input slots per lane: block k = ks + 8*j, j < 12 */
 
 /* Per-stream synthesis state in device memory (lpcnet_private.h:28-48). */
 struct alignas(16) StreamState {
@@ -86,6 +87,12 @@ struct SampleArgs {
   int gb_woff[GB_ROWS / 8];    /* u32 units in image [k][8] / float4 [k][8][2] in gb_wf */
   int gb_coff[GB_ROWS / 8];    /* u16 units in image */
   int gb_rec_off;              /* byte offset of GRU_B recurrent int8 weights in image */
+  /* quad int8 path (LDS image): per wave w / GRU_B row block, group of 4 slots gi:
+   * weights [gi][64 lanes] uint4 at *_qoff (uint4 units), column blocks
+   * [gi][8] u32 (4 x u8, one per lane octet) at *_coff (u32 units) */
+  int ga_K4[SAMPLE_WAVES][3];
+  int ga_qoff[SAMPLE_WAVES][3];
+  int gb_qoff[GB_ROWS / 8];
   const float4 *ga_wf;   /* fp32 variant: GRU_A blocks [chunk][k][64] float4 */
   const float4 *gb_wf;   /* fp32 variant: GRU_B blocks [rb][k][8 rows][2] float4 (in c) */
   const float *gb_recf;  /* fp32 variant: GRU_B recurrent [NB][GB_ROWS] */
@@ -97,7 +104,7 @@ struct SampleArgs {
  * may saturate. lds_bytes from sample_lds_bytes(). */
 int sample_lds_bytes(int S, int variant, int image_bytes);
 int launch_frame(const FrameArgs &a, void *stream);
-int launch_sample(const SampleArgs &a, int S, int variant, int sat, int lds_bytes, void *stream);
+int launch_sample(const SampleArgs &a, int S, int variant, int sat, int reg, int lds_bytes, void *stream);
 
 /* Host LPC (lpc_host.cpp). */
 float lpc_from_cepstrum_host(float *lpc, const float *ceps);
