@@ -54,6 +54,19 @@ LPCNET_EXPORT int lpcnet_batch_nb_streams(const LPCNetBatch *b);
  * Returns 0, or -1 on error (no model, bad N). */
 LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features, short *pcm, int N);
 
+/* lpcnet_synthesize_impl (src/lpcnet.c:273-277, the PLC entry point): as
+ * above, but the first `preload` samples of every stream are teacher-forced
+ * from pcm (input), exactly as lpcnet.c:256-259; pcm[s][preload..N) is output.
+ * N == 0 runs only the frame network (run_frame_network_flush, lpcnet.c:134). */
+LPCNET_EXPORT int lpcnet_batch_synthesize_impl(LPCNetBatch *b, const float *features, short *pcm, int N, int preload);
+
+/* Snapshot / restore of one stream's complete synthesis state (the struct
+ * copies lpcnet_plc.c:223,230 make for speculation).  buf holds
+ * lpcnet_batch_state_size() bytes. */
+LPCNET_EXPORT int lpcnet_batch_state_size(void);
+LPCNET_EXPORT int lpcnet_batch_save_state(LPCNetBatch *b, int stream, void *buf);
+LPCNET_EXPORT int lpcnet_batch_restore_state(LPCNetBatch *b, int stream, const void *buf);
+
 /* nframes consecutive frames for every stream with device-resident I/O:
  * d_features [nframes][B][NB_FEATURES] and d_pcm [nframes][B][N] are device
  * pointers on the batch's device.  h_features holds the same features on the

@@ -57,6 +57,10 @@ def _load():
         "lpcnet_batch_reset_stream": (i, [vp, i]),
         "lpcnet_batch_nb_streams": (i, [vp]),
         "lpcnet_batch_synthesize": (i, [vp, vp, vp, i]),
+        "lpcnet_batch_synthesize_impl": (i, [vp, vp, vp, i, i]),
+        "lpcnet_batch_state_size": (i, []),
+        "lpcnet_batch_save_state": (i, [vp, i, vp]),
+        "lpcnet_batch_restore_state": (i, [vp, i, vp]),
         "lpcnet_batch_synthesize_frames": (i, [vp, vp, vp, vp, i, i]),
         "lpcnet_batch_sync": (i, [vp]),
         "lpcnet_batch_device_alloc": (vp, [vp, C.c_size_t]),
@@ -200,6 +204,31 @@ class LPCNetBatch:
         if lib.lpcnet_batch_synthesize(self._b, f.ctypes.data, out.ctypes.data, n) != 0:
             raise LPCNetError(last_error())
         return out
+
+    def synthesize_impl(self, features: np.ndarray, pcm: np.ndarray, preload: int) -> np.ndarray:
+        """lpcnet_synthesize_impl: pcm [B, N] int16, first ``preload`` samples teacher-forced."""
+        f = np.ascontiguousarray(np.asarray(features, np.float32)[:, :NB_FEATURES])
+        out = np.ascontiguousarray(pcm, np.int16).copy()
+        n = out.shape[1] if out.ndim == 2 else 0
+        if lib.lpcnet_batch_synthesize_impl(self._b, f.ctypes.data, out.ctypes.data if n else None, n, preload) != 0:
+            raise LPCNetError(last_error())
+        return out
+
+    def frame_only(self, features: np.ndarray) -> None:
+        """run_frame_network without samples (lpcnet.c:134 run_frame_network_flush)."""
+        f = np.ascontiguousarray(np.asarray(features, np.float32)[:, :NB_FEATURES])
+        if lib.lpcnet_batch_synthesize_impl(self._b, f.ctypes.data, None, 0, 0) != 0:
+            raise LPCNetError(last_error())
+
+    def save_state(self, stream: int) -> bytes:
+        buf = C.create_string_buffer(lib.lpcnet_batch_state_size())
+        if lib.lpcnet_batch_save_state(self._b, stream, buf) != 0:
+            raise LPCNetError(last_error())
+        return buf.raw
+
+    def restore_state(self, stream: int, state: bytes) -> None:
+        if lib.lpcnet_batch_restore_state(self._b, stream, state) != 0:
+            raise LPCNetError(last_error())
 
     # -- device-resident path (benchmarks) ---------------------------------
     def device_alloc(self, nbytes: int) -> int:

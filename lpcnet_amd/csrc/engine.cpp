@@ -675,7 +675,7 @@ int ensure_trace(LPCNetBatch *b, int N)
   return 0;
 }
 
-int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lpc, short *d_pcm, int N)
+int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lpc, short *d_pcm, int N, int preload = 0)
 {
   FrameArgs fa = b->fa;
   fa.st = b->d_state;
@@ -687,6 +687,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   sa.nstreams = b->B;
   sa.N = N;
   sa.pcm = d_pcm;
+  sa.preload = std::max(0, std::min(preload, N));
   hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
   if (b->timing)
     for (int i = 0; i < 4; i++) e[i] = get_event(b);
@@ -694,7 +695,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   if (launch_frame(fa, b->stream)) { set_err("frame kernel launch failed"); return -1; }
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
-  if (launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream)) {
+  if (N > 0 && launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream)) {
     set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     return -1;
   }
@@ -831,18 +832,43 @@ LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b)
   (void)hipStreamSynchronize(b->stream);
 }
 
-LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features, short *pcm, int N)
+LPCNET_EXPORT int lpcnet_batch_synthesize_impl(LPCNetBatch *b, const float *features, short *pcm, int N, int preload)
 {
   if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
-  if (N < 0 || N > FRAME || !features || !pcm) { set_err("bad arguments"); return -1; }
+  if (N < 0 || N > FRAME || !features || (N > 0 && !pcm) || preload < 0) { set_err("bad arguments"); return -1; }
   if (b->set_device()) return -1;
   if (ensure_trace(b, N)) return -1;
   compute_lpc(b, features, NF, b->h_lpc[0]);
   HIPCHK(hipMemcpyAsync(b->d_lpc[0], b->h_lpc[0], sizeof(float) * NLPC * b->B, hipMemcpyHostToDevice, b->stream));
   HIPCHK(hipMemcpyAsync(b->d_feat, features, sizeof(float) * NF * b->B, hipMemcpyHostToDevice, b->stream));
-  if (launch_frame_step(b, b->d_feat, b->d_lpc[0], b->d_pcm, N)) return -1;
+  if (preload > 0 && N > 0)
+    HIPCHK(hipMemcpyAsync(b->d_pcm, pcm, sizeof(short) * N * b->B, hipMemcpyHostToDevice, b->stream));
+  if (launch_frame_step(b, b->d_feat, b->d_lpc[0], b->d_pcm, N, preload)) return -1;
   if (N > 0) HIPCHK(hipMemcpyAsync(pcm, b->d_pcm, sizeof(short) * N * b->B, hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features, short *pcm, int N)
+{
+  return lpcnet_batch_synthesize_impl(b, features, pcm, N, 0);
+}
+
+LPCNET_EXPORT int lpcnet_batch_state_size(void) { return (int)sizeof(StreamState); }
+
+LPCNET_EXPORT int lpcnet_batch_save_state(LPCNetBatch *b, int stream, void *buf)
+{
+  if (!b || stream < 0 || stream >= b->B || !buf || b->set_device()) return -1;
+  HIPCHK(hipStreamSynchronize(b->stream));
+  HIPCHK(hipMemcpy(buf, &b->d_state[stream], sizeof(StreamState), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_restore_state(LPCNetBatch *b, int stream, const void *buf)
+{
+  if (!b || stream < 0 || stream >= b->B || !buf || b->set_device()) return -1;
+  HIPCHK(hipStreamSynchronize(b->stream));
+  HIPCHK(hipMemcpy(&b->d_state[stream], buf, sizeof(StreamState), hipMemcpyHostToDevice));
   return 0;
 }
 

@@ -513,6 +513,10 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
       ix[my_s * 4 + 2] = last_exc;
     }
   };
+  for (int e = tid; e < S * A.preload; e += SAMPLE_THREADS) {
+    const int s = e / A.preload, n = e % A.preload;
+    pcmbuf[s * FRAME + n] = A.pcm[(size_t)min(s0 + s, A.nstreams - 1) * A.N + n];
+  }
   if (stream_wave) pre_sample();
   __syncthreads();
 
@@ -743,9 +747,18 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
           val = (val << 1) | (thr[b] < v ? 1 : 0);
         }
       }
-      const int exc = val;
-      /* output sample (lpcnet.c:260-269) */
-      float pcm = pred + ulaw[exc];
+      int exc = val;
+      /* output sample (lpcnet.c:256-269) */
+      float pcm;
+      if (n < A.preload) {
+        /* teacher forcing: the caller's PCM replaces the sampled excitation */
+        const float o_in = (float)pcmbuf[s * FRAME + n];
+        const float pd = kPreemph * deemph;
+        exc = lin2ulaw_x86((o_in - pd) - pred);
+        pcm = o_in - pd;
+      } else {
+        pcm = pred + ulaw[exc];
+      }
       float up = __shfl_up(ls, 1);
       ls = lane == 0 ? pcm : up;
       last_exc = exc;
@@ -753,7 +766,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
       deemph = o;
       if (o < -32767) o = -32767;
       if (o > 32767) o = 32767;
-      if (lane == 0) pcmbuf[s * FRAME + n] = (short)(int)floor(.5 + (double)o);
+      if (lane == 0 && n >= A.preload) pcmbuf[s * FRAME + n] = (short)(int)floor(.5 + (double)o);
       if (A.trace_logits && lane < 8 && active[s]) {
         float v = lg[0];
 #pragma unroll

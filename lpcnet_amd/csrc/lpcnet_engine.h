@@ -73,6 +73,7 @@ struct SampleArgs {
   int nstreams;
   int N;                 /* samples to produce (<= FRAME) */
   short *pcm;            /* [B][N] */
+  int preload;           /* samples 0..preload-1 are teacher-forced from pcm (lpcnet.c:256-259) */
   const float *emb_sig, *emb_pred, *emb_exc; /* [256][GA_ROWS] */
   const float *ga_par;   /* [6][NA]: recurrent bias z,r,h then diag z,r,h */
   const int *ga_wsum;    /* [3][NA]: 128*rowsum(int8 w) (non-saturating int8 path) */

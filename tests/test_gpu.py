@@ -143,3 +143,60 @@ def test_full_size_properties(require_gpu, blobs):
     o3 = np.stack([b1.synthesize(allf[f]) for f in range(F)], 1)
     assert np.array_equal(o1, o3)
     assert np.abs(o1[:, 2:].astype(np.float64)).mean() > 100
+
+
+def test_preload_teacher_forcing_matches_oracle(require_gpu, blobs):
+    """lpcnet_synthesize_impl with preload (lpcnet.c:256-259, the PLC entry)."""
+    blob = blobs["streams_int8"]
+    B, F = 3, 9
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    b = L.LPCNetBatch(B, 0, blob)
+    refs = [O.Oracle(blob, 0) for _ in range(B)]
+    t = np.arange(160)
+    for f in range(F):
+        if f in (4, 6):
+            pre = 80 if f == 4 else 160
+            teacher = np.stack([(3000 * np.sin(0.05 * (s + 1) * t)).astype(np.int16) for s in range(B)])
+            out = b.synthesize_impl(allf[f], teacher, pre)
+            for s in range(B):
+                exp = refs[s].synthesize(allf[f, s], 160, preload=teacher[s][:pre] if pre < 160 else teacher[s])
+                if pre < 160:
+                    exp = np.concatenate([teacher[s][:pre], exp[pre:]])
+                assert np.array_equal(out[s], exp), (f, s)
+        else:
+            out = b.synthesize(allf[f])
+            for s in range(B):
+                assert np.array_equal(out[s], refs[s].synthesize(allf[f, s])), (f, s)
+
+
+def test_frame_network_only_flush(require_gpu, blobs):
+    """N == 0: frame network only (run_frame_network_flush, lpcnet.c:134-144)."""
+    blob = blobs["streams_int8"]
+    B, F = 2, 6
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    b = L.LPCNetBatch(B, 0, blob)
+    refs = [O.Oracle(blob, 0) for _ in range(B)]
+    for f in range(F):
+        if f in (1, 3):
+            b.frame_only(allf[f])
+            for s in range(B):
+                refs[s].synthesize(allf[f, s], 0)
+        else:
+            out = b.synthesize(allf[f])
+            for s in range(B):
+                assert np.array_equal(out[s], refs[s].synthesize(allf[f, s])), (f, s)
+
+
+def test_state_save_restore_rollback(require_gpu, blobs):
+    """Speculate-and-roll-back as lpcnet_plc.c:223-231 does with struct copies."""
+    blob = blobs["streams_int8"]
+    B, F = 2, 8
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    b = L.LPCNetBatch(B, 0, blob)
+    for f in range(4):
+        b.synthesize(allf[f])
+    snap = b.save_state(1)
+    first = np.stack([b.synthesize(allf[f]) for f in range(4, 6)])
+    b.restore_state(1, snap)
+    second = np.stack([b.synthesize(allf[f]) for f in range(4, 6)])
+    assert np.array_equal(first[:, 1], second[:, 1])
