@@ -108,14 +108,17 @@ class Oracle:
     def synthesize(self, features: np.ndarray, n: int = 160, preload: np.ndarray | None = None,
                    trace: bool = False):
         f = np.ascontiguousarray(np.asarray(features, np.float32)[:20])
-        out = np.zeros(n, np.int16) if preload is None else np.ascontiguousarray(preload, np.int16).copy()
-        npre = 0 if preload is None else len(preload)
+        out = np.zeros(max(n, 1), np.int16)
+        npre = 0 if preload is None else min(len(preload), n)
+        if npre:
+            out[:npre] = np.asarray(preload, np.int16)[:npre]
         if trace:
             lg = np.zeros((n, 8), np.float32)
             ex = np.zeros(n, np.int32)
             rw = np.zeros((n, 2), np.uint32)
             _ora.oracle_set_trace(self._st, lg.ctypes.data, ex.ctypes.data, rw.ctypes.data)
         _ora.oracle_synthesize(self._st, f.ctypes.data, out.ctypes.data, n, npre)
+        out = out[:n]
         if trace:
             _ora.oracle_set_trace(self._st, None, None, None)
             return out, lg, ex, rw
