@@ -95,6 +95,12 @@ LPCNET_EXPORT double lpcnet_batch_kernel_ms(LPCNetBatch *b, int which, int *laun
  * logits [B][N][8], exc [B][N]. */
 LPCNET_EXPORT int lpcnet_batch_set_trace(LPCNetBatch *b, int enable);
 LPCNET_EXPORT int lpcnet_batch_get_trace(LPCNetBatch *b, float *logits, int *exc);
+/* Diagnostics: per-phase s_memtime sums of the sample kernel, recorded for
+ * the LAST launch when enabled: [workgroup][6 waves][8] u64 (phase B, wait,
+ * phase C, wait, phase F, wait, loop total, samples).  Returns #workgroups. */
+LPCNET_EXPORT int lpcnet_batch_set_stamps(LPCNetBatch *b, int enable);
+LPCNET_EXPORT int lpcnet_batch_get_stamps(LPCNetBatch *b, unsigned long long *out);
+
 /* Per-stream state snapshot: any pointer may be NULL. */
 LPCNET_EXPORT int lpcnet_batch_get_state(LPCNetBatch *b, int stream, float *gru_a_cond /*1152*/, float *gru_b_cond /*48*/,
                                          float *lpc /*16*/, float *gru_a_state /*384*/, float *gru_b_state /*16*/,

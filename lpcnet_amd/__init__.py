@@ -69,6 +69,8 @@ def _load():
         "lpcnet_batch_memcpy_d2h": (i, [vp, vp, vp, C.c_size_t]),
         "lpcnet_batch_reset_timers": (None, [vp, i]),
         "lpcnet_batch_kernel_ms": (C.c_double, [vp, i, C.POINTER(C.c_int)]),
+        "lpcnet_batch_set_stamps": (i, [vp, i]),
+        "lpcnet_batch_get_stamps": (i, [vp, vp]),
         "lpcnet_batch_set_trace": (i, [vp, i]),
         "lpcnet_batch_get_trace": (i, [vp, vp, vp]),
         "lpcnet_batch_get_state": (i, [vp, i, vp, vp, vp, vp, vp, vp]),
@@ -267,6 +269,18 @@ class LPCNetBatch:
         n = C.c_int(0)
         ms = lib.lpcnet_batch_kernel_ms(self._b, which, C.byref(n))
         return ms, n.value
+
+    def set_stamps(self, enable: bool = True) -> None:
+        if lib.lpcnet_batch_set_stamps(self._b, 1 if enable else 0) != 0:
+            raise LPCNetError(last_error())
+
+    def get_stamps(self) -> np.ndarray:
+        """[workgroups, 6 waves, 8] s_memtime sums of the last sample-kernel launch."""
+        out = np.zeros((self.B, 6, 8), np.uint64)
+        g = lib.lpcnet_batch_get_stamps(self._b, out.ctypes.data)
+        if g < 0:
+            raise LPCNetError("stamps not enabled")
+        return out[:g]
 
     def set_trace(self, enable: bool = True) -> None:
         lib.lpcnet_batch_set_trace(self._b, 1 if enable else 0)

@@ -304,6 +304,8 @@ struct LPCNetBatch {
   float *d_trace_logits = nullptr;
   int *d_trace_exc = nullptr;
   int trace_N = 0;
+  /* diagnostics */
+  unsigned long long *d_stamps = nullptr;
   /* timing */
   bool timing = false;
   std::vector<hipEvent_t> ev_pairs[2];
@@ -688,6 +690,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   sa.N = N;
   sa.pcm = d_pcm;
   sa.preload = std::max(0, std::min(preload, N));
+  sa.stamps = b->d_stamps;
   hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
   if (b->timing)
     for (int i = 0; i < 4; i++) e[i] = get_event(b);
@@ -781,6 +784,7 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
   (void)hipFree(b->d_pcm);
   (void)hipFree(b->d_trace_logits);
   (void)hipFree(b->d_trace_exc);
+  (void)hipFree(b->d_stamps);
   for (int i = 0; i < 2; i++) {
     (void)hipFree(b->d_lpc[i]);
     if (b->h_lpc[i]) (void)hipHostFree(b->h_lpc[i]);
@@ -966,6 +970,31 @@ LPCNET_EXPORT double lpcnet_batch_kernel_ms(LPCNetBatch *b, int which, int *laun
   }
   if (launches) *launches = (int)(v.size() / 2);
   return tot;
+}
+
+static int stamp_groups(const LPCNetBatch *b) { return (b->B + b->S - 1) / b->S; }
+
+LPCNET_EXPORT int lpcnet_batch_set_stamps(LPCNetBatch *b, int enable)
+{
+  if (!b || b->set_device()) return -1;
+  (void)hipStreamSynchronize(b->stream);
+  if (b->d_stamps) (void)hipFree(b->d_stamps);
+  b->d_stamps = nullptr;
+  if (enable) {
+    size_t n = (size_t)b->B * SAMPLE_WAVES * 8; /* enough for any S */
+    HIPCHK(hipMalloc(&b->d_stamps, n * 8));
+    HIPCHK(hipMemset(b->d_stamps, 0, n * 8));
+  }
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_get_stamps(LPCNetBatch *b, unsigned long long *out)
+{
+  if (!b || !b->d_stamps || !b->have_model || b->set_device()) return -1;
+  HIPCHK(hipStreamSynchronize(b->stream));
+  int g = stamp_groups(b);
+  HIPCHK(hipMemcpy(out, b->d_stamps, (size_t)g * SAMPLE_WAVES * 8 * 8, hipMemcpyDeviceToHost));
+  return g;
 }
 
 LPCNET_EXPORT int lpcnet_batch_set_trace(LPCNetBatch *b, int enable)

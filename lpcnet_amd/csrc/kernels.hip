@@ -524,6 +524,20 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
   const uint16_t *lds16 = (const uint16_t *)lds;
   const int j8 = lane >> 3;
 
+  /* optional phase timing (diagnostics only): per wave, s_memtime sums of
+   * [0] phase B work [1] barrier 1 wait [2] phase C [3] barrier 2 wait
+   * [4] phase F [5] barrier 3 wait [6] total loop [7] samples */
+  const bool stamping = A.stamps != nullptr;
+  unsigned long long stp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_prev = stamping ? __builtin_amdgcn_s_memtime() : 0, t_loop0 = t_prev;
+  auto stamp = [&](int k) {
+    if (stamping) {
+      unsigned long long t = __builtin_amdgcn_s_memtime();
+      stp[k] += t - t_prev;
+      t_prev = t;
+    }
+  };
+
   for (int n = 0; n < A.N; n++) {
     const int cur = n & 1;
     /* ---- phase B: GRU_A (nnet.c:484-491 + 410-448) ---------------------- */
@@ -622,7 +636,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
           ((float *)(xa_base + nxt * (NA / 4) * S * 16))[((i >> 2) * S + s) * 4 + (i & 3)] = st[s];
       }
     }
+    stamp(0);
     __syncthreads();
+    stamp(1);
 
     /* ---- phase C: GRU_B gate sums, wave w = row block w (nnet.c:345-361) --- */
     {
@@ -685,7 +701,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
         }
       }
     }
+    stamp(2);
     __syncthreads();
+    stamp(3);
 
     /* ---- phase F: per-stream GRU_B update, dual-FC sampling, output -------- */
     if (stream_wave) {
@@ -780,7 +798,14 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
       if (lane < NB) sbuf[s * NB + lane] = sbv;
       if (n + 1 < A.N) pre_sample();
     }
+    stamp(4);
     __syncthreads();
+    stamp(5);
+  }
+  if (stamping && lane == 0) {
+    stp[6] = __builtin_amdgcn_s_memtime() - t_loop0;
+    stp[7] = (unsigned long long)A.N;
+    for (int k = 0; k < 8; k++) A.stamps[((size_t)blockIdx.x * SAMPLE_WAVES + wv) * 8 + k] = stp[k];
   }
 
   /* ---- write back (only streams that synthesised this frame) ------------- */

@@ -97,6 +97,7 @@ struct SampleArgs {
   const float4 *ga_wf;   /* fp32 variant: GRU_A blocks [chunk][k][64] float4 */
   const float4 *gb_wf;   /* fp32 variant: GRU_B blocks [rb][k][8 rows][2] float4 (in c) */
   const float *gb_recf;  /* fp32 variant: GRU_B recurrent [NB][GB_ROWS] */
+  unsigned long long *stamps; /* optional diagnostics [grid][6 waves][8] s_memtime sums */
   float *trace_logits;   /* optional [B][N][8] */
   int *trace_exc;        /* optional [B][N] */
 };

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Per-phase cycle breakdown of the sample kernel (s_memtime stamps).
+Diagnostic build path only: the stamps are off in every timed run."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import lpcnet_amd as L  # noqa: E402
+
+NAMES = ["B(gru_a)", "wait1", "C(gru_b)", "wait2", "F(sample)", "wait3"]
+
+
+def profile(B, variant=0):
+    blob = L.synthetic_model(1, variant)
+    b = L.LPCNetBatch(B, 0, blob)
+    F = 4
+    allf = np.stack([L.synthetic_features(s, F)[:, :20] for s in range(B)], 1)
+    for f in range(3):
+        b.synthesize(allf[f])
+    b.set_stamps(True)
+    b.synthesize(allf[3])
+    st = b.get_stamps().astype(np.float64)  # [g][6][8]
+    n = st[:, :, 7].max()
+    per = st[:, :, :7] / n  # cycles per sample
+    info = b.info()
+    print(f"B={B} variant={variant} S={info.streams_per_workgroup} quad={info.quad_path} groups={st.shape[0]}")
+    for w in range(6):
+        row = per[:, w, :].mean(0)
+        print(f"  wave {w}: " + " ".join(f"{NAMES[k]}={row[k]:7.0f}" for k in range(6)) + f"  loop={row[6]:7.0f}")
+    b.close()
+
+
+if __name__ == "__main__":
+    for B in (1, 1024):
+        profile(B)
+    profile(1, 1)
