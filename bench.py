@@ -152,7 +152,8 @@ def main():
     variant = L.VARIANT_INT8 if args.variant == "int8" else L.VARIANT_FP32
     blob = L.synthetic_model(1, variant)
     B = args.streams
-    dt, (ks, kn, fs, fn), info, pcm = run_batch(L, blob, B, rank * B, args.warmup, args.steps, dist)
+    from lpcnet_amd.shard import weak_shard
+    dt, (ks, kn, fs, fn), info, pcm = run_batch(L, blob, B, weak_shard(rank, B).start, args.warmup, args.steps, dist)
     dt = max_over_ranks(dist, dt)
     samples = world * B * 160 * args.steps
     value = samples / dt
@@ -191,7 +192,13 @@ def main():
         dt1, (k1, n1, _, _), _, _ = run_batch(L, blob, 1, 0, args.warmup, max(args.steps, 20))
         s1 = max(args.steps, 20) * 160 / dt1
         out["batch1"] = {"samples_per_s": s1, "x_realtime": s1 / 16000.0, "ms_per_frame": dt1 / max(args.steps, 20) * 1e3,
-                         "sample_kernel_avg_ms": k1 / max(n1, 1)}
+                         "sample_kernel_avg_ms": k1 / max(n1, 1), "path": "int8"}
+        # BASELINE configs[1]: batch=1 with the fp32 (--disable-dot-product) GRU_A weights
+        blob32 = L.synthetic_model(1, L.VARIANT_FP32)
+        nf = max(args.steps, 20)
+        dt2, (k2, n2, _, _), _, _ = run_batch(L, blob32, 1, 0, args.warmup, nf)
+        out["batch1_fp32"] = {"samples_per_s": nf * 160 / dt2, "x_realtime": nf * 160 / dt2 / 16000.0,
+                              "ms_per_frame": dt2 / nf * 1e3, "sample_kernel_avg_ms": k2 / max(n2, 1)}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
