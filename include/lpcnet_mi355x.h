@@ -96,8 +96,10 @@ LPCNET_EXPORT double lpcnet_batch_kernel_ms(LPCNetBatch *b, int which, int *laun
 LPCNET_EXPORT int lpcnet_batch_set_trace(LPCNetBatch *b, int enable);
 LPCNET_EXPORT int lpcnet_batch_get_trace(LPCNetBatch *b, float *logits, int *exc);
 /* Diagnostics: per-phase s_memtime sums of the sample kernel, recorded for
- * the LAST launch when enabled: [workgroup][6 waves][8] u64 (phase B, wait,
- * phase C, wait, phase F, wait, loop total, samples).  Returns #workgroups. */
+ * the LAST launch when enabled: [workgroup][6 waves][16] u64 (phase B, wait,
+ * phase C, wait, phase F, wait, loop total, samples, then F sub-phases:
+ * GRU_B update, broadcast, tree levels 0-3, levels 4-7, output).  Returns
+ * #workgroups. */
 LPCNET_EXPORT int lpcnet_batch_set_stamps(LPCNetBatch *b, int enable);
 LPCNET_EXPORT int lpcnet_batch_get_stamps(LPCNetBatch *b, unsigned long long *out);
 

@@ -275,8 +275,8 @@ class LPCNetBatch:
             raise LPCNetError(last_error())
 
     def get_stamps(self) -> np.ndarray:
-        """[workgroups, 6 waves, 8] s_memtime sums of the last sample-kernel launch."""
-        out = np.zeros((self.B, 6, 8), np.uint64)
+        """[workgroups, 6 waves, 16] s_memtime sums of the last sample-kernel launch."""
+        out = np.zeros((self.B, 6, 16), np.uint64)
         g = lib.lpcnet_batch_get_stamps(self._b, out.ctypes.data)
         if g < 0:
             raise LPCNetError("stamps not enabled")

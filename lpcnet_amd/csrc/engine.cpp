@@ -981,7 +981,7 @@ LPCNET_EXPORT int lpcnet_batch_set_stamps(LPCNetBatch *b, int enable)
   if (b->d_stamps) (void)hipFree(b->d_stamps);
   b->d_stamps = nullptr;
   if (enable) {
-    size_t n = (size_t)b->B * SAMPLE_WAVES * 8; /* enough for any S */
+    size_t n = (size_t)b->B * SAMPLE_WAVES * 16; /* enough for any S */
     HIPCHK(hipMalloc(&b->d_stamps, n * 8));
     HIPCHK(hipMemset(b->d_stamps, 0, n * 8));
   }
@@ -993,7 +993,7 @@ LPCNET_EXPORT int lpcnet_batch_get_stamps(LPCNetBatch *b, unsigned long long *ou
   if (!b || !b->d_stamps || !b->have_model || b->set_device()) return -1;
   HIPCHK(hipStreamSynchronize(b->stream));
   int g = stamp_groups(b);
-  HIPCHK(hipMemcpy(out, b->d_stamps, (size_t)g * SAMPLE_WAVES * 8 * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out, b->d_stamps, (size_t)g * SAMPLE_WAVES * 16 * 8, hipMemcpyDeviceToHost));
   return g;
 }
 

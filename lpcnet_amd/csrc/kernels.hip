@@ -32,14 +32,20 @@ namespace lpcnet_mi355x {
 __device__ __forceinline__ float rcp_x86(float x, const uint32_t *tab)
 {
   /* _mm256_rcp_ps: table of the top 11 mantissa bits, exponent invariant,
-   * denormal results flushed to zero (probe: SURVEY.md 7 hard part 1). */
-  uint32_t u = __float_as_uint(x), sign = u & 0x80000000u;
-  int e = (int)((u >> 23) & 0xff);
+   * denormal results flushed to zero (probe: SURVEY.md 7 hard part 1).
+   * The table load is issued unconditionally and pinned (empty asm) so the
+   * special cases below stay selects instead of exec-masked branches. */
+  const uint32_t u = __float_as_uint(x);
   uint32_t t = tab[(u >> 12) & 0x7ff];
-  int te = (int)((t >> 23) & 0xff) - (e - 127);
-  uint32_t r = te < 1 ? sign : (sign | (t & 0x007fffffu) | ((uint32_t)te << 23));
+  asm volatile("" : "+v"(t));
+  const uint32_t sign = u & 0x80000000u;
+  const int e = (int)((u >> 23) & 0xff);
+  const int te = (int)((t >> 23) & 0xff) + 127 - e;
+  uint32_t r = sign | (t & 0x007fffffu) | ((uint32_t)te << 23);
+  r = te < 1 ? sign : r;
+  const uint32_t spec = (u & 0x7fffffu) ? (u | 0x00400000u) : sign; /* NaN -> qNaN, inf -> 0 */
+  r = e == 255 ? spec : r;
   r = e == 0 ? (sign | 0x7f800000u) : r;
-  r = e == 255 ? ((u & 0x7fffffu) ? (u | 0x00400000u) : sign) : r;
   return __uint_as_float(r);
 }
 
@@ -466,18 +472,24 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
     ch[s] = p->gru_a_cond[2 * NA + i];
   }
   /* stream-serial state: wave s owns stream s (lanes 0..15 hold last_sig/lpc/GRU_B units) */
-  float ls = 0.f, lp = 0.f, sbv = 0.f, pred = 0.f, deemph = 0.f;
+  /* last_sig / lpc are held as uniform register arrays by every lane of the
+   * stream's wave, so the sequential pred chain needs no cross-lane traffic */
+  float lsr[NLPC], lpr[NLPC];
+  float sbv = 0.f, pred = 0.f, deemph = 0.f;
   uint32_t rz = 0, rw = 0, rj = 0, rc = 0, r0 = 0, r1 = 0;
   int last_exc = 0;
   const int my_s = wv;
   const bool stream_wave = my_s < S;
+#pragma unroll
+  for (int j = 0; j < NLPC; j++) { lsr[j] = 0.f; lpr[j] = 0.f; }
   if (stream_wave) {
     const StreamState *p = &A.st[min(s0 + my_s, A.nstreams - 1)];
-    if (lane < NLPC) {
-      ls = p->last_sig[lane];
-      lp = p->lpc[lane];
-      sbv = p->gru_b_state[lane];
+#pragma unroll
+    for (int j = 0; j < NLPC; j++) {
+      lsr[j] = p->last_sig[j];
+      lpr[j] = p->lpc[j];
     }
+    sbv = p->gru_b_state[lane & (NB - 1)];
     for (int k = lane; k < GB_ROWS; k += 64) condb[my_s * GB_ROWS + k] = p->gru_b_cond[k];
     deemph = p->deemph_mem;
     last_exc = p->last_exc;
@@ -500,16 +512,16 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
 
   /* per-stream step between samples: pred and the u-law indices (lpcnet.c:252-254) */
   auto pre_sample = [&]() {
-    /* pred = -sum last_sig[j]*lpc[j], sequential; lane j holds the j-th product */
-    float prod = ls * lp;
+    /* pred = -sum last_sig[j]*lpc[j], sequential (lpcnet.c:252) */
     float p2 = 0.f;
 #pragma unroll
-    for (int j = 0; j < NLPC; j++) p2 = p2 - __int_as_float(__builtin_amdgcn_readlane(__float_as_int(prod), j));
+    for (int j = 0; j < NLPC; j++) p2 = p2 - lsr[j] * lpr[j];
     pred = p2;
-    float ls0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ls), 0));
+    const int su = lin2ulaw_x86(lsr[0]);
+    const int pu = lin2ulaw_x86(pred);
     if (lane == 0) {
-      ix[my_s * 4 + 0] = lin2ulaw_x86(ls0);
-      ix[my_s * 4 + 1] = lin2ulaw_x86(pred);
+      ix[my_s * 4 + 0] = su;
+      ix[my_s * 4 + 1] = pu;
       ix[my_s * 4 + 2] = last_exc;
     }
   };
@@ -528,7 +540,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
    * [0] phase B work [1] barrier 1 wait [2] phase C [3] barrier 2 wait
    * [4] phase F [5] barrier 3 wait [6] total loop [7] samples */
   const bool stamping = A.stamps != nullptr;
-  unsigned long long stp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long stp[16] = {};
   unsigned long long t_prev = stamping ? __builtin_amdgcn_s_memtime() : 0, t_loop0 = t_prev;
   auto stamp = [&](int k) {
     if (stamping) {
@@ -709,62 +721,83 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
     if (stream_wave) {
       const int s = my_s;
       const float *zs = zr + s * 2 * GB_ROWS;
-      /* GRU_B elementwise (nnet.c:362-371) */
-      if (lane < NB) {
-        float z = sigmoid_x86(zs[lane] + zs[GB_ROWS + lane], rcp);
-        float r = sigmoid_x86(zs[NB + lane] + zs[GB_ROWS + NB + lane], rcp);
-        float h = zs[2 * NB + lane] + zs[GB_ROWS + 2 * NB + lane] * r;
+      /* GRU_B elementwise (nnet.c:362-371): every lane computes unit lane%16
+       * (lanes >= 16 duplicate), so no exec masking on the serial path */
+      {
+        const int u = lane & (NB - 1);
+        float z = sigmoid_x86(zs[u] + zs[GB_ROWS + u], rcp);
+        float r = sigmoid_x86(zs[NB + u] + zs[GB_ROWS + NB + u], rcp);
+        float h = zs[2 * NB + u] + zs[GB_ROWS + 2 * NB + u] * r;
         h = tanh_x86(h, rcp);
         sbv = z * sbv + (1.f - z) * h;
+        if (lane < NB) sbuf[s * NB + lane] = sbv;
       }
+      stamp(8);
+      /* same-wave LDS exchange: the reads below follow the writes in this
+       * wave's LDS queue */
+      __builtin_amdgcn_wave_barrier();
       float xv[NB];
+      {
+        const float4 *sb4 = (const float4 *)(sbuf + s * NB);
 #pragma unroll
-      for (int j = 0; j < NB; j++) xv[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sbv), j));
-      /* dual_fc tree sampling (nnet.c:163-214), 30 (node, channel) chains at a time */
+        for (int j = 0; j < NB / 4; j++) {
+          const float4 v = sb4[j];
+          xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
+        }
+      }
+      /* dual_fc tree sampling (nnet.c:163-214): lane 2q+c computes channel c
+       * of one node; each even lane compares its node's logit with its
+       * level's threshold and the walk runs on the ballot mask in scalar ops */
       float thr[8];
 #pragma unroll
       for (int b = 0; b < 4; b++) {
         thr[b] = logit_tab[(r0 >> (8 * b)) & 0xFF];
         thr[b + 4] = logit_tab[(r1 >> (8 * b)) & 0xFF];
       }
+      stamp(9);
       const int q = lane >> 1, ch2 = lane & 1;
+      const int qq = q < 15 ? q : 0;
+      const int lvl_in = qq == 0 ? 0 : (qq < 3 ? 1 : (qq < 7 ? 2 : 3)); /* level of node qq+1 within 0..3 */
       auto node_logit = [&](int node) -> float {
         float sum = fcb[ch2 * 256 + node];
         const float *w = fcw + node * 32 + ch2 * 16;
 #pragma unroll
         for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
-        float v = fcf[ch2 * 256 + node] * tanh_x86(sum, rcp);
-        return v + __shfl_xor(v, 1);
+        const float v = fcf[ch2 * 256 + node] * tanh_x86(sum, rcp);
+        /* sum1 + sum2 (nnet.c:205); adjacent-lane swap through DPP quad_perm [1,0,3,2] */
+        const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+        return ch2 ? o + v : v + o;
       };
+      const bool tracing = A.trace_logits != nullptr;
       float lg[8];
       int val = 0;
       {
-        int node = q < 15 ? q + 1 : 1; /* levels 0..3: nodes 1..15 */
-        float l = node_logit(node);
+        const float l = node_logit(qq + 1); /* levels 0..3: nodes 1..15 */
+        const float t = lvl_in == 0 ? thr[0] : (lvl_in == 1 ? thr[1] : (lvl_in == 2 ? thr[2] : thr[3]));
+        const unsigned long long m = __ballot(t < l);
 #pragma unroll
         for (int b = 0; b < 4; b++) {
-          int nd = (1 << b) | val;
-          float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), 2 * (nd - 1)));
-          lg[b] = v;
-          val = (val << 1) | (thr[b] < v ? 1 : 0);
+          const int nd = (1 << b) | val;
+          if (tracing) lg[b] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), 2 * (nd - 1)));
+          val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
         }
       }
+      stamp(10);
       {
         /* levels 4..7 under the chosen 4-bit prefix: 1 + 2 + 4 + 8 nodes */
-        int qq = q < 15 ? q : 0;
-        int lvl = qq == 0 ? 4 : (qq < 3 ? 5 : (qq < 7 ? 6 : 7));
-        int off = qq + 1 - (1 << (lvl - 4));
-        int node = (1 << lvl) | (val << (lvl - 4)) | off;
-        float l = node_logit(node);
+        const int lvl = 4 + lvl_in;
+        const int off = qq + 1 - (1 << (lvl - 4));
+        const float l = node_logit((1 << lvl) | (val << (lvl - 4)) | off);
+        const float t = lvl_in == 0 ? thr[4] : (lvl_in == 1 ? thr[5] : (lvl_in == 2 ? thr[6] : thr[7]));
+        const unsigned long long m = __ballot(t < l);
 #pragma unroll
         for (int b = 4; b < 8; b++) {
-          int o = val & ((1 << (b - 4)) - 1);
-          int qi = (1 << (b - 4)) - 1 + o;
-          float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), 2 * qi));
-          lg[b] = v;
-          val = (val << 1) | (thr[b] < v ? 1 : 0);
+          const int qi = (1 << (b - 4)) - 1 + (val & ((1 << (b - 4)) - 1));
+          if (tracing) lg[b] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), 2 * qi));
+          val = (val << 1) | (int)((m >> (2 * qi)) & 1ull);
         }
       }
+      stamp(11);
       int exc = val;
       /* output sample (lpcnet.c:256-269) */
       float pcm;
@@ -777,15 +810,16 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
       } else {
         pcm = pred + ulaw[exc];
       }
-      float up = __shfl_up(ls, 1);
-      ls = lane == 0 ? pcm : up;
+#pragma unroll
+      for (int j = NLPC - 1; j > 0; j--) lsr[j] = lsr[j - 1];
+      lsr[0] = pcm;
       last_exc = exc;
       float o = pcm + kPreemph * deemph;
       deemph = o;
       if (o < -32767) o = -32767;
       if (o > 32767) o = 32767;
       if (lane == 0 && n >= A.preload) pcmbuf[s * FRAME + n] = (short)(int)floor(.5 + (double)o);
-      if (A.trace_logits && lane < 8 && active[s]) {
+      if (tracing && lane < 8 && active[s]) {
         float v = lg[0];
 #pragma unroll
         for (int b = 1; b < 8; b++) v = lane == b ? lg[b] : v;
@@ -795,7 +829,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
       if constexpr (V == 0) {
         if (lane < NB) xb[(lane >> 2) * S * 4 + s * 4 + (lane & 3)] = (unsigned char)quant_s8(sbv);
       }
-      if (lane < NB) sbuf[s * NB + lane] = sbv;
+      stamp(12);
       if (n + 1 < A.N) pre_sample();
     }
     stamp(4);
@@ -805,7 +839,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
   if (stamping && lane == 0) {
     stp[6] = __builtin_amdgcn_s_memtime() - t_loop0;
     stp[7] = (unsigned long long)A.N;
-    for (int k = 0; k < 8; k++) A.stamps[((size_t)blockIdx.x * SAMPLE_WAVES + wv) * 8 + k] = stp[k];
+    for (int k = 0; k < 16; k++) A.stamps[((size_t)blockIdx.x * SAMPLE_WAVES + wv) * 16 + k] = stp[k];
   }
 
   /* ---- write back (only streams that synthesised this frame) ------------- */
@@ -813,9 +847,10 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
     if (active[s]) A.st[s0 + s].gru_a_state[i] = st[s];
   if (stream_wave && active[my_s]) {
     StreamState *p = &A.st[s0 + my_s];
-    if (lane < NLPC) {
-      p->last_sig[lane] = ls;
-      p->gru_b_state[lane] = sbv;
+    if (lane < NB) p->gru_b_state[lane] = sbv;
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < NLPC; j++) p->last_sig[j] = lsr[j];
     }
     if (lane == 0) {
       p->deemph_mem = deemph;

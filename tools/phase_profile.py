@@ -22,14 +22,17 @@ def profile(B, variant=0):
         b.synthesize(allf[f])
     b.set_stamps(True)
     b.synthesize(allf[3])
-    st = b.get_stamps().astype(np.float64)  # [g][6][8]
+    st = b.get_stamps().astype(np.float64)  # [g][6][16]
     n = st[:, :, 7].max()
-    per = st[:, :, :7] / n  # cycles per sample
+    per = st / n  # cycles per sample
     info = b.info()
     print(f"B={B} variant={variant} S={info.streams_per_workgroup} quad={info.quad_path} groups={st.shape[0]}")
     for w in range(6):
         row = per[:, w, :].mean(0)
         print(f"  wave {w}: " + " ".join(f"{NAMES[k]}={row[k]:7.0f}" for k in range(6)) + f"  loop={row[6]:7.0f}")
+    row = per[:, 0, :].mean(0)
+    print("  F detail (wave 0): gru_b=%.0f bcast=%.0f lvl0-3=%.0f lvl4-7=%.0f out=%.0f pre=%.0f" %
+          (row[8], row[9], row[10], row[11], row[12], row[4]))
     b.close()
 
 
