@@ -32,8 +32,8 @@ typedef struct {
   double bytes_shared_per_sample; /* algorithmic weight bytes read once per sample step */
   double bytes_per_stream_sample; /* per-stream bytes per sample (gathers, trace-free) */
   double ops_per_sample;          /* 2*MAC per stream per sample */
-  int streams_per_workgroup;      /* S of the sample kernel */
-  int quad_path;                  /* 1: int8 weights as per-lane uint4 quads in LDS */
+  int streams_per_workgroup;      /* streams per sample-kernel workgroup */
+  int quad_path;                  /* 0 per-slot LDS, 1 quad LDS (lockstep), 2 wave-per-stream */
   int lds_bytes;                  /* dynamic LDS of the sample kernel */
 } LPCNetModelInfo;
 
@@ -44,6 +44,10 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b);
 /* 0 on success, -1 on a missing / mis-sized array (lpcnet_load_model rules). */
 LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *data, int len);
 LPCNET_EXPORT int lpcnet_batch_model_info(const LPCNetBatch *b, LPCNetModelInfo *info);
+/* Sample-kernel selection: 0 automatic (default; env LPCNET_KERNEL), 1 the
+ * lockstep kernel (6 waves per stream group), 2 the wave-per-stream kernel
+ * (int8 models only).  Results are identical; only speed differs. */
+LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode);
 /* lpcnet_reset() on every stream / on one stream. */
 LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b);
 LPCNET_EXPORT int lpcnet_batch_reset_stream(LPCNetBatch *b, int stream);

@@ -53,6 +53,7 @@ def _load():
         "lpcnet_batch_destroy": (None, [vp]),
         "lpcnet_batch_load_model": (i, [vp, C.c_char_p, i]),
         "lpcnet_batch_model_info": (i, [vp, vp]),
+        "lpcnet_batch_set_kernel": (i, [vp, i]),
         "lpcnet_batch_reset": (None, [vp]),
         "lpcnet_batch_reset_stream": (i, [vp, i]),
         "lpcnet_batch_nb_streams": (i, [vp]),
@@ -185,6 +186,11 @@ class LPCNetBatch:
     def load_model(self, blob: bytes) -> None:
         if lib.lpcnet_batch_load_model(self._b, blob, len(blob)) != 0:
             raise LPCNetError(f"lpcnet_batch_load_model failed: {last_error()}")
+
+    def set_kernel(self, mode: int) -> None:
+        """0 automatic, 1 lockstep sample kernel, 2 wave-per-stream kernel."""
+        if lib.lpcnet_batch_set_kernel(self._b, mode) != 0:
+            raise LPCNetError("bad kernel mode")
 
     def info(self) -> ModelInfo:
         mi = ModelInfo()

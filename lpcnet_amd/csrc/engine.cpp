@@ -286,6 +286,9 @@ struct LPCNetBatch {
   int variant = 0;
   bool sat = false;
   bool reg = false;
+  int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 2 wave_kernel */
+  int wave_nw = 0;       /* >0: wave_kernel with this many streams per workgroup */
+  int image_bytes = 0;
   LPCNetModelInfo info{};
   std::vector<void *> model_bufs;
   FrameArgs fa{};
@@ -359,6 +362,33 @@ bool block_may_saturate(const int8_t *w)
       if (255 * pos > 32767 || 255 * neg > 32768) return true;
     }
   return false;
+}
+
+/* Sample-kernel choice: the wave-per-stream kernel for int8 quad-layout
+ * models at >= 256 streams (one wave per stream, NW <= 4 streams per
+ * workgroup so each wave has a whole SIMD's register file), otherwise the
+ * lockstep kernel (6 waves per stream group; best single-stream latency). */
+void choose_kernel(LPCNetBatch *b)
+{
+  b->wave_nw = 0;
+  const bool can_wave = b->variant == LPCNET_VARIANT_INT8 && b->reg;
+  bool use_wave = can_wave && b->B >= 256;
+  if (b->kernel_mode == 1) use_wave = false;
+  if (b->kernel_mode == 2) use_wave = can_wave;
+  if (use_wave) {
+    int nw = std::min(4, std::max(1, (b->B + 255) / 256));
+    while (nw > 1 && wave_lds_bytes(nw, b->image_bytes) > 160 * 1024) nw /= 2;
+    if (wave_lds_bytes(nw, b->image_bytes) <= 160 * 1024) {
+      b->wave_nw = nw;
+      b->info.streams_per_workgroup = nw;
+      b->info.lds_bytes = wave_lds_bytes(nw, b->image_bytes);
+      b->info.quad_path = 2;
+      return;
+    }
+  }
+  b->info.streams_per_workgroup = b->S;
+  b->info.lds_bytes = b->lds_bytes;
+  b->info.quad_path = b->reg ? 1 : 0;
 }
 
 int load_model(LPCNetBatch *b, const unsigned char *data, int len)
@@ -626,6 +656,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   b->variant = variant;
   b->sat = sat;
   b->reg = reg;
+  b->image_bytes = (int)img.size();
   b->S = S;
   b->lds_bytes = lds;
   b->have_model = true;
@@ -636,9 +667,8 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   in.gru_a_blocks = nba;
   in.gru_b_blocks = nbb;
   in.may_saturate = sat ? 1 : 0;
-  in.streams_per_workgroup = S;
   in.quad_path = reg ? 1 : 0;
-  in.lds_bytes = lds;
+  choose_kernel(b);
   double frame_w = (3.0 * FIN * COND + 3.0 * COND * COND + 2.0 * COND * COND + COND * GA_ROWS + COND * GB_ROWS) * 4 +
                    (2.0 * COND + 2 * COND + GA_ROWS + GB_ROWS) * 4 + EP * 4;
   double wbytes = int8 ? 1 : 4;
@@ -698,7 +728,10 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   if (launch_frame(fa, b->stream)) { set_err("frame kernel launch failed"); return -1; }
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
-  if (N > 0 && launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream)) {
+  const int lrc = N <= 0 ? 0
+                : (b->wave_nw ? launch_wave(sa, b->wave_nw, b->sat ? 1 : 0, wave_lds_bytes(b->wave_nw, b->image_bytes), b->stream)
+                              : launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream));
+  if (lrc) {
     set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     return -1;
   }
@@ -769,6 +802,7 @@ LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
     return nullptr;
   }
   b->pool = new Pool(std::min(pool_threads(), std::max(0, nb_streams / 32)));
+  if (const char *km = getenv("LPCNET_KERNEL")) b->kernel_mode = atoi(km);
   lpcnet_batch_reset(b);
   return b;
 }
@@ -804,6 +838,14 @@ LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *d
   if (b->set_device()) return -1;
   (void)hipStreamSynchronize(b->stream);
   return load_model(b, data, len);
+}
+
+LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode)
+{
+  if (!b || mode < 0 || mode > 2) return -1;
+  b->kernel_mode = mode;
+  if (b->have_model) choose_kernel(b);
+  return 0;
 }
 
 LPCNET_EXPORT int lpcnet_batch_model_info(const LPCNetBatch *b, LPCNetModelInfo *info)

@@ -865,6 +865,319 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
 }
 
 /* ------------------------------------------------------------------------ */
+/* wave-per-stream sample network (large batches)                            */
+/*
+ * One wavefront runs one stream through all N samples with no workgroup
+ * barrier after the image load: the NW waves of a workgroup share the LDS
+ * weight image (same quad layout as sample_kernel) and overlap each other's
+ * latency.  Lane l owns GRU_A units l + 64j (j = 0..5): pass j is exactly
+ * chunk j of the quad image.  GRU_B: pass rb = row block rb, lane (row l%8,
+ * k-slice l/8) with three quad groups, reduced across k-slices by shuffles.
+ */
+constexpr int WV_X = NA;              /* quantized GRU_A state, [96 column blocks] u32 */
+constexpr int WV_XB = NB;             /* quantized GRU_B state */
+constexpr int WV_ZR = 2 * GB_ROWS * 4;
+constexpr int WV_SB = NB * 4;
+constexpr int WV_PCM = FRAME * 2;
+constexpr int WV_STRIDE = ((WV_X + WV_XB + WV_ZR + WV_SB + WV_PCM) + 15) / 16 * 16;
+
+int wave_lds_bytes(int nw, int image_bytes) { return image_bytes + nw * WV_STRIDE; }
+
+template <int NW, bool SAT>
+__global__ __launch_bounds__(NW * 64) void wave_kernel(SampleArgs A)
+{
+  extern __shared__ uint4 lds4[];
+  unsigned char *lds = (unsigned char *)lds4;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int sid = blockIdx.x * NW + wv;
+  const bool valid = sid < A.nstreams;
+  const bool active = valid && A.st[sid].frame_count > FEATURES_DELAY;
+
+  for (int o = tid; o < A.image_bytes / 16; o += NW * 64) lds4[o] = A.image[o];
+  __syncthreads(); /* the only workgroup barrier */
+
+  unsigned char *wbase = lds + A.image_bytes + wv * WV_STRIDE;
+  unsigned char *xa = wbase;                 /* byte u = quantized unit u (XOR 0x80) */
+  unsigned char *xb = wbase + WV_X;
+  float *zr = (float *)(xb + WV_XB);
+  float *sbuf = zr + 2 * GB_ROWS;
+  short *pcmbuf = (short *)(sbuf + NB);
+  if (!active) {
+    if (valid)
+      for (int n = lane; n < A.N; n += 64) A.pcm[(size_t)sid * A.N + n] = 0;
+    return;
+  }
+  const uint32_t *rcp = (const uint32_t *)(lds + IMG_RCP);
+  const float *ulaw = (const float *)(lds + IMG_ULAW);
+  const float *logit_tab = (const float *)(lds + IMG_LOGIT);
+  const float *fcw = (const float *)(lds + IMG_FCW);
+  const float *fcb = (const float *)(lds + IMG_FCB);
+  const float *fcf = (const float *)(lds + IMG_FCF);
+  const uint4 *wq = (const uint4 *)lds;
+  const uint32_t *cq = (const uint32_t *)lds;
+  StreamState *P = &A.st[sid];
+
+  /* GRU_A units of this lane */
+  float st[6], cz[6], cr[6], ch[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    const int u = 64 * j + lane;
+    st[j] = P->gru_a_state[u];
+    cz[j] = P->gru_a_cond[u];
+    cr[j] = P->gru_a_cond[NA + u];
+    ch[j] = P->gru_a_cond[2 * NA + u];
+    xa[u] = (unsigned char)quant_s8(st[j]);
+  }
+  /* GRU_B: lane r = lane % 8 seeds rows 8*rb + r */
+  const int r8 = lane & 7, ks = lane >> 3;
+  float cbr[6];
+#pragma unroll
+  for (int rb = 0; rb < 6; rb++) cbr[rb] = P->gru_b_cond[rb * 8 + r8];
+  float sbv = P->gru_b_state[lane & (NB - 1)];
+  if (lane < NB) xb[lane] = (unsigned char)quant_s8(sbv);
+  float lsr[NLPC], lpr[NLPC];
+#pragma unroll
+  for (int j = 0; j < NLPC; j++) {
+    lsr[j] = P->last_sig[j];
+    lpr[j] = P->lpc[j];
+  }
+  float deemph = P->deemph_mem;
+  int last_exc = P->last_exc;
+  uint32_t rz = P->rng[0], rw = P->rng[1], rj = P->rng[2], rc = P->rng[3];
+  for (int e = lane; e < A.preload; e += 64) pcmbuf[e] = A.pcm[(size_t)sid * A.N + e];
+  const bool tracing = A.trace_logits != nullptr;
+
+  for (int n = 0; n < A.N; n++) {
+    /* ---- per-stream scalars: pred, u-law indices, kiss99 draws ---------- */
+    float pred = 0.f;
+#pragma unroll
+    for (int j = 0; j < NLPC; j++) pred = pred - lsr[j] * lpr[j];
+    const int sig = lin2ulaw_x86(lsr[0]) & 0xFF, prd = lin2ulaw_x86(pred) & 0xFF, exc_in = last_exc & 0xFF;
+    const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
+    const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
+
+    /* ---- GRU_A: gathers in flight during the integer matvec ------------- */
+    const float *e1 = A.emb_sig + sig * GA_ROWS, *e2 = A.emb_pred + prd * GA_ROWS, *e3 = A.emb_exc + exc_in * GA_ROWS;
+    float g1[18], g2[18], g3[18];
+#pragma unroll
+    for (int j = 0; j < 6; j++)
+#pragma unroll
+      for (int g = 0; g < 3; g++) {
+        const int row = g * NA + 64 * j + lane;
+        g1[3 * j + g] = e1[row];
+        g2[3 * j + g] = e2[row];
+        g3[3 * j + g] = e3[row];
+      }
+    int acc[18];
+#pragma unroll
+    for (int j = 0; j < 6; j++)
+#pragma unroll
+      for (int g = 0; g < 3; g++) {
+        int a = SAT ? 0 : A.ga_wsum[g * NA + 64 * j + lane];
+        const uint4 *wp = wq + A.ga_qoff[j][g] + lane;
+        const uint32_t *cp = cq + A.ga_coff[j][g] + (lane >> 3);
+        const int K4 = A.ga_K4[j][g];
+        for (int k = 0; k < K4; k++) {
+          const uint4 w = wp[k * 64];
+          const uint32_t c = cp[k * 8];
+          const uint32_t *x32 = (const uint32_t *)xa;
+          a = dot4<SAT>(w.x, x32[c & 0xFF], a);
+          a = dot4<SAT>(w.y, x32[(c >> 8) & 0xFF], a);
+          a = dot4<SAT>(w.z, x32[(c >> 16) & 0xFF], a);
+          a = dot4<SAT>(w.w, x32[c >> 24], a);
+        }
+        acc[3 * j + g] = a;
+      }
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      const int u = 64 * j + lane;
+      const float bz = A.ga_par[u], br = A.ga_par[NA + u], bh = A.ga_par[2 * NA + u];
+      const float dz = A.ga_par[3 * NA + u], dr = A.ga_par[4 * NA + u], dh = A.ga_par[5 * NA + u];
+      const float inz = ((cz[j] + g1[3 * j]) + g2[3 * j]) + g3[3 * j];
+      const float inr = ((cr[j] + g1[3 * j + 1]) + g2[3 * j + 1]) + g3[3 * j + 1];
+      const float inh = ((ch[j] + g1[3 * j + 2]) + g2[3 * j + 2]) + g3[3 * j + 2];
+      const float gz = (float)(acc[3 * j] + cvt_rne(((bz + dz * st[j]) + inz) * kScale)) * kScale1;
+      const float gr = (float)(acc[3 * j + 1] + cvt_rne(((br + dr * st[j]) + inr) * kScale)) * kScale1;
+      const float gh = (float)(acc[3 * j + 2] + cvt_rne((bh + dh * st[j]) * kScale)) * kScale1;
+      const float z = sigmoid_x86(gz, rcp);
+      const float r = sigmoid_x86(gr, rcp);
+      float h = gh * r + inh;
+      h = tanh_x86(h, rcp);
+      st[j] = z * st[j] + (1.f - z) * h;
+    }
+    /* every read of the old x is done (program order, in-order LDS queue) */
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < 6; j++) xa[64 * j + lane] = (unsigned char)quant_s8(st[j]);
+    __builtin_amdgcn_wave_barrier();
+
+    /* ---- GRU_B gate sums (nnet.c:345-361) -------------------------------- */
+#pragma unroll
+    for (int rb = 0; rb < 6; rb++) {
+      int a = 0, ar = 0;
+      const uint4 *wp = wq + A.gb_qoff[rb] + lane;
+      const uint32_t *cp = cq + A.gb_coff[rb] + ks;
+      const uint32_t *x32 = (const uint32_t *)xa;
+#pragma unroll
+      for (int k = 0; k < REG_GB / 4; k++) {
+        const uint4 w = wp[k * 64];
+        const uint32_t c = cp[k * 8];
+        a = dot4<SAT>(w.x, x32[c & 0xFF], a);
+        a = dot4<SAT>(w.y, x32[(c >> 8) & 0xFF], a);
+        a = dot4<SAT>(w.z, x32[(c >> 16) & 0xFF], a);
+        a = dot4<SAT>(w.w, x32[c >> 24], a);
+      }
+      if (ks < NB / 4)
+        ar = dot4<SAT>(((const uint32_t *)(lds + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r8], ((const uint32_t *)xb)[ks], ar);
+      a += __shfl_xor(a, 8);
+      a += __shfl_xor(a, 16);
+      a += __shfl_xor(a, 32);
+      ar += __shfl_xor(ar, 8);
+      ar += __shfl_xor(ar, 16);
+      ar += __shfl_xor(ar, 32);
+      if (ks == 0) {
+        const int row = rb * 8 + r8;
+        const int seed = cvt_rne((A.gb_par[row] + cbr[rb]) * kScale) + (SAT ? 0 : A.gb_wsum[row]);
+        const int seedr = cvt_rne(A.gb_par[GB_ROWS + row] * kScale) + (SAT ? 0 : A.gb_wsum[GB_ROWS + row]);
+        zr[row] = (float)(seed + a) * kScale1;
+        zr[GB_ROWS + row] = (float)(seedr + ar) * kScale1;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+
+    /* ---- GRU_B update, dual-FC tree sampling, output (as sample_kernel) -- */
+    {
+      const int u = lane & (NB - 1);
+      const float z = sigmoid_x86(zr[u] + zr[GB_ROWS + u], rcp);
+      const float r = sigmoid_x86(zr[NB + u] + zr[GB_ROWS + NB + u], rcp);
+      float h = zr[2 * NB + u] + zr[GB_ROWS + 2 * NB + u] * r;
+      h = tanh_x86(h, rcp);
+      sbv = z * sbv + (1.f - z) * h;
+      if (lane < NB) sbuf[lane] = sbv;
+    }
+    __builtin_amdgcn_wave_barrier();
+    float xv[NB];
+    {
+      const float4 *sb4 = (const float4 *)sbuf;
+#pragma unroll
+      for (int j = 0; j < NB / 4; j++) {
+        const float4 v = sb4[j];
+        xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
+      }
+    }
+    float thr[8];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      thr[b] = logit_tab[(r0 >> (8 * b)) & 0xFF];
+      thr[b + 4] = logit_tab[(r1 >> (8 * b)) & 0xFF];
+    }
+    const int q = lane >> 1, ch2 = lane & 1;
+    const int qq = q < 15 ? q : 0;
+    const int lvl_in = qq == 0 ? 0 : (qq < 3 ? 1 : (qq < 7 ? 2 : 3));
+    auto node_logit = [&](int node) -> float {
+      float sum = fcb[ch2 * 256 + node];
+      const float *w = fcw + node * 32 + ch2 * 16;
+#pragma unroll
+      for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
+      const float v = fcf[ch2 * 256 + node] * tanh_x86(sum, rcp);
+      const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+      return ch2 ? o + v : v + o;
+    };
+    float lg[8];
+    int val = 0;
+    {
+      const float l = node_logit(qq + 1);
+      const float t = lvl_in == 0 ? thr[0] : (lvl_in == 1 ? thr[1] : (lvl_in == 2 ? thr[2] : thr[3]));
+      const unsigned long long m = __ballot(t < l);
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int nd = (1 << b) | val;
+        if (tracing) lg[b] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), 2 * (nd - 1)));
+        val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
+      }
+    }
+    {
+      const int lvl = 4 + lvl_in;
+      const int off = qq + 1 - (1 << (lvl - 4));
+      const float l = node_logit((1 << lvl) | (val << (lvl - 4)) | off);
+      const float t = lvl_in == 0 ? thr[4] : (lvl_in == 1 ? thr[5] : (lvl_in == 2 ? thr[6] : thr[7]));
+      const unsigned long long m = __ballot(t < l);
+#pragma unroll
+      for (int b = 4; b < 8; b++) {
+        const int qi = (1 << (b - 4)) - 1 + (val & ((1 << (b - 4)) - 1));
+        if (tracing) lg[b] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), 2 * qi));
+        val = (val << 1) | (int)((m >> (2 * qi)) & 1ull);
+      }
+    }
+    int exc = val;
+    float pcm;
+    if (n < A.preload) {
+      const float o_in = (float)pcmbuf[n];
+      const float pd = kPreemph * deemph;
+      exc = lin2ulaw_x86((o_in - pd) - pred);
+      pcm = o_in - pd;
+    } else {
+      pcm = pred + ulaw[exc];
+    }
+#pragma unroll
+    for (int j = NLPC - 1; j > 0; j--) lsr[j] = lsr[j - 1];
+    lsr[0] = pcm;
+    last_exc = exc;
+    float o = pcm + kPreemph * deemph;
+    deemph = o;
+    if (o < -32767) o = -32767;
+    if (o > 32767) o = 32767;
+    if (lane == 0 && n >= A.preload) pcmbuf[n] = (short)(int)floor(.5 + (double)o);
+    if (tracing && lane < 8) {
+      float v = lg[0];
+#pragma unroll
+      for (int b = 1; b < 8; b++) v = lane == b ? lg[b] : v;
+      A.trace_logits[((size_t)sid * A.N + n) * 8 + lane] = v;
+    }
+    if (A.trace_exc && lane == 0) A.trace_exc[(size_t)sid * A.N + n] = exc;
+    if (lane < NB) xb[lane] = (unsigned char)quant_s8(sbv);
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  /* ---- write back ---------------------------------------------------------- */
+#pragma unroll
+  for (int j = 0; j < 6; j++) P->gru_a_state[64 * j + lane] = st[j];
+  if (lane < NB) P->gru_b_state[lane] = sbv;
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < NLPC; j++) P->last_sig[j] = lsr[j];
+    P->deemph_mem = deemph;
+    P->last_exc = last_exc;
+    P->rng[0] = rz; P->rng[1] = rw; P->rng[2] = rj; P->rng[3] = rc;
+  }
+  for (int e = lane; e < A.N; e += 64) A.pcm[(size_t)sid * A.N + e] = pcmbuf[e];
+}
+
+template <int NW, bool SAT>
+static int launch_wave_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
+{
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void *)wave_kernel<NW, SAT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+        hipSuccess)
+      return -1;
+    attr_set = true;
+  }
+  int grid = (a.nstreams + NW - 1) / NW;
+  hipLaunchKernelGGL((wave_kernel<NW, SAT>), dim3(grid), dim3(NW * 64), lds_bytes, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_wave(const SampleArgs &a, int nw, int sat, int lds_bytes, void *stream)
+{
+  hipStream_t st = (hipStream_t)stream;
+#define W(n) if (nw == n) return sat ? launch_wave_t<n, true>(a, lds_bytes, st) : launch_wave_t<n, false>(a, lds_bytes, st);
+  W(1) W(2) W(4) W(8) W(16)
+#undef W
+  return -1;
+}
+
+/* ------------------------------------------------------------------------ */
 int launch_frame(const FrameArgs &a, void *stream)
 {
   int grid = (a.nstreams + FRAME_STREAMS - 1) / FRAME_STREAMS;

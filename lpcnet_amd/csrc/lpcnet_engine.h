@@ -108,6 +108,10 @@ int sample_lds_bytes(int S, int variant, int image_bytes);
 int launch_frame(const FrameArgs &a, void *stream);
 int launch_sample(const SampleArgs &a, int S, int variant, int sat, int reg, int lds_bytes, void *stream);
 
+/* Wave-per-stream sample kernel (int8 quad layout): nw streams per workgroup. */
+int wave_lds_bytes(int nw, int image_bytes);
+int launch_wave(const SampleArgs &a, int nw, int sat, int lds_bytes, void *stream);
+
 /* Host LPC (lpc_host.cpp). */
 float lpc_from_cepstrum_host(float *lpc, const float *ceps);
 

@@ -29,12 +29,16 @@ def blobs():
             "streams_int8_sat": L.synthetic_model(1, 0, True)}
 
 
-@pytest.mark.parametrize("name", ["streams_int8", "streams_fp32", "streams_int8_sat"])
-def test_batch_matches_golden(require_gpu, blobs, name):
+@pytest.mark.parametrize("name,kernel", [("streams_int8", 1), ("streams_fp32", 1), ("streams_int8_sat", 1),
+                                         ("streams_int8", 2), ("streams_int8_sat", 2)])
+def test_batch_matches_golden(require_gpu, blobs, name, kernel):
+    """kernel 1: lockstep sample_kernel, 2: wave-per-stream kernel."""
     G = np.load(os.path.join(GOLD, name + ".npz"))
     streams = list(G["streams"])
     F = G["pcm"].shape[1]
     b = L.LPCNetBatch(len(streams), 0, blobs[name])
+    b.set_kernel(kernel)
+    assert b.info().quad_path == (2 if kernel == 2 else 1)
     info = b.info()
     assert info.variant == int(G["variant"])
     if name.endswith("_sat"):
@@ -67,12 +71,16 @@ def test_single_stream_api_matches_golden(require_gpu, blobs):
     assert np.array_equal(net.synthesize(G["features"][0, 0]), G["pcm"][0, 0])
 
 
-@pytest.mark.parametrize("B,check", [(512, (0, 255, 511)), (1024, (0, 3, 517, 1023)), (1100, (1099, 1024, 5))])
-def test_large_batch_streams_match_oracle(require_gpu, blobs, B, check):
-    """Streams-per-workgroup 2 and 4 (and a ragged last workgroup) against the oracle."""
+@pytest.mark.parametrize("B,check,kernel", [(512, (0, 255, 511), 1), (1024, (0, 3, 517, 1023), 1),
+                                            (1100, (1099, 1024, 5), 1), (1024, (0, 3, 517, 1023), 0),
+                                            (1101, (1100, 1024, 5), 0), (300, (299, 7), 2)])
+def test_large_batch_streams_match_oracle(require_gpu, blobs, B, check, kernel):
+    """Lockstep kernel at 2 and 4 streams/workgroup, the wave-per-stream kernel
+    (auto at >= 256 streams), ragged last workgroups, against the oracle."""
     F = 5
     blob = blobs["streams_int8"]
     b = L.LPCNetBatch(B, 0, blob)
+    b.set_kernel(kernel)
     allf = np.stack([feats(s, F) for s in range(B)], 1)  # [F][B][20]
     out = np.stack([b.synthesize(allf[f]) for f in range(F)], 1)  # [B][F][160]
     for s in check:
@@ -145,12 +153,14 @@ def test_full_size_properties(require_gpu, blobs):
     assert np.abs(o1[:, 2:].astype(np.float64)).mean() > 100
 
 
-def test_preload_teacher_forcing_matches_oracle(require_gpu, blobs):
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_preload_teacher_forcing_matches_oracle(require_gpu, blobs, kernel):
     """lpcnet_synthesize_impl with preload (lpcnet.c:256-259, the PLC entry)."""
     blob = blobs["streams_int8"]
     B, F = 3, 9
     allf = np.stack([feats(s, F) for s in range(B)], 1)
     b = L.LPCNetBatch(B, 0, blob)
+    b.set_kernel(kernel)
     refs = [O.Oracle(blob, 0) for _ in range(B)]
     t = np.arange(160)
     for f in range(F):
