@@ -29,6 +29,23 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+def measured_traffic(kernel_prefix):
+    """HBM bytes per launch of the sample kernel from the committed rocprofv3
+    FETCH_SIZE/WRITE_SIZE passes of this same command (tools/gpu_profile.sh ->
+    tools/pmc_summary.py -> profiles/<round>/pmc_traffic.json); PMC counters
+    cannot be read in-process.  None when no profile matches the kernel."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for k, v in d.items():
+            if kernel_prefix in k:
+                return v["hbm_bytes_per_launch_corrected"], os.path.relpath(f, ROOT), k
+    return None, None, None
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -161,6 +178,8 @@ def main():
     sample_ms = ks / max(kn, 1)
     bytes_launch = 160 * info.bytes_shared_per_sample + B * 160 * info.bytes_per_stream_sample
     achieved = bytes_launch / (sample_ms * 1e-3) / 1e9
+    kname = info.kernel_name
+    traffic, tsrc, _ = measured_traffic(kname) if B == 1024 else (None, None, None)
     out = {
         "metric": "real-time 16 kHz streams/GPU; samples/s at batch=1 and batch=1024",
         "value": value,
@@ -180,8 +199,8 @@ def main():
         "rt_streams_per_gpu": value / world / 16000.0,
         "frame_step_ms": dt / args.steps * 1e3,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "sample_kernel", "avg_launch_ms": sample_ms, "launches": kn,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                     "kernel": kname, "avg_launch_ms": sample_ms, "launches": kn,
                      "algorithmic_bytes_per_launch": bytes_launch},
         "frame_kernel_avg_ms": fs / max(fn, 1),
         "kernel_config": {"streams_per_workgroup": info.streams_per_workgroup, "quad_path": info.quad_path,

@@ -99,6 +99,16 @@ class ModelInfo(C.Structure):
                 ("ops_per_sample", C.c_double), ("streams_per_workgroup", C.c_int), ("quad_path", C.c_int),
                 ("lds_bytes", C.c_int)]
 
+    @property
+    def kernel_name(self) -> str:
+        """Demangled template instance of the sample kernel this model runs
+        (as rocprofv3 names it)."""
+        sat = "true" if self.may_saturate else "false"
+        if self.quad_path == 2:
+            return f"wave_kernel<{self.streams_per_workgroup}, {sat}>"
+        quad = "true" if self.quad_path == 1 else "false"
+        return f"sample_kernel<{self.streams_per_workgroup}, {self.variant}, {sat}, {quad}>"
+
 
 def last_error() -> str:
     return (lib.lpcnet_mi355x_last_error() or b"").decode()

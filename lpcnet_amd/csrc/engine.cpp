@@ -372,7 +372,7 @@ void choose_kernel(LPCNetBatch *b)
 {
   b->wave_nw = 0;
   const bool can_wave = b->variant == LPCNET_VARIANT_INT8 && b->reg;
-  bool use_wave = can_wave && b->B >= 256;
+  bool use_wave = false;  /* measured slower than lockstep (profiles/r01/perf_log.md) */
   if (b->kernel_mode == 1) use_wave = false;
   if (b->kernel_mode == 2) use_wave = can_wave;
   if (use_wave) {

@@ -38,7 +38,7 @@ def test_batch_matches_golden(require_gpu, blobs, name, kernel):
     F = G["pcm"].shape[1]
     b = L.LPCNetBatch(len(streams), 0, blobs[name])
     b.set_kernel(kernel)
-    assert b.info().quad_path == (2 if kernel == 2 else 1)
+    assert (b.info().quad_path == 2) == (kernel == 2)
     info = b.info()
     assert info.variant == int(G["variant"])
     if name.endswith("_sat"):

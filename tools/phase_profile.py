@@ -16,6 +16,7 @@ NAMES = ["B(gru_a)", "wait1", "C(gru_b)", "wait2", "F(sample)", "wait3"]
 def profile(B, variant=0):
     blob = L.synthetic_model(1, variant)
     b = L.LPCNetBatch(B, 0, blob)
+    b.set_kernel(1)  # stamps are instrumented in the lockstep kernel only
     F = 4
     allf = np.stack([L.synthetic_features(s, F)[:, :20] for s in range(B)], 1)
     for f in range(3):
