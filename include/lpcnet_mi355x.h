@@ -33,7 +33,7 @@ typedef struct {
   double bytes_per_stream_sample; /* per-stream bytes per sample (gathers, trace-free) */
   double ops_per_sample;          /* 2*MAC per stream per sample */
   int streams_per_workgroup;      /* streams per sample-kernel workgroup */
-  int quad_path;                  /* 0 per-slot LDS, 1 quad LDS (lockstep), 2 wave-per-stream */
+  int quad_path;                  /* 0 per-slot LDS, 1 quad LDS (lockstep), 2 wave-per-stream, 3 pipelined */
   int lds_bytes;                  /* dynamic LDS of the sample kernel */
 } LPCNetModelInfo;
 
@@ -45,8 +45,9 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b);
 LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *data, int len);
 LPCNET_EXPORT int lpcnet_batch_model_info(const LPCNetBatch *b, LPCNetModelInfo *info);
 /* Sample-kernel selection: 0 automatic (default; env LPCNET_KERNEL), 1 the
- * lockstep kernel (6 waves per stream group), 2 the wave-per-stream kernel
- * (int8 models only).  Results are identical; only speed differs. */
+ * lockstep kernel (6 waves per stream group), 2 the wave-per-stream kernel,
+ * 3 the pipelined kernel (2 and 3: int8 quad-layout models only; otherwise
+ * the lockstep kernel runs).  Results are identical; only speed differs. */
 LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode);
 /* lpcnet_reset() on every stream / on one stream. */
 LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b);
@@ -100,10 +101,11 @@ LPCNET_EXPORT double lpcnet_batch_kernel_ms(LPCNetBatch *b, int which, int *laun
 LPCNET_EXPORT int lpcnet_batch_set_trace(LPCNetBatch *b, int enable);
 LPCNET_EXPORT int lpcnet_batch_get_trace(LPCNetBatch *b, float *logits, int *exc);
 /* Diagnostics: per-phase s_memtime sums of the sample kernel, recorded for
- * the LAST launch when enabled: [workgroup][6 waves][16] u64 (phase B, wait,
+ * the LAST launch when enabled: [workgroup][8 waves][16] u64 (phase B, wait,
  * phase C, wait, phase F, wait, loop total, samples, then F sub-phases:
- * GRU_B update, broadcast, tree levels 0-3, levels 4-7, output).  Returns
- * #workgroups. */
+ * GRU_B update, broadcast, tree levels 0-3, levels 4-7, output; the
+ * pipelined kernel records [0] X->Y work, [1] wait, [2] Y->Z work, [3] wait,
+ * [4] Z->X work, [5] wait per wave).  Returns #workgroups. */
 LPCNET_EXPORT int lpcnet_batch_set_stamps(LPCNetBatch *b, int enable);
 LPCNET_EXPORT int lpcnet_batch_get_stamps(LPCNetBatch *b, unsigned long long *out);
 

@@ -106,6 +106,8 @@ class ModelInfo(C.Structure):
         sat = "true" if self.may_saturate else "false"
         if self.quad_path == 2:
             return f"wave_kernel<{self.streams_per_workgroup}, {sat}>"
+        if self.quad_path == 3:
+            return f"pipe_kernel<{self.streams_per_workgroup}, {sat}>"
         quad = "true" if self.quad_path == 1 else "false"
         return f"sample_kernel<{self.streams_per_workgroup}, {self.variant}, {sat}, {quad}>"
 
@@ -198,7 +200,7 @@ class LPCNetBatch:
             raise LPCNetError(f"lpcnet_batch_load_model failed: {last_error()}")
 
     def set_kernel(self, mode: int) -> None:
-        """0 automatic, 1 lockstep sample kernel, 2 wave-per-stream kernel."""
+        """0 automatic, 1 lockstep sample kernel, 2 wave-per-stream kernel, 3 pipelined kernel."""
         if lib.lpcnet_batch_set_kernel(self._b, mode) != 0:
             raise LPCNetError("bad kernel mode")
 
@@ -291,8 +293,8 @@ class LPCNetBatch:
             raise LPCNetError(last_error())
 
     def get_stamps(self) -> np.ndarray:
-        """[workgroups, 6 waves, 16] s_memtime sums of the last sample-kernel launch."""
-        out = np.zeros((self.B, 6, 16), np.uint64)
+        """[workgroups, 8 waves, 16] s_memtime sums of the last sample-kernel launch."""
+        out = np.zeros((self.B, 8, 16), np.uint64)
         g = lib.lpcnet_batch_get_stamps(self._b, out.ctypes.data)
         if g < 0:
             raise LPCNetError("stamps not enabled")

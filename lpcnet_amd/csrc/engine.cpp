@@ -286,8 +286,9 @@ struct LPCNetBatch {
   int variant = 0;
   bool sat = false;
   bool reg = false;
-  int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 2 wave_kernel */
+  int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 2 wave_kernel, 3 pipe_kernel */
   int wave_nw = 0;       /* >0: wave_kernel with this many streams per workgroup */
+  bool pipe = false;     /* pipe_kernel (mode 3) */
   int image_bytes = 0;
   LPCNetModelInfo info{};
   std::vector<void *> model_bufs;
@@ -371,11 +372,11 @@ bool block_may_saturate(const int8_t *w)
 void choose_kernel(LPCNetBatch *b)
 {
   b->wave_nw = 0;
-  const bool can_wave = b->variant == LPCNET_VARIANT_INT8 && b->reg;
-  bool use_wave = false;  /* measured slower than lockstep (profiles/r01/perf_log.md) */
-  if (b->kernel_mode == 1) use_wave = false;
-  if (b->kernel_mode == 2) use_wave = can_wave;
-  if (use_wave) {
+  b->pipe = false;
+  const bool quad_int8 = b->variant == LPCNET_VARIANT_INT8 && b->reg;
+  int mode = b->kernel_mode;
+  if (mode == 0) mode = quad_int8 ? 3 : 1;
+  if (mode == 2 && quad_int8) {
     int nw = std::min(4, std::max(1, (b->B + 255) / 256));
     while (nw > 1 && wave_lds_bytes(nw, b->image_bytes) > 160 * 1024) nw /= 2;
     if (wave_lds_bytes(nw, b->image_bytes) <= 160 * 1024) {
@@ -385,6 +386,13 @@ void choose_kernel(LPCNetBatch *b)
       b->info.quad_path = 2;
       return;
     }
+  }
+  if (mode == 3 && quad_int8 && pipe_lds_bytes(b->S, b->image_bytes) <= 160 * 1024) {
+    b->pipe = true;
+    b->info.streams_per_workgroup = b->S;
+    b->info.lds_bytes = pipe_lds_bytes(b->S, b->image_bytes);
+    b->info.quad_path = 3;
+    return;
   }
   b->info.streams_per_workgroup = b->S;
   b->info.lds_bytes = b->lds_bytes;
@@ -526,22 +534,35 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
     if ((int)gb_blocks[rb].size() > 8 * REG_GB) reg = false;
   if (getenv("LPCNET_NO_QUAD")) reg = false; /* A/B switch: per-slot LDS layout */
   if (reg) {
-    /* quad layout: wave w, gate g, group gi of 4 slots, lane l = 8*(row block in wave) + row */
-    for (int w = 0; w < SAMPLE_WAVES; w++)
+    /* quad layout: wave w, gate g, group gi of 4 slots, lane l = 8*(row block in wave) + row.
+     * The z, r and h groups of one wave are contiguous (weights and column
+     * words alike), so the kernel runs them as one software-pipelined stream. */
+    for (int w = 0; w < SAMPLE_WAVES; w++) {
+      int K4[3], G = 0;
       for (int g = 0; g < 3; g++) {
-        const int K4 = (gaK[w][g] + 3) / 4;
-        sa.ga_K4[w][g] = K4;
-        std::vector<uint32_t> q((size_t)std::max(K4, 1) * 64 * 4, 0), c((size_t)std::max(K4, 1) * 8, 0);
+        K4[g] = (gaK[w][g] + 3) / 4;
+        sa.ga_K4[w][g] = K4[g];
+        G += K4[g];
+      }
+      std::vector<uint32_t> q((size_t)std::max(G, 1) * 64 * 4, 0), c((size_t)std::max(G, 1) * 8, 0);
+      int g0 = 0;
+      for (int g = 0; g < 3; g++) {
         for (int l = 0; l < 64; l++) {
           const int j = l >> 3, r = l & 7, rb = g * (NA / 8) + w * 8 + j;
           for (int k = 0; k < (int)ga_blocks[rb].size(); k++) {
-            memcpy(&q[((size_t)(k / 4) * 64 + l) * 4 + (k & 3)], (const int8_t *)gaw->data + 32 * (ga_first[rb] + k) + 4 * r, 4);
-            if (r == 0) c[(k / 4) * 8 + j] |= (uint32_t)(ga_blocks[rb][k] / 4) << (8 * (k & 3));
+            memcpy(&q[((size_t)(g0 + k / 4) * 64 + l) * 4 + (k & 3)], (const int8_t *)gaw->data + 32 * (ga_first[rb] + k) + 4 * r, 4);
+            if (r == 0) c[(g0 + k / 4) * 8 + j] |= (uint32_t)(ga_blocks[rb][k] / 4) << (8 * (k & 3));
           }
         }
-        sa.ga_qoff[w][g] = (int)(put(q.data(), q.size() * 4) / 16);
-        sa.ga_coff[w][g] = (int)(put(c.data(), c.size() * 4) / 4);
+        g0 += K4[g];
       }
+      const int qbase = (int)(put(q.data(), q.size() * 4) / 16);
+      const int cbase = (int)(put(c.data(), c.size() * 4) / 4);
+      for (int g = 0, acc = 0; g < 3; acc += K4[g], g++) {
+        sa.ga_qoff[w][g] = qbase + acc * 64;
+        sa.ga_coff[w][g] = cbase + acc * 8;
+      }
+    }
     for (int rb = 0; rb < GB_ROWS / 8; rb++) {
       std::vector<uint32_t> q((size_t)(REG_GB / 4) * 64 * 4, 0), c((size_t)(REG_GB / 4) * 8, 0);
       for (int l = 0; l < 64; l++) {
@@ -729,8 +750,9 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
   const int lrc = N <= 0 ? 0
-                : (b->wave_nw ? launch_wave(sa, b->wave_nw, b->sat ? 1 : 0, wave_lds_bytes(b->wave_nw, b->image_bytes), b->stream)
-                              : launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream));
+                : b->pipe  ? launch_pipe(sa, b->S, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
+                : b->wave_nw ? launch_wave(sa, b->wave_nw, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
+                             : launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream);
   if (lrc) {
     set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     return -1;
@@ -842,7 +864,7 @@ LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *d
 
 LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode)
 {
-  if (!b || mode < 0 || mode > 2) return -1;
+  if (!b || mode < 0 || mode > 3) return -1;
   b->kernel_mode = mode;
   if (b->have_model) choose_kernel(b);
   return 0;
@@ -1014,7 +1036,11 @@ LPCNET_EXPORT double lpcnet_batch_kernel_ms(LPCNetBatch *b, int which, int *laun
   return tot;
 }
 
-static int stamp_groups(const LPCNetBatch *b) { return (b->B + b->S - 1) / b->S; }
+static int stamp_groups(const LPCNetBatch *b)
+{
+  const int spw = std::max(1, b->info.streams_per_workgroup);
+  return (b->B + spw - 1) / spw;
+}
 
 LPCNET_EXPORT int lpcnet_batch_set_stamps(LPCNetBatch *b, int enable)
 {
@@ -1023,7 +1049,7 @@ LPCNET_EXPORT int lpcnet_batch_set_stamps(LPCNetBatch *b, int enable)
   if (b->d_stamps) (void)hipFree(b->d_stamps);
   b->d_stamps = nullptr;
   if (enable) {
-    size_t n = (size_t)b->B * SAMPLE_WAVES * 16; /* enough for any S */
+    size_t n = (size_t)b->B * STAMP_WAVES * 16; /* enough for any S */
     HIPCHK(hipMalloc(&b->d_stamps, n * 8));
     HIPCHK(hipMemset(b->d_stamps, 0, n * 8));
   }
@@ -1035,7 +1061,7 @@ LPCNET_EXPORT int lpcnet_batch_get_stamps(LPCNetBatch *b, unsigned long long *ou
   if (!b || !b->d_stamps || !b->have_model || b->set_device()) return -1;
   HIPCHK(hipStreamSynchronize(b->stream));
   int g = stamp_groups(b);
-  HIPCHK(hipMemcpy(out, b->d_stamps, (size_t)g * SAMPLE_WAVES * 16 * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out, b->d_stamps, (size_t)g * STAMP_WAVES * 16 * 8, hipMemcpyDeviceToHost));
   return g;
 }
 

@@ -412,6 +412,58 @@ __device__ __forceinline__ void gate_quad(const unsigned char *xa, const uint4 *
   }
 }
 
+/* Sum over the 8 lanes {l ^ 8k} (xor 8, 16, 32) without LDS: DPP row_ror:8
+ * inside each 16-lane row, then the gfx950 row-swap permutes.  Integer sums,
+ * so the order is immaterial. */
+__device__ __forceinline__ int sum_lanes_xor8_16_32(int x)
+{
+  x += __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);
+  const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  x = (int)p[0] + (int)p[1];
+  const auto q = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return (int)q[0] + (int)q[1];
+}
+
+/* The z, r and h quad groups of one wave as one software-pipelined stream
+ * (they are contiguous in the image): the column word is loaded two groups
+ * ahead and the x gathers one group ahead, so neither dependent LDS round
+ * trip (column word -> x address -> x) sits on the chain of a group; the
+ * dot4s of group g run while the gathers of g+1 are in flight.  Prefetches
+ * past the end re-read the last group. */
+template <int S, bool SAT>
+__device__ __forceinline__ void gru_a_stream(const unsigned char *xa, const uint4 *wq, const uint32_t *cq, int qoff,
+                                             int coff, int Kz, int Kr, int Kh, int lane, int *az, int *ar, int *ah)
+{
+  using X = typename XQ<S>::T;
+  const int G = Kz + Kr + Kh;
+  if (G == 0) return;
+  const uint4 *wp = wq + qoff + lane;
+  const uint32_t *cp = cq + coff + (lane >> 3);
+  auto xat = [&](uint32_t c, int b) -> X { return *(const X *)(xa + ((c >> (8 * b)) & 0xFF) * (S * 4)); };
+  const uint32_t c0 = cp[0];
+  uint32_t c1 = cp[min(1, G - 1) * 8];
+  uint4 w = wp[0];
+  X x0 = xat(c0, 0), x1 = xat(c0, 1), x2 = xat(c0, 2), x3 = xat(c0, 3);
+  int g = 0;
+  auto step = [&](int *acc) {
+    const int g1 = min(g + 1, G - 1), g2 = min(g + 2, G - 1);
+    const uint32_t c2 = cp[g2 * 8];
+    const uint4 wn = wp[g1 * 64];
+    const X y0 = xat(c1, 0), y1 = xat(c1, 1), y2 = xat(c1, 2), y3 = xat(c1, 3);
+    dot_x<S, SAT>(x0, w.x, acc);
+    dot_x<S, SAT>(x1, w.y, acc);
+    dot_x<S, SAT>(x2, w.z, acc);
+    dot_x<S, SAT>(x3, w.w, acc);
+    x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+    w = wn;
+    c1 = c2;
+    g++;
+  };
+  while (g < Kz) step(az);
+  while (g < Kz + Kr) step(ar);
+  while (g < G) step(ah);
+}
+
 template <int S, int V, bool SAT, bool REG>
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
 {
@@ -426,7 +478,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
   int *ix = (int *)(condb + S * GB_ROWS);
   short *pcmbuf = (short *)(ix + S * 4);
 
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6); /* wave-uniform */
   const int s0 = blockIdx.x * S;
   const uint32_t *rcp = (const uint32_t *)(lds + IMG_RCP);
   const float *ulaw = (const float *)(lds + IMG_ULAW);
@@ -535,6 +587,26 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
   const uint32_t *lds32 = (const uint32_t *)lds;
   const uint16_t *lds16 = (const uint16_t *)lds;
   const int j8 = lane >> 3;
+  /* dual_fc nodes 1..15 (tree levels 0..3) never change lane: node qq+1,
+   * channel lane&1 -> weights, bias and factor held in registers */
+  float f03w[NB], f03b = 0.f, f03f = 0.f;
+  {
+    const int q0 = lane >> 1, node = (q0 < 15 ? q0 : 0) + 1, c2 = lane & 1;
+#pragma unroll
+    for (int j = 0; j < NB; j++) f03w[j] = stream_wave ? fcw[node * 32 + c2 * 16 + j] : 0.f;
+    if (stream_wave) {
+      f03b = fcb[c2 * 256 + node];
+      f03f = fcf[c2 * 256 + node];
+    }
+  }
+  /* frame-constant GRU_B accumulator seeds of this lane's row (nnet.c:347-356) */
+  int gb_seed[S], gb_seedr = 0;
+  if constexpr (V == 0) {
+    const int row = wv * 8 + (lane & 7);
+    for (int s = 0; s < S; s++)
+      gb_seed[s] = cvt_rne((A.gb_par[row] + condb[s * GB_ROWS + row]) * kScale) + (SAT ? 0 : A.gb_wsum[row]);
+    gb_seedr = cvt_rne(A.gb_par[GB_ROWS + row] * kScale) + (SAT ? 0 : A.gb_wsum[GB_ROWS + row]);
+  }
 
   /* optional phase timing (diagnostics only): per wave, s_memtime sums of
    * [0] phase B work [1] barrier 1 wait [2] phase C [3] barrier 2 wait
@@ -580,9 +652,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
         }
         const unsigned char *xa = xa_base + cur * (NA / 4) * S * 4;
         if constexpr (REG) {
-          gate_quad<S, SAT>(xa, wq, cq, A.ga_qoff[wv][0], A.ga_coff[wv][0], K4z, lane, az);
-          gate_quad<S, SAT>(xa, wq, cq, A.ga_qoff[wv][1], A.ga_coff[wv][1], K4r, lane, ar);
-          gate_quad<S, SAT>(xa, wq, cq, A.ga_qoff[wv][2], A.ga_coff[wv][2], K4h, lane, ah);
+          gru_a_stream<S, SAT>(xa, wq, cq, A.ga_qoff[wv][0], A.ga_coff[wv][0], K4z, K4r, K4h, lane, az, ar, ah);
         } else {
           auto run_gate = [&](int g, int *acc) {
             const uint32_t *wp = lds32 + A.ga_woff[wv][g] + lane;
@@ -661,7 +731,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
         int acc[S], accr[S];
         for (int s = 0; s < S; s++) { acc[s] = 0; accr[s] = 0; }
         if constexpr (REG) {
-          gate_quad<S, SAT>(xa, wq, cq, A.gb_qoff[rb], A.gb_coff[rb], REG_GB / 4, lane, acc);
+          gru_a_stream<S, SAT>(xa, wq, cq, A.gb_qoff[rb], A.gb_coff[rb], REG_GB / 4, 0, 0, lane, acc, acc, acc);
         } else {
           const uint32_t *wp = lds32 + A.gb_woff[rb];
           const uint16_t *cp = lds16 + A.gb_coff[rb];
@@ -674,19 +744,13 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
           dot_streams<S, SAT>(xb, ks * S * 4, w, accr);
         }
         for (int s = 0; s < S; s++) {
-          acc[s] += __shfl_xor(acc[s], 8);
-          acc[s] += __shfl_xor(acc[s], 16);
-          acc[s] += __shfl_xor(acc[s], 32);
-          accr[s] += __shfl_xor(accr[s], 8);
-          accr[s] += __shfl_xor(accr[s], 16);
-          accr[s] += __shfl_xor(accr[s], 32);
+          acc[s] = sum_lanes_xor8_16_32(acc[s]);
+          accr[s] = sum_lanes_xor8_16_32(accr[s]);
         }
         if (ks == 0) {
           for (int s = 0; s < S; s++) {
-            int seed = cvt_rne((A.gb_par[row] + condb[s * GB_ROWS + row]) * kScale) + (SAT ? 0 : A.gb_wsum[row]);
-            int seedr = cvt_rne(A.gb_par[GB_ROWS + row] * kScale) + (SAT ? 0 : A.gb_wsum[GB_ROWS + row]);
-            zr[s * 2 * GB_ROWS + row] = (float)(seed + acc[s]) * kScale1;
-            zr[s * 2 * GB_ROWS + GB_ROWS + row] = (float)(seedr + accr[s]) * kScale1;
+            zr[s * 2 * GB_ROWS + row] = (float)(gb_seed[s] + acc[s]) * kScale1;
+            zr[s * 2 * GB_ROWS + GB_ROWS + row] = (float)(gb_seedr + accr[s]) * kScale1;
           }
         }
       } else {
@@ -758,21 +822,23 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
       const int q = lane >> 1, ch2 = lane & 1;
       const int qq = q < 15 ? q : 0;
       const int lvl_in = qq == 0 ? 0 : (qq < 3 ? 1 : (qq < 7 ? 2 : 3)); /* level of node qq+1 within 0..3 */
-      auto node_logit = [&](int node) -> float {
-        float sum = fcb[ch2 * 256 + node];
-        const float *w = fcw + node * 32 + ch2 * 16;
+      auto node_logit_w = [&](float bias, float factor, const float *w) -> float {
+        float sum = bias;
 #pragma unroll
         for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
-        const float v = fcf[ch2 * 256 + node] * tanh_x86(sum, rcp);
+        const float v = factor * tanh_x86(sum, rcp);
         /* sum1 + sum2 (nnet.c:205); adjacent-lane swap through DPP quad_perm [1,0,3,2] */
         const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
         return ch2 ? o + v : v + o;
+      };
+      auto node_logit = [&](int node) -> float {
+        return node_logit_w(fcb[ch2 * 256 + node], fcf[ch2 * 256 + node], fcw + node * 32 + ch2 * 16);
       };
       const bool tracing = A.trace_logits != nullptr;
       float lg[8];
       int val = 0;
       {
-        const float l = node_logit(qq + 1); /* levels 0..3: nodes 1..15 */
+        const float l = node_logit_w(f03b, f03f, f03w); /* levels 0..3: nodes 1..15, weights in registers */
         const float t = lvl_in == 0 ? thr[0] : (lvl_in == 1 ? thr[1] : (lvl_in == 2 ? thr[2] : thr[3]));
         const unsigned long long m = __ballot(t < l);
 #pragma unroll
@@ -839,7 +905,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
   if (stamping && lane == 0) {
     stp[6] = __builtin_amdgcn_s_memtime() - t_loop0;
     stp[7] = (unsigned long long)A.N;
-    for (int k = 0; k < 16; k++) A.stamps[((size_t)blockIdx.x * SAMPLE_WAVES + wv) * 16 + k] = stp[k];
+    for (int k = 0; k < 16; k++) A.stamps[((size_t)blockIdx.x * STAMP_WAVES + wv) * 16 + k] = stp[k];
   }
 
   /* ---- write back (only streams that synthesised this frame) ------------- */
@@ -888,7 +954,7 @@ __global__ __launch_bounds__(NW * 64) void wave_kernel(SampleArgs A)
 {
   extern __shared__ uint4 lds4[];
   unsigned char *lds = (unsigned char *)lds4;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6); /* wave-uniform */
   const int sid = blockIdx.x * NW + wv;
   const bool valid = sid < A.nstreams;
   const bool active = valid && A.st[sid].frame_count > FEATURES_DELAY;
@@ -1183,6 +1249,405 @@ int launch_frame(const FrameArgs &a, void *stream)
   int grid = (a.nstreams + FRAME_STREAMS - 1) / FRAME_STREAMS;
   hipLaunchKernelGGL(frame_kernel, dim3(grid), dim3(FRAME_THREADS), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* pipe_kernel: fixed wave roles, the GRU_A recurrent product of sample n+1
+ * overlapping the sampling of sample n.
+ *
+ * The recurrent part of GRU_A, W·q(h_A(n)) (sparse_sgemv_accum8x4 inside
+ * compute_sparse_gru, nnet.c:441), depends on the GRU_A state only, not on
+ * the excitation sampled at n (which enters sample n+1 through the embedding
+ * gathers, nnet.c:484-491).  So while the sampler waves run GRU_B's update
+ * and the dual-FC tree walk of sample n (nnet.c:362-371, 163-214), the six
+ * GRU_A waves already accumulate W·q(h_A(n)) for sample n+1 in registers.
+ * Per sample, three workgroup barriers:
+ *   X  ix(n) (sig, pred, exc indices) published by the samplers
+ *      GRU_A waves: embedding gathers + elementwise GRU_A(n) -> q(h_A(n))
+ *      sampler waves: the two kiss99 draws and their logit thresholds
+ *   Y  q(h_A(n)) complete
+ *      GRU_A wave w: GRU_B gate sums of row block w (nnet.c:345-361)
+ *   Z  GRU_B gate sums complete
+ *      GRU_A waves: W·q(h_A(n)) for sample n+1
+ *      sampler waves: GRU_B update, tree walk, output, pred(n+1) -> ix(n+1)
+ * Same arithmetic as sample_kernel's quad path, term for term. */
+template <int S>
+struct PipeLds {
+  static constexpr int x = (NA / 4) * S * 4;   /* quantized GRU_A state (single buffer) */
+  static constexpr int xb = (NB / 4) * S * 4;  /* quantized GRU_B state */
+  static constexpr int sb = S * NB * 4;        /* float GRU_B state */
+  static constexpr int zr = S * 2 * GB_ROWS * 4;
+  static constexpr int ix = S * 4 * 4;
+  static constexpr int pcm = S * FRAME * 2;
+  static constexpr int total = x + xb + sb + zr + ix + ((pcm + 15) / 16) * 16;
+};
+
+int pipe_lds_bytes(int S, int image_bytes)
+{
+  return image_bytes + (S == 4 ? PipeLds<4>::total : (S == 2 ? PipeLds<2>::total : PipeLds<1>::total));
+}
+
+template <int S, bool SAT>
+__global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
+{
+  extern __shared__ uint4 lds4[];
+  unsigned char *lds = (unsigned char *)lds4;
+  using L = PipeLds<S>;
+  unsigned char *xa = lds + A.image_bytes;
+  unsigned char *xb = xa + L::x;
+  float *sbuf = (float *)(xb + L::xb);
+  float *zr = sbuf + S * NB;
+  int *ix = (int *)(zr + S * 2 * GB_ROWS);
+  short *pcmbuf = (short *)(ix + S * 4);
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int s0 = blockIdx.x * S;
+  const uint32_t *rcp = (const uint32_t *)(lds + IMG_RCP);
+  const float *ulaw = (const float *)(lds + IMG_ULAW);
+  const float *logit_tab = (const float *)(lds + IMG_LOGIT);
+  const float *fcw = (const float *)(lds + IMG_FCW);
+  const float *fcb = (const float *)(lds + IMG_FCB);
+  const float *fcf = (const float *)(lds + IMG_FCF);
+
+  /* roles: waves 0..5 GRU_A (thread = unit), waves 6..7 samplers.  With S=4
+   * a sampler wave carries two streams, one per 32-lane half. */
+  const bool ga_wave = wv < SAMPLE_WAVES;
+  const int sw = wv - SAMPLE_WAVES;
+  const int half = lane >> 5, hl = lane & 31;
+  const int my_s = S == 4 ? 2 * sw + half : sw;
+  const bool samp = !ga_wave && my_s >= 0 && my_s < S;
+  const bool samp_w = samp && (S == 4 || half == 0); /* lanes that own the stream's outputs */
+
+  bool active[S];
+  bool any = false;
+  for (int s = 0; s < S; s++) {
+    const int sid = s0 + s;
+    active[s] = sid < A.nstreams && A.st[sid].frame_count > FEATURES_DELAY;
+    any |= active[s];
+  }
+  if (!any) {
+    for (int e = tid; e < S * A.N; e += PIPE_THREADS) {
+      const int s = e / A.N, n = e % A.N;
+      if (s0 + s < A.nstreams) A.pcm[(size_t)(s0 + s) * A.N + n] = 0;
+    }
+    return;
+  }
+  const int ms = samp ? my_s : 0;
+  const bool my_active = samp && s0 + ms < A.nstreams && A.st[s0 + ms].frame_count > FEATURES_DELAY;
+
+  for (int o = tid; o < A.image_bytes / 16; o += PIPE_THREADS) lds4[o] = A.image[o];
+
+  const uint4 *wq = (const uint4 *)lds;
+  const uint32_t *cq = (const uint32_t *)lds;
+
+  /* ---- GRU_A waves: unit i = tid ------------------------------------------ */
+  const int i = ga_wave ? tid : 0;
+  const int gw = ga_wave ? wv : 0;
+  const int K4z = A.ga_K4[gw][0], K4r = A.ga_K4[gw][1], K4h = A.ga_K4[gw][2];
+  const float bz = A.ga_par[i], br = A.ga_par[NA + i], bh = A.ga_par[2 * NA + i];
+  const float dz = A.ga_par[3 * NA + i], dr = A.ga_par[4 * NA + i], dh = A.ga_par[5 * NA + i];
+  const int wsz = A.ga_wsum[i], wsr = A.ga_wsum[NA + i], wsh = A.ga_wsum[2 * NA + i];
+  float st[S], cz[S], cr[S], ch[S];
+  int gb_seed[S], gb_seedr;
+  {
+    const int row = gw * 8 + (lane & 7);
+    for (int s = 0; s < S; s++) {
+      const StreamState *p = &A.st[min(s0 + s, A.nstreams - 1)];
+      st[s] = p->gru_a_state[i];
+      cz[s] = p->gru_a_cond[i];
+      cr[s] = p->gru_a_cond[NA + i];
+      ch[s] = p->gru_a_cond[2 * NA + i];
+      gb_seed[s] = cvt_rne((A.gb_par[row] + p->gru_b_cond[row]) * kScale) + (SAT ? 0 : A.gb_wsum[row]);
+    }
+    gb_seedr = cvt_rne(A.gb_par[GB_ROWS + row] * kScale) + (SAT ? 0 : A.gb_wsum[GB_ROWS + row]);
+  }
+
+  /* ---- sampler lanes: per-stream serial state ----------------------------- */
+  float lsr[NLPC], lpr[NLPC];
+  float sbv = 0.f, pred = 0.f, deemph = 0.f;
+  uint32_t rz = 0, rw = 0, rj = 0, rc = 0;
+  int last_exc = 0;
+#pragma unroll
+  for (int j = 0; j < NLPC; j++) { lsr[j] = 0.f; lpr[j] = 0.f; }
+  if (samp) {
+    const StreamState *p = &A.st[min(s0 + ms, A.nstreams - 1)];
+#pragma unroll
+    for (int j = 0; j < NLPC; j++) {
+      lsr[j] = p->last_sig[j];
+      lpr[j] = p->lpc[j];
+    }
+    sbv = p->gru_b_state[hl & (NB - 1)];
+    deemph = p->deemph_mem;
+    last_exc = p->last_exc;
+    rz = p->rng[0]; rw = p->rng[1]; rj = p->rng[2]; rc = p->rng[3];
+  }
+  const int q = hl >> 1, ch2 = lane & 1;
+  const int qq = q < 15 ? q : 0;
+  const int lvl_in = qq == 0 ? 0 : (qq < 3 ? 1 : (qq < 7 ? 2 : 3)); /* level of node qq+1 within 0..3 */
+  const int hb = 32 * half;                                          /* this half's bits in a ballot */
+  __syncthreads(); /* image in LDS */
+
+  float f03w[NB], f03b = 0.f, f03f = 0.f;
+#pragma unroll
+  for (int j = 0; j < NB; j++) f03w[j] = samp ? fcw[(qq + 1) * 32 + ch2 * 16 + j] : 0.f;
+  if (samp) {
+    f03b = fcb[ch2 * 256 + qq + 1];
+    f03f = fcf[ch2 * 256 + qq + 1];
+  }
+
+  if (ga_wave)
+    for (int s = 0; s < S; s++) xa[(i >> 2) * S * 4 + s * 4 + (i & 3)] = (unsigned char)quant_s8(st[s]);
+  if (samp_w && hl < NB) {
+    xb[(hl >> 2) * S * 4 + ms * 4 + (hl & 3)] = (unsigned char)quant_s8(sbv);
+    sbuf[ms * NB + hl] = sbv;
+  }
+  for (int e = tid; e < S * A.preload; e += PIPE_THREADS) {
+    const int s = e / A.preload, n = e % A.preload;
+    pcmbuf[s * FRAME + n] = A.pcm[(size_t)min(s0 + s, A.nstreams - 1) * A.N + n];
+  }
+  auto pre_sample = [&]() {
+    float p2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NLPC; j++) p2 = p2 - lsr[j] * lpr[j];
+    pred = p2;
+    const int su = lin2ulaw_x86(lsr[0]);
+    const int pu = lin2ulaw_x86(pred);
+    if (samp_w && hl == 0) {
+      ix[ms * 4 + 0] = su;
+      ix[ms * 4 + 1] = pu;
+      ix[ms * 4 + 2] = last_exc;
+    }
+  };
+  if (samp) pre_sample();
+  __syncthreads();
+
+  const bool stamping = A.stamps != nullptr;
+  unsigned long long stp[16] = {};
+  unsigned long long t_prev = stamping ? __builtin_amdgcn_s_memtime() : 0, t_loop0 = t_prev;
+  auto stamp = [&](int k) {
+    if (stamping) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      stp[k] += t - t_prev;
+      t_prev = t;
+    }
+  };
+
+  /* R(0): recurrent product over the initial state */
+  int az[S], ar[S], ah[S];
+  auto recurrent = [&]() {
+    for (int s = 0; s < S; s++) {
+      az[s] = SAT ? 0 : wsz;
+      ar[s] = SAT ? 0 : wsr;
+      ah[s] = SAT ? 0 : wsh;
+    }
+    gru_a_stream<S, SAT>(xa, wq, cq, A.ga_qoff[gw][0], A.ga_coff[gw][0], K4z, K4r, K4h, lane, az, ar, ah);
+  };
+  if (ga_wave) recurrent();
+
+  float thr[8];
+  const bool tracing = A.trace_logits != nullptr;
+  for (int n = 0; n < A.N; n++) {
+    stamp(4);
+    __syncthreads(); /* X */
+    stamp(5);
+    if (ga_wave) {
+      /* GRU_A input (nnet.c:484-491) and elementwise update (nnet.c:431-447) */
+      float gz[S], gr[S], gh[S], inh[S];
+      for (int s = 0; s < S; s++) {
+        const int sig = ix[s * 4 + 0] & 0xFF, prd = ix[s * 4 + 1] & 0xFF, exc = ix[s * 4 + 2] & 0xFF;
+        const float *e1 = A.emb_sig + sig * GA_ROWS, *e2 = A.emb_pred + prd * GA_ROWS, *e3 = A.emb_exc + exc * GA_ROWS;
+        const float inz = ((cz[s] + e1[i]) + e2[i]) + e3[i];
+        const float inr = ((cr[s] + e1[NA + i]) + e2[NA + i]) + e3[NA + i];
+        inh[s] = ((ch[s] + e1[2 * NA + i]) + e2[2 * NA + i]) + e3[2 * NA + i];
+        gz[s] = (float)(az[s] + cvt_rne(((bz + dz * st[s]) + inz) * kScale)) * kScale1;
+        gr[s] = (float)(ar[s] + cvt_rne(((br + dr * st[s]) + inr) * kScale)) * kScale1;
+        gh[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
+      }
+      for (int s = 0; s < S; s++) {
+        const float z = sigmoid_x86(gz[s], rcp);
+        const float r = sigmoid_x86(gr[s], rcp);
+        float h = gh[s] * r + inh[s];
+        h = tanh_x86(h, rcp);
+        st[s] = z * st[s] + (1.f - z) * h;
+        xa[(i >> 2) * S * 4 + s * 4 + (i & 3)] = (unsigned char)quant_s8(st[s]);
+      }
+    } else if (samp) {
+      /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
+      const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
+      const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        thr[b] = logit_tab[(r0 >> (8 * b)) & 0xFF];
+        thr[b + 4] = logit_tab[(r1 >> (8 * b)) & 0xFF];
+      }
+    }
+    stamp(0);
+    __syncthreads(); /* Y */
+    stamp(1);
+    if (ga_wave) {
+      /* GRU_B gate sums, wave w = row block w (nnet.c:345-361) */
+      const int rb = wv, r = lane & 7, ks = lane >> 3, row = rb * 8 + r;
+      int acc[S], accr[S];
+      for (int s = 0; s < S; s++) { acc[s] = 0; accr[s] = 0; }
+      gru_a_stream<S, SAT>(xa, wq, cq, A.gb_qoff[rb], A.gb_coff[rb], REG_GB / 4, 0, 0, lane, acc, acc, acc);
+      if (ks < NB / 4) {
+        const uint32_t w = ((const uint32_t *)(lds + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r];
+        dot_streams<S, SAT>(xb, ks * S * 4, w, accr);
+      }
+      for (int s = 0; s < S; s++) {
+        acc[s] = sum_lanes_xor8_16_32(acc[s]);
+        accr[s] = sum_lanes_xor8_16_32(accr[s]);
+      }
+      if (ks == 0) {
+        for (int s = 0; s < S; s++) {
+          zr[s * 2 * GB_ROWS + row] = (float)(gb_seed[s] + acc[s]) * kScale1;
+          zr[s * 2 * GB_ROWS + GB_ROWS + row] = (float)(gb_seedr + accr[s]) * kScale1;
+        }
+      }
+    }
+    stamp(2);
+    __syncthreads(); /* Z */
+    stamp(3);
+    if (ga_wave) {
+      if (n + 1 < A.N) recurrent();
+    } else if (samp) {
+      const int s = ms;
+      const float *zs = zr + s * 2 * GB_ROWS;
+      {
+        /* GRU_B elementwise (nnet.c:362-371); lanes >= 16 of a half duplicate */
+        const int u = hl & (NB - 1);
+        const float z = sigmoid_x86(zs[u] + zs[GB_ROWS + u], rcp);
+        const float r = sigmoid_x86(zs[NB + u] + zs[GB_ROWS + NB + u], rcp);
+        float h = zs[2 * NB + u] + zs[GB_ROWS + 2 * NB + u] * r;
+        h = tanh_x86(h, rcp);
+        sbv = z * sbv + (1.f - z) * h;
+        if (samp_w && hl < NB) sbuf[s * NB + hl] = sbv;
+      }
+      __builtin_amdgcn_wave_barrier();
+      float xv[NB];
+      {
+        const float4 *sb4 = (const float4 *)(sbuf + s * NB);
+#pragma unroll
+        for (int j = 0; j < NB / 4; j++) {
+          const float4 v = sb4[j];
+          xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
+        }
+      }
+      auto node_logit_w = [&](float bias, float factor, const float *w) -> float {
+        float sum = bias;
+#pragma unroll
+        for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
+        const float v = factor * tanh_x86(sum, rcp);
+        const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+        return ch2 ? o + v : v + o;
+      };
+      float lg[8];
+      int val = 0;
+      {
+        const float l = node_logit_w(f03b, f03f, f03w);
+        const float t = lvl_in == 0 ? thr[0] : (lvl_in == 1 ? thr[1] : (lvl_in == 2 ? thr[2] : thr[3]));
+        const unsigned long long m = __ballot(t < l) >> hb;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const int nd = (1 << b) | val;
+          if (tracing) lg[b] = __shfl(l, hb + 2 * (nd - 1));
+          val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
+        }
+      }
+      {
+        const int lvl = 4 + lvl_in;
+        const int off = qq + 1 - (1 << (lvl - 4));
+        const int node = (1 << lvl) | (val << (lvl - 4)) | off;
+        const float l = node_logit_w(fcb[ch2 * 256 + node], fcf[ch2 * 256 + node], fcw + node * 32 + ch2 * 16);
+        const float t = lvl_in == 0 ? thr[4] : (lvl_in == 1 ? thr[5] : (lvl_in == 2 ? thr[6] : thr[7]));
+        const unsigned long long m = __ballot(t < l) >> hb;
+#pragma unroll
+        for (int b = 4; b < 8; b++) {
+          const int qi = (1 << (b - 4)) - 1 + (val & ((1 << (b - 4)) - 1));
+          if (tracing) lg[b] = __shfl(l, hb + 2 * qi);
+          val = (val << 1) | (int)((m >> (2 * qi)) & 1ull);
+        }
+      }
+      int exc = val;
+      float pcm;
+      if (n < A.preload) {
+        const float o_in = (float)pcmbuf[s * FRAME + n];
+        const float pd = kPreemph * deemph;
+        exc = lin2ulaw_x86((o_in - pd) - pred);
+        pcm = o_in - pd;
+      } else {
+        pcm = pred + ulaw[exc];
+      }
+#pragma unroll
+      for (int j = NLPC - 1; j > 0; j--) lsr[j] = lsr[j - 1];
+      lsr[0] = pcm;
+      last_exc = exc;
+      float o = pcm + kPreemph * deemph;
+      deemph = o;
+      if (o < -32767) o = -32767;
+      if (o > 32767) o = 32767;
+      if (samp_w && hl == 0 && n >= A.preload) pcmbuf[s * FRAME + n] = (short)(int)floor(.5 + (double)o);
+      if (tracing && samp_w && hl < 8 && my_active) {
+        float v = lg[0];
+#pragma unroll
+        for (int b = 1; b < 8; b++) v = hl == b ? lg[b] : v;
+        A.trace_logits[((size_t)(s0 + s) * A.N + n) * 8 + hl] = v;
+      }
+      if (A.trace_exc && samp_w && hl == 0 && my_active) A.trace_exc[(size_t)(s0 + s) * A.N + n] = exc;
+      if (samp_w && hl < NB) xb[(hl >> 2) * S * 4 + s * 4 + (hl & 3)] = (unsigned char)quant_s8(sbv);
+      if (n + 1 < A.N) pre_sample();
+    }
+  }
+  stamp(4);
+  __syncthreads();
+  stamp(5);
+  if (stamping && lane == 0) {
+    stp[6] = __builtin_amdgcn_s_memtime() - t_loop0;
+    stp[7] = (unsigned long long)A.N;
+    for (int k = 0; k < 16; k++) A.stamps[((size_t)blockIdx.x * STAMP_WAVES + wv) * 16 + k] = stp[k];
+  }
+
+  if (ga_wave)
+    for (int s = 0; s < S; s++)
+      if (active[s]) A.st[s0 + s].gru_a_state[i] = st[s];
+  if (samp_w && my_active) {
+    StreamState *p = &A.st[s0 + ms];
+    if (hl < NB) p->gru_b_state[hl] = sbv;
+    if (hl == 0) {
+#pragma unroll
+      for (int j = 0; j < NLPC; j++) p->last_sig[j] = lsr[j];
+      p->deemph_mem = deemph;
+      p->last_exc = last_exc;
+      p->rng[0] = rz; p->rng[1] = rw; p->rng[2] = rj; p->rng[3] = rc;
+    }
+  }
+  for (int e = tid; e < S * A.N; e += PIPE_THREADS) {
+    const int s = e / A.N, n = e % A.N;
+    if (s0 + s < A.nstreams) A.pcm[(size_t)(s0 + s) * A.N + n] = active[s] ? pcmbuf[s * FRAME + n] : (short)0;
+  }
+}
+
+template <int S, bool SAT>
+static int launch_pipe_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
+{
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void *)pipe_kernel<S, SAT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+        hipSuccess)
+      return -1;
+    attr_set = true;
+  }
+  const int grid = (a.nstreams + S - 1) / S;
+  hipLaunchKernelGGL((pipe_kernel<S, SAT>), dim3(grid), dim3(PIPE_THREADS), lds_bytes, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_pipe(const SampleArgs &a, int S, int sat, int lds_bytes, void *stream)
+{
+  hipStream_t st = (hipStream_t)stream;
+  if (S == 4) return sat ? launch_pipe_t<4, true>(a, lds_bytes, st) : launch_pipe_t<4, false>(a, lds_bytes, st);
+  if (S == 2) return sat ? launch_pipe_t<2, true>(a, lds_bytes, st) : launch_pipe_t<2, false>(a, lds_bytes, st);
+  return sat ? launch_pipe_t<1, true>(a, lds_bytes, st) : launch_pipe_t<1, false>(a, lds_bytes, st);
 }
 
 template <int S, int V, bool SAT, bool REG>

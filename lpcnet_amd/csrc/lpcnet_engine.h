@@ -25,6 +25,9 @@ constexpr int GB_ROWS = 3 * NB;
 constexpr int FEATURES_DELAY = 2;
 constexpr int SAMPLE_THREADS = 384; /* one thread per GRU_A unit */
 constexpr int SAMPLE_WAVES = SAMPLE_THREADS / 64;
+constexpr int PIPE_THREADS = 512;   /* pipe_kernel: 6 GRU_A waves + 2 sampler waves */
+constexpr int PIPE_WAVES = PIPE_THREADS / 64;
+constexpr int STAMP_WAVES = PIPE_WAVES; /* stamps are [workgroup][STAMP_WAVES][16] */
 constexpr int FRAME_THREADS = 256;
 constexpr int FRAME_STREAMS = 4;    /* streams per frame-network workgroup */
 constexpr int REG_GB = 12;          /* GRU_B input slots per lane: block k = ks + 8*j, j < 12 */
@@ -97,7 +100,7 @@ struct SampleArgs {
   const float4 *ga_wf;   /* fp32 variant: GRU_A blocks [chunk][k][64] float4 */
   const float4 *gb_wf;   /* fp32 variant: GRU_B blocks [rb][k][8 rows][2] float4 (in c) */
   const float *gb_recf;  /* fp32 variant: GRU_B recurrent [NB][GB_ROWS] */
-  unsigned long long *stamps; /* optional diagnostics [grid][6 waves][8] s_memtime sums */
+  unsigned long long *stamps; /* optional diagnostics [grid][STAMP_WAVES][16] s_memtime sums */
   float *trace_logits;   /* optional [B][N][8] */
   int *trace_exc;        /* optional [B][N] */
 };
@@ -111,6 +114,10 @@ int launch_sample(const SampleArgs &a, int S, int variant, int sat, int reg, int
 /* Wave-per-stream sample kernel (int8 quad layout): nw streams per workgroup. */
 int wave_lds_bytes(int nw, int image_bytes);
 int launch_wave(const SampleArgs &a, int nw, int sat, int lds_bytes, void *stream);
+/* Pipelined int8 quad-layout kernel: the GRU_A recurrent product of sample
+ * n+1 overlaps the sampling of sample n (fixed wave roles). */
+int pipe_lds_bytes(int S, int image_bytes);
+int launch_pipe(const SampleArgs &a, int S, int sat, int lds_bytes, void *stream);
 
 /* Host LPC (lpc_host.cpp). */
 float lpc_from_cepstrum_host(float *lpc, const float *ceps);

@@ -30,15 +30,18 @@ def blobs():
 
 
 @pytest.mark.parametrize("name,kernel", [("streams_int8", 1), ("streams_fp32", 1), ("streams_int8_sat", 1),
-                                         ("streams_int8", 2), ("streams_int8_sat", 2)])
+                                         ("streams_int8", 2), ("streams_int8_sat", 2),
+                                         ("streams_int8", 3), ("streams_int8_sat", 3), ("streams_fp32", 3)])
 def test_batch_matches_golden(require_gpu, blobs, name, kernel):
-    """kernel 1: lockstep sample_kernel, 2: wave-per-stream kernel."""
+    """kernel 1: lockstep sample_kernel, 2: wave-per-stream, 3: pipelined
+    (fp32 models always run the lockstep kernel)."""
     G = np.load(os.path.join(GOLD, name + ".npz"))
     streams = list(G["streams"])
     F = G["pcm"].shape[1]
     b = L.LPCNetBatch(len(streams), 0, blobs[name])
     b.set_kernel(kernel)
-    assert (b.info().quad_path == 2) == (kernel == 2)
+    expect = 1 if kernel == 1 or name == "streams_fp32" else kernel
+    assert b.info().quad_path == (0 if name == "streams_fp32" else expect)
     info = b.info()
     assert info.variant == int(G["variant"])
     if name.endswith("_sat"):
@@ -73,7 +76,8 @@ def test_single_stream_api_matches_golden(require_gpu, blobs):
 
 @pytest.mark.parametrize("B,check,kernel", [(512, (0, 255, 511), 1), (1024, (0, 3, 517, 1023), 1),
                                             (1100, (1099, 1024, 5), 1), (1024, (0, 3, 517, 1023), 0),
-                                            (1101, (1100, 1024, 5), 0), (300, (299, 7), 2)])
+                                            (1101, (1100, 1024, 5), 0), (300, (299, 7), 2),
+                                            (513, (512, 1, 300), 3), (1030, (1029, 1027, 2), 3)])
 def test_large_batch_streams_match_oracle(require_gpu, blobs, B, check, kernel):
     """Lockstep kernel at 2 and 4 streams/workgroup, the wave-per-stream kernel
     (auto at >= 256 streams), ragged last workgroups, against the oracle."""
@@ -153,7 +157,7 @@ def test_full_size_properties(require_gpu, blobs):
     assert np.abs(o1[:, 2:].astype(np.float64)).mean() > 100
 
 
-@pytest.mark.parametrize("kernel", [1, 2])
+@pytest.mark.parametrize("kernel", [1, 2, 3])
 def test_preload_teacher_forcing_matches_oracle(require_gpu, blobs, kernel):
     """lpcnet_synthesize_impl with preload (lpcnet.c:256-259, the PLC entry)."""
     blob = blobs["streams_int8"]

@@ -6,7 +6,7 @@ timeout -k 10 420 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpur
 rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 120 python tools/phase_profile.py > gpurun_out/phase.log 2>&1 || { echo "phase rc=$?"; exit 1; }
-grep -E "B=|wave 0|wave 4|F detail" gpurun_out/phase.log
+grep -E "B=|wave [0-7]|F detail" gpurun_out/phase.log
 timeout -k 10 200 python bench.py --steps 20 --no-cpu > gpurun_out/bench.log 2>&1 || exit $?
 python3 -c "
 import json; d=json.loads(open('gpurun_out/bench.log').read().strip().splitlines()[-1])

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-phase cycle breakdown of the sample kernel (s_memtime stamps).
+"""Per-phase cycle breakdown of the sample kernels (s_memtime stamps).
 Diagnostic build path only: the stamps are off in every timed run."""
 import os
 import sys
@@ -10,34 +10,40 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import lpcnet_amd as L  # noqa: E402
 
-NAMES = ["B(gru_a)", "wait1", "C(gru_b)", "wait2", "F(sample)", "wait3"]
+NAMES = {1: ["B(gru_a)", "wait1", "C(gru_b)", "wait2", "F(sample)", "wait3"],
+         3: ["X->Y", "waitY", "Y->Z", "waitZ", "Z->X", "waitX"]}
 
 
-def profile(B, variant=0):
+def profile(B, variant=0, kernel=1):
     blob = L.synthetic_model(1, variant)
     b = L.LPCNetBatch(B, 0, blob)
-    b.set_kernel(1)  # stamps are instrumented in the lockstep kernel only
+    b.set_kernel(kernel)
     F = 4
     allf = np.stack([L.synthetic_features(s, F)[:, :20] for s in range(B)], 1)
     for f in range(3):
         b.synthesize(allf[f])
     b.set_stamps(True)
     b.synthesize(allf[3])
-    st = b.get_stamps().astype(np.float64)  # [g][6][16]
-    n = st[:, :, 7].max()
+    st = b.get_stamps().astype(np.float64)  # [g][8][16]
+    n = max(st[:, :, 7].max(), 1)
     per = st / n  # cycles per sample
     info = b.info()
-    print(f"B={B} variant={variant} S={info.streams_per_workgroup} quad={info.quad_path} groups={st.shape[0]}")
-    for w in range(6):
+    k = 3 if info.quad_path == 3 else 1
+    print(f"B={B} variant={variant} kernel={info.kernel_name} groups={st.shape[0]}")
+    for w in range(8):
         row = per[:, w, :].mean(0)
-        print(f"  wave {w}: " + " ".join(f"{NAMES[k]}={row[k]:7.0f}" for k in range(6)) + f"  loop={row[6]:7.0f}")
-    row = per[:, 0, :].mean(0)
-    print("  F detail (wave 0): gru_b=%.0f bcast=%.0f lvl0-3=%.0f lvl4-7=%.0f out=%.0f pre=%.0f" %
-          (row[8], row[9], row[10], row[11], row[12], row[4]))
+        if row[6] == 0:
+            continue
+        print(f"  wave {w}: " + " ".join(f"{NAMES[k][j]}={row[j]:7.0f}" for j in range(6)) + f"  loop={row[6]:7.0f}")
+    if k == 1:
+        row = per[:, 0, :].mean(0)
+        print("  F detail (wave 0): gru_b=%.0f bcast=%.0f lvl0-3=%.0f lvl4-7=%.0f out=%.0f pre=%.0f" %
+              (row[8], row[9], row[10], row[11], row[12], row[4]))
     b.close()
 
 
 if __name__ == "__main__":
-    for B in (1, 1024):
-        profile(B)
+    for kern in (1, 3):
+        for B in (1, 1024):
+            profile(B, 0, kern)
     profile(1, 1)
