@@ -77,6 +77,68 @@ __device__ __forceinline__ float sigmoid_x86(float X, const uint32_t *tab)
   return mm_max(0.f, mm_min(1.f, num));
 }
 
+/* N independent rcp_x86: all N table reads are issued before any is pinned,
+ * so their LDS latencies overlap (rcp_x86's pin alone serialises a chain). */
+__device__ __forceinline__ float rcp_x86_fix(float x, uint32_t t)
+{
+  const uint32_t u = __float_as_uint(x);
+  const uint32_t sign = u & 0x80000000u;
+  const int e = (int)((u >> 23) & 0xff);
+  const int te = (int)((t >> 23) & 0xff) + 127 - e;
+  uint32_t r = sign | (t & 0x007fffffu) | ((uint32_t)te << 23);
+  r = te < 1 ? sign : r;
+  const uint32_t spec = (u & 0x7fffffu) ? (u | 0x00400000u) : sign;
+  r = e == 255 ? spec : r;
+  r = e == 0 ? (sign | 0x7f800000u) : r;
+  return __uint_as_float(r);
+}
+
+template <int N>
+__device__ __forceinline__ void rcp_x86_n(float (&x)[N], const uint32_t *tab)
+{
+  uint32_t t[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) t[k] = tab[(__float_as_uint(x[k]) >> 12) & 0x7ff];
+#pragma unroll
+  for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
+#pragma unroll
+  for (int k = 0; k < N; k++) x[k] = rcp_x86_fix(x[k], t[k]);
+}
+
+/* N sigmoid8_approx / tanh8_approx lanes with one batched rcp (same
+ * arithmetic as sigmoid_x86 / tanh_x86, term for term) */
+template <int N>
+__device__ __forceinline__ void sigmoid_x86_n(float (&X)[N], const uint32_t *tab)
+{
+  float num[N], den[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const float X2 = X[k] * X[k];
+    num[k] = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
+    den[k] = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
+    num[k] = num[k] * X[k];
+  }
+  rcp_x86_n<N>(den, tab);
+#pragma unroll
+  for (int k = 0; k < N; k++) X[k] = mm_max(0.f, mm_min(1.f, __builtin_fmaf(num[k], den[k], 0.5f)));
+}
+
+template <int N>
+__device__ __forceinline__ void tanh_x86_n(float (&X)[N], const uint32_t *tab)
+{
+  float num[N], den[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const float X2 = X[k] * X[k];
+    num[k] = __builtin_fmaf(__builtin_fmaf(0.60863042f, X2, 96.39235687f), X2, 952.52801514f);
+    den[k] = __builtin_fmaf(__builtin_fmaf(11.88600922f, X2, 413.36801147f), X2, 952.72399902f);
+    num[k] = num[k] * X[k];
+  }
+  rcp_x86_n<N>(den, tab);
+#pragma unroll
+  for (int k = 0; k < N; k++) X[k] = mm_max(-1.f, mm_min(1.f, num[k] * den[k]));
+}
+
 /* _mm256_cvtps_epi32: round to nearest even, out of range / NaN -> INT_MIN */
 __device__ __forceinline__ int cvt_rne(float v)
 {
@@ -96,6 +158,7 @@ __device__ __forceinline__ uint32_t quant_s8(float x)
 constexpr float kScale = 128.f * 127.f;          /* vec_avx.h:686 */
 constexpr float kScale1 = 1.f / 128.f / 127.f;   /* vec_avx.h:687 */
 constexpr float kLog256 = 5.5451774445f;         /* common.h:17 */
+constexpr float kRcpLog256 = 1.f / kLog256;       /* RN(1/log 256), see lin2ulaw_x86 */
 constexpr float kPreemph = 0.85f;                /* lpcnet.c:40 */
 
 /* common.h:18-33, 47-58 lin2ulaw */
@@ -111,11 +174,26 @@ __device__ __forceinline__ int lin2ulaw_x86(float x)
   float frac = __uint_as_float(bits) - 1.5f;
   frac = -0.41445418f + frac * (0.95909232f + frac * (-0.33951290f + frac * 0.16541097f));
   float l2 = (float)(1 + integer) + frac;
-  float u = (float)s * ((128.f * (0.69315f * l2)) / kLog256);
+  /* RN(v / log(256)) by one FMA-corrected product: exact for every v in
+   * [2^-10, 2^15) (oracle/checks/exact_identities.c); v here is in
+   * [0.0395, 11500] */
+  const float v = 128.f * (0.69315f * l2);
+  const float q0 = v * kRcpLog256;
+  const float q = __builtin_fmaf(__builtin_fmaf(-q0, kLog256, v), kRcpLog256, q0);
+  float u = (float)s * q;
   u = 128.f + u;
   if (u < 0) u = 0;
   if (u > 255) u = 255;
-  return (int)floor(.5 + (double)u);
+  /* (int)floor(.5 + (double)u) for u in [0, 255] (exact_identities.c) */
+  const int k = (int)u;
+  return k + (u - (float)k >= .5f ? 1 : 0);
+}
+
+/* (int)floor(.5 + (double)o) for |o| <= 32767 (exact_identities.c) */
+__device__ __forceinline__ int round_half_up(float o)
+{
+  const float k = floorf(o);
+  return (int)k + (o - k >= .5f ? 1 : 0);
 }
 
 /* kiss99.c:59-81 */
@@ -884,7 +962,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
       deemph = o;
       if (o < -32767) o = -32767;
       if (o > 32767) o = 32767;
-      if (lane == 0 && n >= A.preload) pcmbuf[s * FRAME + n] = (short)(int)floor(.5 + (double)o);
+      if (lane == 0 && n >= A.preload) pcmbuf[s * FRAME + n] = (short)round_half_up(o);
       if (tracing && lane < 8 && active[s]) {
         float v = lg[0];
 #pragma unroll
@@ -1193,7 +1271,7 @@ __global__ __launch_bounds__(NW * 64) void wave_kernel(SampleArgs A)
     deemph = o;
     if (o < -32767) o = -32767;
     if (o > 32767) o = 32767;
-    if (lane == 0 && n >= A.preload) pcmbuf[n] = (short)(int)floor(.5 + (double)o);
+    if (lane == 0 && n >= A.preload) pcmbuf[n] = (short)round_half_up(o);
     if (tracing && lane < 8) {
       float v = lg[0];
 #pragma unroll
@@ -1303,20 +1381,6 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = blockIdx.x * S;
   const uint32_t *rcp = (const uint32_t *)(lds + IMG_RCP);
-  const float *ulaw = (const float *)(lds + IMG_ULAW);
-  const float *logit_tab = (const float *)(lds + IMG_LOGIT);
-  const float *fcw = (const float *)(lds + IMG_FCW);
-  const float *fcb = (const float *)(lds + IMG_FCB);
-  const float *fcf = (const float *)(lds + IMG_FCF);
-
-  /* roles: waves 0..5 GRU_A (thread = unit), waves 6..7 samplers.  With S=4
-   * a sampler wave carries two streams, one per 32-lane half. */
-  const bool ga_wave = wv < SAMPLE_WAVES;
-  const int sw = wv - SAMPLE_WAVES;
-  const int half = lane >> 5, hl = lane & 31;
-  const int my_s = S == 4 ? 2 * sw + half : sw;
-  const bool samp = !ga_wave && my_s >= 0 && my_s < S;
-  const bool samp_w = samp && (S == 4 || half == 0); /* lanes that own the stream's outputs */
 
   bool active[S];
   bool any = false;
@@ -1332,25 +1396,43 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
     }
     return;
   }
-  const int ms = samp ? my_s : 0;
-  const bool my_active = samp && s0 + ms < A.nstreams && A.st[s0 + ms].frame_count > FEATURES_DELAY;
-
   for (int o = tid; o < A.image_bytes / 16; o += PIPE_THREADS) lds4[o] = A.image[o];
+  for (int e = tid; e < S * A.preload; e += PIPE_THREADS) {
+    const int s = e / A.preload, n = e % A.preload;
+    pcmbuf[s * FRAME + n] = A.pcm[(size_t)min(s0 + s, A.nstreams - 1) * A.N + n];
+  }
 
-  const uint4 *wq = (const uint4 *)lds;
-  const uint32_t *cq = (const uint32_t *)lds;
+  const bool stamping = A.stamps != nullptr;
+  unsigned long long stp[16] = {};
+  unsigned long long t_prev = 0, t_loop0 = 0;
+  auto stamp = [&](int k) {
+    if (stamping) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      stp[k] += t - t_prev;
+      t_prev = t;
+    }
+  };
+  auto stamp_start = [&]() {
+    if (stamping) t_prev = t_loop0 = __builtin_amdgcn_s_memtime();
+  };
 
-  /* ---- GRU_A waves: unit i = tid ------------------------------------------ */
-  const int i = ga_wave ? tid : 0;
-  const int gw = ga_wave ? wv : 0;
-  const int K4z = A.ga_K4[gw][0], K4r = A.ga_K4[gw][1], K4h = A.ga_K4[gw][2];
-  const float bz = A.ga_par[i], br = A.ga_par[NA + i], bh = A.ga_par[2 * NA + i];
-  const float dz = A.ga_par[3 * NA + i], dr = A.ga_par[4 * NA + i], dh = A.ga_par[5 * NA + i];
-  const int wsz = A.ga_wsum[i], wsr = A.ga_wsum[NA + i], wsh = A.ga_wsum[2 * NA + i];
-  float st[S], cz[S], cr[S], ch[S];
-  int gb_seed[S], gb_seedr;
-  {
-    const int row = gw * 8 + (lane & 7);
+  /* Roles (wave-uniform): waves 0..5 GRU_A (thread = unit), waves 6..7
+   * samplers.  Each role runs its own sample loop with the same barrier
+   * sequence (prologue, then X, Y, Z per sample, then one final), so the
+   * registers of one role are not live in the other's code. */
+  if (wv < SAMPLE_WAVES) {
+    /* ======================= GRU_A role ================================== */
+    const uint4 *wq = (const uint4 *)lds;
+    const uint32_t *cq = (const uint32_t *)lds;
+    const int i = tid;
+    const int K4z = A.ga_K4[wv][0], K4r = A.ga_K4[wv][1], K4h = A.ga_K4[wv][2];
+    const int qoff = A.ga_qoff[wv][0], coff = A.ga_coff[wv][0];
+    const float bz = A.ga_par[i], br = A.ga_par[NA + i], bh = A.ga_par[2 * NA + i];
+    const float dz = A.ga_par[3 * NA + i], dr = A.ga_par[4 * NA + i], dh = A.ga_par[5 * NA + i];
+    const int wsz = A.ga_wsum[i], wsr = A.ga_wsum[NA + i], wsh = A.ga_wsum[2 * NA + i];
+    const int rb = wv, r8 = lane & 7, ks = lane >> 3, row = rb * 8 + r8;
+    float st[S], cz[S], cr[S], ch[S];
+    int gb_seed[S];
     for (int s = 0; s < S; s++) {
       const StreamState *p = &A.st[min(s0 + s, A.nstreams - 1)];
       st[s] = p->gru_a_state[i];
@@ -1359,187 +1441,207 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
       ch[s] = p->gru_a_cond[2 * NA + i];
       gb_seed[s] = cvt_rne((A.gb_par[row] + p->gru_b_cond[row]) * kScale) + (SAT ? 0 : A.gb_wsum[row]);
     }
-    gb_seedr = cvt_rne(A.gb_par[GB_ROWS + row] * kScale) + (SAT ? 0 : A.gb_wsum[GB_ROWS + row]);
-  }
-
-  /* ---- sampler lanes: per-stream serial state ----------------------------- */
-  float lsr[NLPC], lpr[NLPC];
-  float sbv = 0.f, pred = 0.f, deemph = 0.f;
-  uint32_t rz = 0, rw = 0, rj = 0, rc = 0;
-  int last_exc = 0;
-#pragma unroll
-  for (int j = 0; j < NLPC; j++) { lsr[j] = 0.f; lpr[j] = 0.f; }
-  if (samp) {
-    const StreamState *p = &A.st[min(s0 + ms, A.nstreams - 1)];
-#pragma unroll
-    for (int j = 0; j < NLPC; j++) {
-      lsr[j] = p->last_sig[j];
-      lpr[j] = p->lpc[j];
-    }
-    sbv = p->gru_b_state[hl & (NB - 1)];
-    deemph = p->deemph_mem;
-    last_exc = p->last_exc;
-    rz = p->rng[0]; rw = p->rng[1]; rj = p->rng[2]; rc = p->rng[3];
-  }
-  const int q = hl >> 1, ch2 = lane & 1;
-  const int qq = q < 15 ? q : 0;
-  const int lvl_in = qq == 0 ? 0 : (qq < 3 ? 1 : (qq < 7 ? 2 : 3)); /* level of node qq+1 within 0..3 */
-  const int hb = 32 * half;                                          /* this half's bits in a ballot */
-  __syncthreads(); /* image in LDS */
-
-  float f03w[NB], f03b = 0.f, f03f = 0.f;
-#pragma unroll
-  for (int j = 0; j < NB; j++) f03w[j] = samp ? fcw[(qq + 1) * 32 + ch2 * 16 + j] : 0.f;
-  if (samp) {
-    f03b = fcb[ch2 * 256 + qq + 1];
-    f03f = fcf[ch2 * 256 + qq + 1];
-  }
-
-  if (ga_wave)
+    const int gb_seedr = cvt_rne(A.gb_par[GB_ROWS + row] * kScale) + (SAT ? 0 : A.gb_wsum[GB_ROWS + row]);
+    __syncthreads(); /* image in LDS */
     for (int s = 0; s < S; s++) xa[(i >> 2) * S * 4 + s * 4 + (i & 3)] = (unsigned char)quant_s8(st[s]);
-  if (samp_w && hl < NB) {
-    xb[(hl >> 2) * S * 4 + ms * 4 + (hl & 3)] = (unsigned char)quant_s8(sbv);
-    sbuf[ms * NB + hl] = sbv;
-  }
-  for (int e = tid; e < S * A.preload; e += PIPE_THREADS) {
-    const int s = e / A.preload, n = e % A.preload;
-    pcmbuf[s * FRAME + n] = A.pcm[(size_t)min(s0 + s, A.nstreams - 1) * A.N + n];
-  }
-  auto pre_sample = [&]() {
-    float p2 = 0.f;
-#pragma unroll
-    for (int j = 0; j < NLPC; j++) p2 = p2 - lsr[j] * lpr[j];
-    pred = p2;
-    const int su = lin2ulaw_x86(lsr[0]);
-    const int pu = lin2ulaw_x86(pred);
-    if (samp_w && hl == 0) {
-      ix[ms * 4 + 0] = su;
-      ix[ms * 4 + 1] = pu;
-      ix[ms * 4 + 2] = last_exc;
-    }
-  };
-  if (samp) pre_sample();
-  __syncthreads();
+    __syncthreads(); /* initial q(h_A), q(h_B), ix */
+    stamp_start();
 
-  const bool stamping = A.stamps != nullptr;
-  unsigned long long stp[16] = {};
-  unsigned long long t_prev = stamping ? __builtin_amdgcn_s_memtime() : 0, t_loop0 = t_prev;
-  auto stamp = [&](int k) {
-    if (stamping) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      stp[k] += t - t_prev;
-      t_prev = t;
-    }
-  };
-
-  /* R(0): recurrent product over the initial state */
-  int az[S], ar[S], ah[S];
-  auto recurrent = [&]() {
-    for (int s = 0; s < S; s++) {
-      az[s] = SAT ? 0 : wsz;
-      ar[s] = SAT ? 0 : wsr;
-      ah[s] = SAT ? 0 : wsh;
-    }
-    gru_a_stream<S, SAT>(xa, wq, cq, A.ga_qoff[gw][0], A.ga_coff[gw][0], K4z, K4r, K4h, lane, az, ar, ah);
-  };
-  if (ga_wave) recurrent();
-
-  float thr[8];
-  const bool tracing = A.trace_logits != nullptr;
-  for (int n = 0; n < A.N; n++) {
-    stamp(4);
-    __syncthreads(); /* X */
-    stamp(5);
-    if (ga_wave) {
-      /* GRU_A input (nnet.c:484-491) and elementwise update (nnet.c:431-447) */
-      float gz[S], gr[S], gh[S], inh[S];
+    int az[S], ar[S], ah[S];
+    auto recurrent = [&]() {
       for (int s = 0; s < S; s++) {
-        const int sig = ix[s * 4 + 0] & 0xFF, prd = ix[s * 4 + 1] & 0xFF, exc = ix[s * 4 + 2] & 0xFF;
-        const float *e1 = A.emb_sig + sig * GA_ROWS, *e2 = A.emb_pred + prd * GA_ROWS, *e3 = A.emb_exc + exc * GA_ROWS;
-        const float inz = ((cz[s] + e1[i]) + e2[i]) + e3[i];
-        const float inr = ((cr[s] + e1[NA + i]) + e2[NA + i]) + e3[NA + i];
-        inh[s] = ((ch[s] + e1[2 * NA + i]) + e2[2 * NA + i]) + e3[2 * NA + i];
-        gz[s] = (float)(az[s] + cvt_rne(((bz + dz * st[s]) + inz) * kScale)) * kScale1;
-        gr[s] = (float)(ar[s] + cvt_rne(((br + dr * st[s]) + inr) * kScale)) * kScale1;
-        gh[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
+        az[s] = SAT ? 0 : wsz;
+        ar[s] = SAT ? 0 : wsr;
+        ah[s] = SAT ? 0 : wsh;
       }
-      for (int s = 0; s < S; s++) {
-        const float z = sigmoid_x86(gz[s], rcp);
-        const float r = sigmoid_x86(gr[s], rcp);
-        float h = gh[s] * r + inh[s];
-        h = tanh_x86(h, rcp);
-        st[s] = z * st[s] + (1.f - z) * h;
-        xa[(i >> 2) * S * 4 + s * 4 + (i & 3)] = (unsigned char)quant_s8(st[s]);
-      }
-    } else if (samp) {
-      /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
-      const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
-      const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        thr[b] = logit_tab[(r0 >> (8 * b)) & 0xFF];
-        thr[b + 4] = logit_tab[(r1 >> (8 * b)) & 0xFF];
-      }
-    }
-    stamp(0);
-    __syncthreads(); /* Y */
-    stamp(1);
-    if (ga_wave) {
-      /* GRU_B gate sums, wave w = row block w (nnet.c:345-361) */
-      const int rb = wv, r = lane & 7, ks = lane >> 3, row = rb * 8 + r;
-      int acc[S], accr[S];
-      for (int s = 0; s < S; s++) { acc[s] = 0; accr[s] = 0; }
-      gru_a_stream<S, SAT>(xa, wq, cq, A.gb_qoff[rb], A.gb_coff[rb], REG_GB / 4, 0, 0, lane, acc, acc, acc);
-      if (ks < NB / 4) {
-        const uint32_t w = ((const uint32_t *)(lds + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r];
-        dot_streams<S, SAT>(xb, ks * S * 4, w, accr);
-      }
-      for (int s = 0; s < S; s++) {
-        acc[s] = sum_lanes_xor8_16_32(acc[s]);
-        accr[s] = sum_lanes_xor8_16_32(accr[s]);
-      }
-      if (ks == 0) {
+      gru_a_stream<S, SAT>(xa, wq, cq, qoff, coff, K4z, K4r, K4h, lane, az, ar, ah);
+    };
+    recurrent();
+    for (int n = 0; n < A.N; n++) {
+      stamp(4);
+      __syncthreads(); /* X */
+      stamp(5);
+      {
+        /* GRU_A input (nnet.c:484-491): all 9*S gathers in flight at once */
+        float e[S][9];
         for (int s = 0; s < S; s++) {
-          zr[s * 2 * GB_ROWS + row] = (float)(gb_seed[s] + acc[s]) * kScale1;
-          zr[s * 2 * GB_ROWS + GB_ROWS + row] = (float)(gb_seedr + accr[s]) * kScale1;
+          const int4 v = *(const int4 *)(ix + s * 4);
+          const float *e1 = A.emb_sig + (v.x & 0xFF) * GA_ROWS;
+          const float *e2 = A.emb_pred + (v.y & 0xFF) * GA_ROWS;
+          const float *e3 = A.emb_exc + (v.z & 0xFF) * GA_ROWS;
+#pragma unroll
+          for (int g = 0; g < 3; g++) {
+            e[s][g] = e1[g * NA + i];
+            e[s][3 + g] = e2[g * NA + i];
+            e[s][6 + g] = e3[g * NA + i];
+          }
+        }
+        /* compute_sparse_gru elementwise (nnet.c:431-447) */
+        float zrv[2 * S], hv[S], inh[S];
+        for (int s = 0; s < S; s++) {
+          const float inz = ((cz[s] + e[s][0]) + e[s][3]) + e[s][6];
+          const float inr = ((cr[s] + e[s][1]) + e[s][4]) + e[s][7];
+          inh[s] = ((ch[s] + e[s][2]) + e[s][5]) + e[s][8];
+          zrv[s] = (float)(az[s] + cvt_rne(((bz + dz * st[s]) + inz) * kScale)) * kScale1;
+          zrv[S + s] = (float)(ar[s] + cvt_rne(((br + dr * st[s]) + inr) * kScale)) * kScale1;
+          hv[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
+        }
+        sigmoid_x86_n<2 * S>(zrv, rcp);
+        for (int s = 0; s < S; s++) hv[s] = hv[s] * zrv[S + s] + inh[s];
+        tanh_x86_n<S>(hv, rcp);
+        for (int s = 0; s < S; s++) {
+          st[s] = zrv[s] * st[s] + (1.f - zrv[s]) * hv[s];
+          xa[(i >> 2) * S * 4 + s * 4 + (i & 3)] = (unsigned char)quant_s8(st[s]);
         }
       }
+      stamp(0);
+      __syncthreads(); /* Y */
+      stamp(1);
+      {
+        /* GRU_B gate sums of row block rb (nnet.c:345-361) */
+        int acc[S], accr[S];
+        for (int s = 0; s < S; s++) { acc[s] = 0; accr[s] = 0; }
+        gru_a_stream<S, SAT>(xa, wq, cq, A.gb_qoff[rb], A.gb_coff[rb], REG_GB / 4, 0, 0, lane, acc, acc, acc);
+        if (ks < NB / 4) {
+          const uint32_t w = ((const uint32_t *)(lds + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r8];
+          dot_streams<S, SAT>(xb, ks * S * 4, w, accr);
+        }
+        for (int s = 0; s < S; s++) {
+          acc[s] = sum_lanes_xor8_16_32(acc[s]);
+          accr[s] = sum_lanes_xor8_16_32(accr[s]);
+        }
+        if (ks == 0) {
+          for (int s = 0; s < S; s++) {
+            zr[s * 2 * GB_ROWS + row] = (float)(gb_seed[s] + acc[s]) * kScale1;
+            zr[s * 2 * GB_ROWS + GB_ROWS + row] = (float)(gb_seedr + accr[s]) * kScale1;
+          }
+        }
+      }
+      stamp(2);
+      __syncthreads(); /* Z */
+      stamp(3);
+      if (n + 1 < A.N) recurrent(); /* W q(h_A(n)) for sample n+1, beside the sampling of n */
     }
-    stamp(2);
-    __syncthreads(); /* Z */
-    stamp(3);
-    if (ga_wave) {
-      if (n + 1 < A.N) recurrent();
-    } else if (samp) {
+    stamp(4);
+    __syncthreads(); /* final */
+    stamp(5);
+    for (int s = 0; s < S; s++)
+      if (active[s]) A.st[s0 + s].gru_a_state[i] = st[s];
+  } else {
+    /* ======================= sampler role ================================ */
+    const float *ulaw = (const float *)(lds + IMG_ULAW);
+    const float *logit_tab = (const float *)(lds + IMG_LOGIT);
+    const float *fcw = (const float *)(lds + IMG_FCW);
+    const float *fcb = (const float *)(lds + IMG_FCB);
+    const float *fcf = (const float *)(lds + IMG_FCF);
+    /* with S=4 a sampler wave carries two streams, one per 32-lane half */
+    const int sw = wv - SAMPLE_WAVES;
+    const int half = lane >> 5, hl = lane & 31;
+    const int my_s = S == 4 ? 2 * sw + half : sw;
+    const bool samp = my_s < S;                         /* wave-uniform */
+    const bool samp_w = samp && (S == 4 || half == 0);  /* lanes owning the stream's outputs */
+    const int ms = samp ? my_s : 0;
+    const bool my_active = samp && s0 + ms < A.nstreams && A.st[s0 + ms].frame_count > FEATURES_DELAY;
+    const int q = hl >> 1, ch2 = lane & 1;
+    const int qq = q < 15 ? q : 0;
+    const int lvl_in = qq == 0 ? 0 : (qq < 3 ? 1 : (qq < 7 ? 2 : 3)); /* level of node qq+1 within 0..3 */
+    const int hb = 32 * half;                                          /* this half's bits in a ballot */
+
+    float lsr[NLPC], lpr[NLPC];
+    float sbv = 0.f, pred = 0.f, deemph = 0.f;
+    uint32_t rz = 0, rw = 0, rj = 0, rc = 0;
+    int last_exc = 0;
+    {
+      const StreamState *p = &A.st[min(s0 + ms, A.nstreams - 1)];
+#pragma unroll
+      for (int j = 0; j < NLPC; j++) {
+        lsr[j] = p->last_sig[j];
+        lpr[j] = p->lpc[j];
+      }
+      sbv = p->gru_b_state[hl & (NB - 1)];
+      deemph = p->deemph_mem;
+      last_exc = p->last_exc;
+      rz = p->rng[0]; rw = p->rng[1]; rj = p->rng[2]; rc = p->rng[3];
+    }
+    __syncthreads(); /* image in LDS */
+    /* dual_fc nodes 1..15 (tree levels 0..3) of this lane: registers */
+    float f03w[NB];
+#pragma unroll
+    for (int j = 0; j < NB; j++) f03w[j] = fcw[(qq + 1) * 32 + ch2 * 16 + j];
+    const float f03b = fcb[ch2 * 256 + qq + 1], f03f = fcf[ch2 * 256 + qq + 1];
+    auto pre_sample = [&]() {
+      /* pred and the u-law indices of the next sample (lpcnet.c:252-254) */
+      float p2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < NLPC; j++) p2 = p2 - lsr[j] * lpr[j];
+      pred = p2;
+      const int su = lin2ulaw_x86(lsr[0]);
+      const int pu = lin2ulaw_x86(pred);
+      if (samp_w && hl == 0) *(int4 *)(ix + ms * 4) = make_int4(su, pu, last_exc, 0);
+    };
+    if (samp_w && hl < NB) {
+      xb[(hl >> 2) * S * 4 + ms * 4 + (hl & 3)] = (unsigned char)quant_s8(sbv);
+      sbuf[ms * NB + hl] = sbv;
+    }
+    if (samp) pre_sample();
+    __syncthreads(); /* initial q(h_A), q(h_B), ix */
+    stamp_start();
+
+    float thr[8];
+    const bool tracing = A.trace_logits != nullptr;
+    for (int n = 0; n < A.N; n++) {
+      stamp(4);
+      __syncthreads(); /* X */
+      stamp(5);
+      if (samp) {
+        /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
+        const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
+        const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          thr[b] = logit_tab[(r0 >> (8 * b)) & 0xFF];
+          thr[b + 4] = logit_tab[(r1 >> (8 * b)) & 0xFF];
+        }
+      }
+      stamp(0);
+      __syncthreads(); /* Y */
+      stamp(1);
+      stamp(2);
+      __syncthreads(); /* Z */
+      stamp(3);
+      if (!samp) continue;
       const int s = ms;
       const float *zs = zr + s * 2 * GB_ROWS;
       {
         /* GRU_B elementwise (nnet.c:362-371); lanes >= 16 of a half duplicate */
         const int u = hl & (NB - 1);
-        const float z = sigmoid_x86(zs[u] + zs[GB_ROWS + u], rcp);
-        const float r = sigmoid_x86(zs[NB + u] + zs[GB_ROWS + NB + u], rcp);
-        float h = zs[2 * NB + u] + zs[GB_ROWS + 2 * NB + u] * r;
-        h = tanh_x86(h, rcp);
-        sbv = z * sbv + (1.f - z) * h;
-        if (samp_w && hl < NB) sbuf[s * NB + hl] = sbv;
+        float zrb[2] = {zs[u] + zs[GB_ROWS + u], zs[NB + u] + zs[GB_ROWS + NB + u]};
+        sigmoid_x86_n<2>(zrb, rcp);
+        float h[1] = {zs[2 * NB + u] + zs[GB_ROWS + 2 * NB + u] * zrb[1]};
+        tanh_x86_n<1>(h, rcp);
+        sbv = zrb[0] * sbv + (1.f - zrb[0]) * h[0];
       }
-      __builtin_amdgcn_wave_barrier();
+      stamp(8);
+      /* GRU_B state to every lane of its half: unit j is lane j (half 0) or
+       * 32+j (half 1) -- scalar reads, no LDS round trip */
       float xv[NB];
-      {
-        const float4 *sb4 = (const float4 *)(sbuf + s * NB);
 #pragma unroll
-        for (int j = 0; j < NB / 4; j++) {
-          const float4 v = sb4[j];
-          xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
-        }
+      for (int j = 0; j < NB; j++) {
+        const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sbv), j));
+        const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sbv), 32 + j));
+        xv[j] = half ? b : a;
       }
+      stamp(9);
       auto node_logit_w = [&](float bias, float factor, const float *w) -> float {
         float sum = bias;
 #pragma unroll
         for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
-        const float v = factor * tanh_x86(sum, rcp);
-        const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
-        return ch2 ? o + v : v + o;
+        float v[1] = {sum};
+        tanh_x86_n<1>(v, rcp);
+        const float vv = factor * v[0];
+        /* sum1 + sum2 (nnet.c:205); adjacent-lane swap through DPP quad_perm [1,0,3,2] */
+        const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(vv), 0xB1, 0xF, 0xF, false));
+        return ch2 ? o + vv : vv + o;
       };
       float lg[8];
       int val = 0;
@@ -1554,6 +1656,7 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
           val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
         }
       }
+      stamp(10);
       {
         const int lvl = 4 + lvl_in;
         const int off = qq + 1 - (1 << (lvl - 4));
@@ -1568,9 +1671,11 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
           val = (val << 1) | (int)((m >> (2 * qi)) & 1ull);
         }
       }
+      stamp(11);
       int exc = val;
       float pcm;
       if (n < A.preload) {
+        /* teacher forcing (lpcnet.c:256-259) */
         const float o_in = (float)pcmbuf[s * FRAME + n];
         const float pd = kPreemph * deemph;
         exc = lin2ulaw_x86((o_in - pd) - pred);
@@ -1586,7 +1691,7 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
       deemph = o;
       if (o < -32767) o = -32767;
       if (o > 32767) o = 32767;
-      if (samp_w && hl == 0 && n >= A.preload) pcmbuf[s * FRAME + n] = (short)(int)floor(.5 + (double)o);
+      if (samp_w && hl == 0 && n >= A.preload) pcmbuf[s * FRAME + n] = (short)round_half_up(o);
       if (tracing && samp_w && hl < 8 && my_active) {
         float v = lg[0];
 #pragma unroll
@@ -1595,31 +1700,29 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
       }
       if (A.trace_exc && samp_w && hl == 0 && my_active) A.trace_exc[(size_t)(s0 + s) * A.N + n] = exc;
       if (samp_w && hl < NB) xb[(hl >> 2) * S * 4 + s * 4 + (hl & 3)] = (unsigned char)quant_s8(sbv);
+      stamp(12);
       if (n + 1 < A.N) pre_sample();
+      stamp(13);
+    }
+    stamp(4);
+    __syncthreads(); /* final */
+    stamp(5);
+    if (samp_w && my_active) {
+      StreamState *p = &A.st[s0 + ms];
+      if (hl < NB) p->gru_b_state[hl] = sbv;
+      if (hl == 0) {
+#pragma unroll
+        for (int j = 0; j < NLPC; j++) p->last_sig[j] = lsr[j];
+        p->deemph_mem = deemph;
+        p->last_exc = last_exc;
+        p->rng[0] = rz; p->rng[1] = rw; p->rng[2] = rj; p->rng[3] = rc;
+      }
     }
   }
-  stamp(4);
-  __syncthreads();
-  stamp(5);
   if (stamping && lane == 0) {
     stp[6] = __builtin_amdgcn_s_memtime() - t_loop0;
     stp[7] = (unsigned long long)A.N;
     for (int k = 0; k < 16; k++) A.stamps[((size_t)blockIdx.x * STAMP_WAVES + wv) * 16 + k] = stp[k];
-  }
-
-  if (ga_wave)
-    for (int s = 0; s < S; s++)
-      if (active[s]) A.st[s0 + s].gru_a_state[i] = st[s];
-  if (samp_w && my_active) {
-    StreamState *p = &A.st[s0 + ms];
-    if (hl < NB) p->gru_b_state[hl] = sbv;
-    if (hl == 0) {
-#pragma unroll
-      for (int j = 0; j < NLPC; j++) p->last_sig[j] = lsr[j];
-      p->deemph_mem = deemph;
-      p->last_exc = last_exc;
-      p->rng[0] = rz; p->rng[1] = rw; p->rng[2] = rj; p->rng[3] = rc;
-    }
   }
   for (int e = tid; e < S * A.N; e += PIPE_THREADS) {
     const int s = e / A.N, n = e % A.N;

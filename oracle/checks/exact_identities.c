@@ -1,0 +1,47 @@
+/* Exhaustive proofs of the float identities the HIP kernels use in place of
+ * slower operations of the reference (TEST INFRASTRUCTURE ONLY):
+ *  (1) lin2ulaw's float division by log(256) (common.h:47-58):
+ *      RN(v / c) == fma(fma(-q0, c, v), rc, q0), q0 = RN(v*rc), rc = RN(1/c),
+ *      for every float v in [2^-10, 2^15) -- lin2ulaw's numerator
+ *      128*(0.69315*l2) lies in [0.0395, 11500] (y >= 1 gives l2 >= 4.4e-4);
+ *  (2) (int)floor(.5 + (double)u) == k + (u - k >= .5f), k = (int)u, for
+ *      every float u in [0, 255] (the u-law index, common.h:57);
+ *  (3) (int)floor(.5 + (double)o) == (int)floorf(o) + (o - floorf(o) >= .5f)
+ *      for every float o in [-32767, 32767] (the output sample, lpcnet.c:268).
+ * Build: gcc -O2 -ffp-contract=off exact_identities.c -lm; exit status 0 = all hold. */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+static float f_of(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static uint32_t u_of(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+
+int main(void)
+{
+  unsigned long long bad = 0;
+  const float c = 5.5451774445f, rc = 1.0f / c;
+  for (uint32_t u = u_of(0x1p-10f); u < u_of(32768.f); u++) {
+    const float v = f_of(u), ref = v / c, q0 = v * rc, q1 = fmaf(fmaf(-q0, c, v), rc, q0);
+    if (u_of(ref) != u_of(q1)) bad++;
+  }
+  printf("division: %llu mismatches\n", bad);
+  unsigned long long bad2 = 0;
+  for (uint32_t u = 0; u <= u_of(255.f); u++) {
+    const float x = f_of(u);
+    const int ref = (int)floor(.5 + (double)x);
+    const int k = (int)x;
+    if (ref != k + (x - (float)k >= .5f)) bad2++;
+  }
+  printf("round u: %llu mismatches\n", bad2);
+  unsigned long long bad3 = 0;
+  for (int sgn = 0; sgn < 2; sgn++)
+    for (uint32_t u = 0; u <= u_of(32767.f); u++) {
+      const float x = sgn ? -f_of(u) : f_of(u);
+      const int ref = (int)floor(.5 + (double)x);
+      const float k = floorf(x);
+      if (ref != (int)k + (x - k >= .5f)) bad3++;
+    }
+  printf("round o: %llu mismatches\n", bad3);
+  return (bad || bad2 || bad3) ? 1 : 0;
+}

@@ -78,3 +78,15 @@ def test_batch_create_fails_cleanly_without_device():
     import pytest
     with pytest.raises(L.LPCNetError):
         L.LPCNetBatch(4)
+
+
+def test_kernel_float_identities_exhaustive(tmp_path):
+    """The HIP kernels replace lin2ulaw's float division and the
+    floor(.5 + (double)x) roundings with exact float forms; this proves them
+    over every float input they can see (oracle/checks/exact_identities.c)."""
+    import subprocess
+    exe = tmp_path / "exact_identities"
+    src = os.path.join(ROOT, "oracle", "checks", "exact_identities.c")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), src, "-lm"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout
