@@ -29,24 +29,28 @@ namespace lpcnet_mi355x {
 /* ------------------------------------------------------------------------ */
 /* numerics helpers                                                          */
 
+/* rcpps of a Pade denominator from its table entry t (see rcp_x86) */
+__device__ __forceinline__ float rcp_x86_fix(float x, uint32_t t)
+{
+  const int e = (int)((__float_as_uint(x) >> 23) & 0xff);
+  const float q = __builtin_ldexpf(__uint_as_float(t), 127 - e);
+  return q < 0x1p-126f ? 0.f : q;
+}
+
 __device__ __forceinline__ float rcp_x86(float x, const uint32_t *tab)
 {
-  /* _mm256_rcp_ps: table of the top 11 mantissa bits, exponent invariant,
-   * denormal results flushed to zero (probe: SURVEY.md 7 hard part 1).
-   * The table load is issued unconditionally and pinned (empty asm) so the
-   * special cases below stay selects instead of exec-masked branches. */
+  /* _mm256_rcp_ps of a Pade denominator (its only use, tanh8_approx and
+   * sigmoid8_approx): den = fma(fma(D2,X2,D1),X2,D0) with positive D's and
+   * X2 = X*X lies in [952.72, +inf] or is NaN.  rcpps there is the
+   * 2048-entry table of the top 11 mantissa bits, rebiased; results below
+   * 2^-126 (and rcp(+inf)) are +0.  ldexp + flush reproduces it for every
+   * such den (oracle/checks/exact_identities.c (4)); a NaN den only occurs
+   * with a NaN numerator, whose product stays NaN.  The table load is pinned
+   * (empty asm) so the select stays branch-free. */
   const uint32_t u = __float_as_uint(x);
   uint32_t t = tab[(u >> 12) & 0x7ff];
   asm volatile("" : "+v"(t));
-  const uint32_t sign = u & 0x80000000u;
-  const int e = (int)((u >> 23) & 0xff);
-  const int te = (int)((t >> 23) & 0xff) + 127 - e;
-  uint32_t r = sign | (t & 0x007fffffu) | ((uint32_t)te << 23);
-  r = te < 1 ? sign : r;
-  const uint32_t spec = (u & 0x7fffffu) ? (u | 0x00400000u) : sign; /* NaN -> qNaN, inf -> 0 */
-  r = e == 255 ? spec : r;
-  r = e == 0 ? (sign | 0x7f800000u) : r;
-  return __uint_as_float(r);
+  return rcp_x86_fix(x, t);
 }
 
 /* _mm256_min_ps / _mm256_max_ps return the second operand when unordered */
@@ -79,20 +83,6 @@ __device__ __forceinline__ float sigmoid_x86(float X, const uint32_t *tab)
 
 /* N independent rcp_x86: all N table reads are issued before any is pinned,
  * so their LDS latencies overlap (rcp_x86's pin alone serialises a chain). */
-__device__ __forceinline__ float rcp_x86_fix(float x, uint32_t t)
-{
-  const uint32_t u = __float_as_uint(x);
-  const uint32_t sign = u & 0x80000000u;
-  const int e = (int)((u >> 23) & 0xff);
-  const int te = (int)((t >> 23) & 0xff) + 127 - e;
-  uint32_t r = sign | (t & 0x007fffffu) | ((uint32_t)te << 23);
-  r = te < 1 ? sign : r;
-  const uint32_t spec = (u & 0x7fffffu) ? (u | 0x00400000u) : sign;
-  r = e == 255 ? spec : r;
-  r = e == 0 ? (sign | 0x7f800000u) : r;
-  return __uint_as_float(r);
-}
-
 template <int N>
 __device__ __forceinline__ void rcp_x86_n(float (&x)[N], const uint32_t *tab)
 {
@@ -712,7 +702,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
       /* embedding gathers issued first; consumed after the recurrent matvec */
       float e1z[S], e1r[S], e1h[S], e2z[S], e2r[S], e2h[S], e3z[S], e3r[S], e3h[S];
       for (int s = 0; s < S; s++) {
-        const int sig = ix[s * 4 + 0] & 0xFF, prd = ix[s * 4 + 1] & 0xFF, exc = ix[s * 4 + 2] & 0xFF;
+        const int sig = __builtin_amdgcn_readfirstlane(ix[s * 4 + 0]) & 0xFF;
+        const int prd = __builtin_amdgcn_readfirstlane(ix[s * 4 + 1]) & 0xFF;
+        const int exc = __builtin_amdgcn_readfirstlane(ix[s * 4 + 2]) & 0xFF;
         const float *e1 = A.emb_sig + sig * GA_ROWS, *e2 = A.emb_pred + prd * GA_ROWS, *e3 = A.emb_exc + exc * GA_ROWS;
         e1z[s] = e1[i]; e1r[s] = e1[NA + i]; e1h[s] = e1[2 * NA + i];
         e2z[s] = e2[i]; e2r[s] = e2[NA + i]; e2h[s] = e2[2 * NA + i];
@@ -1465,10 +1457,11 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
         /* GRU_A input (nnet.c:484-491): all 9*S gathers in flight at once */
         float e[S][9];
         for (int s = 0; s < S; s++) {
+          /* the indices are the same in every lane: scalar row addresses */
           const int4 v = *(const int4 *)(ix + s * 4);
-          const float *e1 = A.emb_sig + (v.x & 0xFF) * GA_ROWS;
-          const float *e2 = A.emb_pred + (v.y & 0xFF) * GA_ROWS;
-          const float *e3 = A.emb_exc + (v.z & 0xFF) * GA_ROWS;
+          const float *e1 = A.emb_sig + (__builtin_amdgcn_readfirstlane(v.x) & 0xFF) * GA_ROWS;
+          const float *e2 = A.emb_pred + (__builtin_amdgcn_readfirstlane(v.y) & 0xFF) * GA_ROWS;
+          const float *e3 = A.emb_exc + (__builtin_amdgcn_readfirstlane(v.z) & 0xFF) * GA_ROWS;
 #pragma unroll
           for (int g = 0; g < 3; g++) {
             e[s][g] = e1[g * NA + i];
@@ -1620,18 +1613,20 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
         float h[1] = {zs[2 * NB + u] + zs[GB_ROWS + 2 * NB + u] * zrb[1]};
         tanh_x86_n<1>(h, rcp);
         sbv = zrb[0] * sbv + (1.f - zrb[0]) * h[0];
+        if (samp_w && hl < NB) sbuf[s * NB + hl] = sbv;
       }
-      stamp(8);
-      /* GRU_B state to every lane of its half: unit j is lane j (half 0) or
-       * 32+j (half 1) -- scalar reads, no LDS round trip */
+      /* same-wave LDS exchange (measured faster than 32 v_readlane: gfx9
+       * VALU ops read one SGPR each and SGPR hazards add wait states) */
+      __builtin_amdgcn_wave_barrier();
       float xv[NB];
+      {
+        const float4 *sb4 = (const float4 *)(sbuf + s * NB);
 #pragma unroll
-      for (int j = 0; j < NB; j++) {
-        const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sbv), j));
-        const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sbv), 32 + j));
-        xv[j] = half ? b : a;
+        for (int j = 0; j < NB / 4; j++) {
+          const float4 v = sb4[j];
+          xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
+        }
       }
-      stamp(9);
       auto node_logit_w = [&](float bias, float factor, const float *w) -> float {
         float sum = bias;
 #pragma unroll
@@ -1656,7 +1651,6 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
           val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
         }
       }
-      stamp(10);
       {
         const int lvl = 4 + lvl_in;
         const int off = qq + 1 - (1 << (lvl - 4));
@@ -1671,7 +1665,6 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
           val = (val << 1) | (int)((m >> (2 * qi)) & 1ull);
         }
       }
-      stamp(11);
       int exc = val;
       float pcm;
       if (n < A.preload) {
@@ -1700,9 +1693,7 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
       }
       if (A.trace_exc && samp_w && hl == 0 && my_active) A.trace_exc[(size_t)(s0 + s) * A.N + n] = exc;
       if (samp_w && hl < NB) xb[(hl >> 2) * S * 4 + s * 4 + (hl & 3)] = (unsigned char)quant_s8(sbv);
-      stamp(12);
       if (n + 1 < A.N) pre_sample();
-      stamp(13);
     }
     stamp(4);
     __syncthreads(); /* final */

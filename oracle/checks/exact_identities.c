@@ -8,6 +8,13 @@
  *      every float u in [0, 255] (the u-law index, common.h:57);
  *  (3) (int)floor(.5 + (double)o) == (int)floorf(o) + (o - floorf(o) >= .5f)
  *      for every float o in [-32767, 32767] (the output sample, lpcnet.c:268).
+ *  (4) the rcpps emulation of the Pade denominators of tanh8_approx /
+ *      sigmoid8_approx (vec_avx.h:393-440), den = fma(fma(D2,X2,D1),X2,D0) with
+ *      positive D's and X2 = X*X, i.e. den in [952.72, +inf] or NaN:
+ *      ldexp(table[m], 127 - e) flushed to +0 below 2^-126 equals the
+ *      general emulation (sign | table mantissa | rebiased exponent, 0 for
+ *      denormal results, 0 for +inf) for every such finite or infinite den
+ *      (argv[1] = the 2048-entry table, tests/golden/rcp_x86.bin).
  * Build: gcc -O2 -ffp-contract=off exact_identities.c -lm; exit status 0 = all hold. */
 #include <math.h>
 #include <stdint.h>
@@ -17,7 +24,7 @@
 static float f_of(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 static uint32_t u_of(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 
-int main(void)
+int main(int argc, char **argv)
 {
   unsigned long long bad = 0;
   const float c = 5.5451774445f, rc = 1.0f / c;
@@ -43,5 +50,28 @@ int main(void)
       if (ref != (int)k + (x - k >= .5f)) bad3++;
     }
   printf("round o: %llu mismatches\n", bad3);
-  return (bad || bad2 || bad3) ? 1 : 0;
+  unsigned long long bad4 = 0;
+  if (argc > 1) {
+    static uint32_t tab[2048];
+    FILE *f = fopen(argv[1], "rb");
+    if (!f || fread(tab, 4, 2048, f) != 2048) { printf("cannot read table\n"); return 2; }
+    fclose(f);
+    for (uint32_t u = u_of(952.72f); u <= 0x7f800000u; u++) {
+      const uint32_t t = tab[(u >> 12) & 0x7ff];
+      /* general form (kernels.hip rcp_x86 before specialisation) */
+      const uint32_t sign = u & 0x80000000u;
+      const int e = (int)((u >> 23) & 0xff);
+      const int te = (int)((t >> 23) & 0xff) + 127 - e;
+      uint32_t r = sign | (t & 0x007fffffu) | ((uint32_t)te << 23);
+      r = te < 1 ? sign : r;
+      const uint32_t spec = (u & 0x7fffffu) ? (u | 0x00400000u) : sign;
+      r = e == 255 ? spec : r;
+      /* specialised form */
+      float q = ldexpf(f_of(t), 127 - e);
+      q = q < 0x1p-126f ? 0.f : q;
+      if (r != u_of(q)) bad4++;
+    }
+    printf("rcp pade: %llu mismatches\n", bad4);
+  }
+  return (bad || bad2 || bad3 || bad4) ? 1 : 0;
 }

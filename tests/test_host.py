@@ -88,5 +88,6 @@ def test_kernel_float_identities_exhaustive(tmp_path):
     exe = tmp_path / "exact_identities"
     src = os.path.join(ROOT, "oracle", "checks", "exact_identities.c")
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), src, "-lm"], check=True)
-    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([str(exe), os.path.join(ROOT, "tests", "golden", "rcp_x86.bin")], capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stdout
