@@ -33,7 +33,8 @@ typedef struct {
   double bytes_per_stream_sample; /* per-stream bytes per sample (gathers, trace-free) */
   double ops_per_sample;          /* 2*MAC per stream per sample */
   int streams_per_workgroup;      /* streams per sample-kernel workgroup */
-  int quad_path;                  /* 0 per-slot LDS, 1 quad LDS (lockstep), 2 wave-per-stream, 3 pipelined */
+  int quad_path;                  /* 0 per-slot LDS, 1 quad LDS (lockstep), 2 wave-per-stream, 3 pipelined,
+                                     4 pipelined on the matrix cores */
   int lds_bytes;                  /* dynamic LDS of the sample kernel */
 } LPCNetModelInfo;
 
@@ -47,7 +48,10 @@ LPCNET_EXPORT int lpcnet_batch_model_info(const LPCNetBatch *b, LPCNetModelInfo 
 /* Sample-kernel selection: 0 automatic (default; env LPCNET_KERNEL), 1 the
  * lockstep kernel (6 waves per stream group), 2 the wave-per-stream kernel,
  * 3 the pipelined kernel (2 and 3: int8 quad-layout models only; otherwise
- * the lockstep kernel runs).  Results are identical; only speed differs. */
+ * the lockstep kernel runs), 4 the pipelined kernel with both int8 products
+ * on the matrix cores (non-saturating int8 models whose blocks fit its
+ * register tables; otherwise mode 3 rules apply).  Results are identical;
+ * only speed differs. */
 LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode);
 /* lpcnet_reset() on every stream / on one stream. */
 LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b);

@@ -286,9 +286,11 @@ struct LPCNetBatch {
   int variant = 0;
   bool sat = false;
   bool reg = false;
-  int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 2 wave_kernel, 3 pipe_kernel */
+  int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 2 wave_kernel, 3 pipe_kernel, 4 matrix-core pipe_kernel */
   int wave_nw = 0;       /* >0: wave_kernel with this many streams per workgroup */
-  bool pipe = false;     /* pipe_kernel (mode 3) */
+  bool pipe = false;     /* pipe_kernel (modes 3, 4) */
+  bool mf_ok = false;    /* model fits the matrix-core register tables */
+  bool mf = false;       /* pipe_kernel runs the matrix-core path */
   int image_bytes = 0;
   LPCNetModelInfo info{};
   std::vector<void *> model_bufs;
@@ -373,9 +375,19 @@ void choose_kernel(LPCNetBatch *b)
 {
   b->wave_nw = 0;
   b->pipe = false;
+  b->mf = false;
   const bool quad_int8 = b->variant == LPCNET_VARIANT_INT8 && b->reg;
   int mode = b->kernel_mode;
-  if (mode == 0) mode = quad_int8 ? 3 : 1;
+  if (mode == 0) mode = b->mf_ok ? 4 : (quad_int8 ? 3 : 1);
+  if (mode == 4 && b->mf_ok && pipe_lds_bytes(b->S, b->image_bytes, 1) <= 160 * 1024) {
+    b->pipe = true;
+    b->mf = true;
+    b->info.streams_per_workgroup = b->S;
+    b->info.lds_bytes = pipe_lds_bytes(b->S, b->image_bytes, 1);
+    b->info.quad_path = 4;
+    return;
+  }
+  if (mode == 4) mode = quad_int8 ? 3 : 1;
   if (mode == 2 && quad_int8) {
     int nw = std::min(4, std::max(1, (b->B + 255) / 256));
     while (nw > 1 && wave_lds_bytes(nw, b->image_bytes) > 160 * 1024) nw /= 2;
@@ -387,10 +399,10 @@ void choose_kernel(LPCNetBatch *b)
       return;
     }
   }
-  if (mode == 3 && quad_int8 && pipe_lds_bytes(b->S, b->image_bytes) <= 160 * 1024) {
+  if (mode == 3 && quad_int8 && pipe_lds_bytes(b->S, b->image_bytes, 0) <= 160 * 1024) {
     b->pipe = true;
     b->info.streams_per_workgroup = b->S;
-    b->info.lds_bytes = pipe_lds_bytes(b->S, b->image_bytes);
+    b->info.lds_bytes = pipe_lds_bytes(b->S, b->image_bytes, 0);
     b->info.quad_path = 3;
     return;
   }
@@ -630,6 +642,53 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
     }
   align16();
 
+  /* ---- matrix-core register tables (non-saturating int8 models) ---- */
+  std::vector<uint32_t> mft;
+  bool mf_ok = int8 && !sat && !getenv("LPCNET_NO_MFMA");
+  for (int w = 0; w < SAMPLE_WAVES && mf_ok; w++)
+    for (int j = 0; j < 8; j++) {
+      if ((int)ga_blocks[w * 8 + j].size() > MF_ZMAX || (int)ga_blocks[NA / 8 + w * 8 + j].size() > MF_ZMAX ||
+          (int)ga_blocks[2 * (NA / 8) + w * 8 + j].size() > MF_HMAX)
+        mf_ok = false;
+    }
+  for (int rb = 0; rb < GB_ROWS / 8 && mf_ok; rb++)
+    if ((int)gb_blocks[rb].size() > 8 * REG_GB) mf_ok = false;
+  if (mf_ok) {
+    const int8_t *wa = (const int8_t *)gaw->data, *wb = (const int8_t *)gbw, *wr = (const int8_t *)gbrec;
+    mft.assign((size_t)SAMPLE_WAVES * MF_LANE_U32 * 64, 0);
+    for (int w = 0; w < SAMPLE_WAVES; w++) {
+      auto word = [&](int k, int l) -> uint32_t & { return mft[((size_t)w * MF_LANE_U32 + k) * 64 + l]; };
+      int kz = 0, kh = 0;
+      for (int j = 0; j < 8; j++) {
+        kz = std::max(kz, (int)std::max(ga_blocks[w * 8 + j].size(), ga_blocks[NA / 8 + w * 8 + j].size()));
+        kh = std::max(kh, (int)ga_blocks[2 * (NA / 8) + w * 8 + j].size());
+      }
+      sa.mf_nzr[w] = (kz + 3) / 4;
+      sa.mf_nh[w] = (kh + 3) / 4;
+      for (int l = 0; l < 64; l++) {
+        const int j = l >> 3, r = l & 7, ks = l >> 3;
+        for (int g = 0; g < 3; g++) {
+          const int rb = g * (NA / 8) + w * 8 + j, base = g == 0 ? 0 : (g == 1 ? MF_ZMAX : 2 * MF_ZMAX);
+          for (int t = 0; t < (int)ga_blocks[rb].size(); t++) {
+            memcpy(&word(base + t, l), wa + 32 * (ga_first[rb] + t) + 4 * r, 4);
+            word(MF_GA + (base + t) / 4, l) |= (uint32_t)(ga_blocks[rb][t] / 4) << (8 * ((base + t) & 3));
+          }
+        }
+        /* GRU_B row block w: input blocks ks + 8t, recurrent column block ks */
+        for (int t = 0; t < REG_GB; t++) {
+          const int k = ks + 8 * t;
+          if (k >= (int)gb_blocks[w].size()) continue;
+          memcpy(&word(MF_W_GB + t, l), wb + 32 * (gb_first[w] + k) + 4 * r, 4);
+          word(MF_C_GB + t / 4, l) |= (uint32_t)(gb_blocks[w][k] / 4) << (8 * (t & 3));
+        }
+        if (ks < NB / 4) {
+          memcpy(&word(MF_W_GBREC, l), wr + 32 * (w * (NB / 4) + ks) + 4 * r, 4);
+          word(MF_C_GB + REG_GB / 4, l) |= (uint32_t)ks;
+        }
+      }
+    }
+  }
+
   /* choose streams per workgroup and check the LDS budget */
   int S = b->B >= 1024 ? 4 : (b->B >= 512 ? 2 : 1);
   int lds = sample_lds_bytes(S, variant, (int)img.size());
@@ -668,6 +727,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   UP(sa.gb_par, gb_par.data(), gb_par.size() * 4);
   UP(sa.gb_wsum, gb_wsum.data(), gb_wsum.size() * 4);
   UP(sa.image, img.data(), img.size());
+  if (mf_ok) UP(sa.mf, mft.data(), mft.size() * 4);
   if (!int8) {
     UP(sa.ga_wf, ga_wf.data(), ga_wf.size() * sizeof(float4));
     UP(sa.gb_recf, gbrec, 3 * NB * NB * 4);
@@ -677,6 +737,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   b->variant = variant;
   b->sat = sat;
   b->reg = reg;
+  b->mf_ok = mf_ok;
   b->image_bytes = (int)img.size();
   b->S = S;
   b->lds_bytes = lds;
@@ -750,7 +811,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
   const int lrc = N <= 0 ? 0
-                : b->pipe  ? launch_pipe(sa, b->S, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
+                : b->pipe  ? launch_pipe(sa, b->S, b->sat ? 1 : 0, b->mf ? 1 : 0, b->info.lds_bytes, b->stream)
                 : b->wave_nw ? launch_wave(sa, b->wave_nw, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
                              : launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream);
   if (lrc) {
@@ -864,7 +925,7 @@ LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *d
 
 LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode)
 {
-  if (!b || mode < 0 || mode > 3) return -1;
+  if (!b || mode < 0 || mode > 4) return -1;
   b->kernel_mode = mode;
   if (b->have_model) choose_kernel(b);
   return 0;

@@ -1341,38 +1341,143 @@ int launch_frame(const FrameArgs &a, void *stream)
  *      GRU_A waves: W·q(h_A(n)) for sample n+1
  *      sampler waves: GRU_B update, tree walk, output, pred(n+1) -> ix(n+1)
  * Same arithmetic as sample_kernel's quad path, term for term. */
-template <int S>
+template <int S, bool MF>
 struct PipeLds {
   static constexpr int x = (NA / 4) * S * 4;   /* quantized GRU_A state (single buffer) */
   static constexpr int xb = (NB / 4) * S * 4;  /* quantized GRU_B state */
   static constexpr int sb = S * NB * 4;        /* float GRU_B state */
   static constexpr int zr = S * 2 * GB_ROWS * 4;
   static constexpr int ix = S * 4 * 4;
-  static constexpr int pcm = S * FRAME * 2;
-  static constexpr int total = x + xb + sb + zr + ix + ((pcm + 15) / 16) * 16;
+  static constexpr int pcm = ((S * FRAME * 2 + 15) / 16) * 16;
+  /* matrix-core path: frame constants kept out of registers -- GRU_A
+   * conditioning [3][NA][S] and GRU_B accumulator seeds [GB_ROWS][S] */
+  static constexpr int cnd = MF ? GA_ROWS * S * 4 : 0;
+  static constexpr int gbs = MF ? GB_ROWS * S * 4 : 0;
+  static constexpr int total = x + xb + sb + zr + ix + pcm + cnd + gbs;
 };
 
-int pipe_lds_bytes(int S, int image_bytes)
+/* LDS: quad path = [image | regions]; matrix-core path = [regions | fixed
+ * image sections] (x first, so every x address fits the 16-bit offsets the
+ * lanes keep in registers; the GRU weights live in registers). */
+int pipe_lds_bytes(int S, int image_bytes, int mf)
 {
-  return image_bytes + (S == 4 ? PipeLds<4>::total : (S == 2 ? PipeLds<2>::total : PipeLds<1>::total));
+  if (mf) return IMG_VAR + (S == 4 ? PipeLds<4, true>::total : (S == 2 ? PipeLds<2, true>::total : PipeLds<1, true>::total));
+  return image_bytes + (S == 4 ? PipeLds<4, false>::total : (S == 2 ? PipeLds<2, false>::total : PipeLds<1, false>::total));
 }
 
-template <int S, bool SAT>
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+/* Keep packed offsets packed: without this the compiler hoists every
+ * unpacked 16-bit offset out of the sample loop (one VGPR per slot). */
+template <int N>
+__device__ __forceinline__ void mf_opaque(uint32_t (&o)[N])
+{
+#pragma unroll
+  for (int k = 0; k < N; k++) asm volatile("" : "+v"(o[k]));
+}
+
+/* x word of slot t: the packed 16-bit LDS byte offsets o[t/2] */
+template <int NO>
+__device__ __forceinline__ uint32_t mf_x(const unsigned char *lds, const uint32_t (&o)[NO], int t)
+{
+  return *(const uint32_t *)(lds + ((o[t >> 1] >> (16 * (t & 1))) & 0xFFFF));
+}
+
+/* v_mfma_i32_4x4x4_16b_i8, 16 blocks: block b = lanes 4b..4b+3.
+ * A (src0) lane 4b+m: 4 int8 of row m (= stream m's x quad of the block's
+ * column block); B (src1) lane 4b+n: 4 int8 of column n (= weight row n);
+ * D lane 4b+n, register m: sum over k of A[m][k] B[k][n] (exact int32).
+ * Layout measured on gfx950 (tools/probes/mfma_i8_probe.hip). */
+__device__ __forceinline__ v4i mfma4(uint32_t x, uint32_t w, v4i acc)
+{
+  return __builtin_amdgcn_mfma_i32_4x4x4i8((int)x, (int)w, acc, 0, 0, 0);
+}
+
+/* GRU_A z and r products over ng 4-slot groups (wave-uniform ng): the two
+ * gates interleave (independent accumulators), x words of group g+1 are
+ * read from LDS while the MFMAs of group g run. */
+__device__ __forceinline__ void mf_zr(const unsigned char *lds, const uint32_t (&wz)[MF_ZMAX],
+                                      const uint32_t (&wr)[MF_ZMAX], const uint32_t (&oz)[MF_ZMAX / 2],
+                                      const uint32_t (&orr)[MF_ZMAX / 2], int ng, v4i &az, v4i &ar)
+{
+  uint32_t xz[4], xr[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    xz[k] = mf_x(lds, oz, k);
+    xr[k] = mf_x(lds, orr, k);
+  }
+#pragma unroll
+  for (int g = 0; g < MF_ZMAX / 4; g++) {
+    if (g < ng) {
+      uint32_t nz[4], nr[4];
+      if (g + 1 < MF_ZMAX / 4 && g + 1 < ng) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          nz[k] = mf_x(lds, oz, 4 * (g + 1) + k);
+          nr[k] = mf_x(lds, orr, 4 * (g + 1) + k);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        az = mfma4(xz[k], wz[4 * g + k], az);
+        ar = mfma4(xr[k], wr[4 * g + k], ar);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        xz[k] = nz[k];
+        xr[k] = nr[k];
+      }
+    }
+  }
+}
+
+/* NS-slot product over ng 4-slot groups, alternating two accumulators */
+template <int NS>
+__device__ __forceinline__ void mf_run(const unsigned char *lds, const uint32_t (&w)[NS], const uint32_t (&o)[NS / 2],
+                                       int ng, v4i &a0, v4i &a1)
+{
+  uint32_t x[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) x[k] = mf_x(lds, o, k);
+#pragma unroll
+  for (int g = 0; g < NS / 4; g++) {
+    if (g < ng) {
+      uint32_t n[4];
+      if (g + 1 < NS / 4 && g + 1 < ng) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) n[k] = mf_x(lds, o, 4 * (g + 1) + k);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (k & 1) a1 = mfma4(x[k], w[4 * g + k], a1);
+        else a0 = mfma4(x[k], w[4 * g + k], a0);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) x[k] = n[k];
+    }
+  }
+}
+
+template <int S, bool SAT, bool MF>
 __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
 {
   extern __shared__ uint4 lds4[];
   unsigned char *lds = (unsigned char *)lds4;
-  using L = PipeLds<S>;
-  unsigned char *xa = lds + A.image_bytes;
+  using L = PipeLds<S, MF>;
+  static_assert(!(MF && SAT), "the matrix-core path has no int16 saturation");
+  unsigned char *img = MF ? lds + L::total : lds;
+  unsigned char *xa = MF ? lds : lds + A.image_bytes;
   unsigned char *xb = xa + L::x;
   float *sbuf = (float *)(xb + L::xb);
   float *zr = sbuf + S * NB;
   int *ix = (int *)(zr + S * 2 * GB_ROWS);
   short *pcmbuf = (short *)(ix + S * 4);
+  float *cnd = (float *)((unsigned char *)pcmbuf + L::pcm);
+  int *gbs = (int *)((unsigned char *)cnd + L::cnd);
 
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = blockIdx.x * S;
-  const uint32_t *rcp = (const uint32_t *)(lds + IMG_RCP);
+  const uint32_t *rcp = (const uint32_t *)(img + IMG_RCP);
 
   bool active[S];
   bool any = false;
@@ -1388,7 +1493,11 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
     }
     return;
   }
-  for (int o = tid; o < A.image_bytes / 16; o += PIPE_THREADS) lds4[o] = A.image[o];
+  {
+    uint4 *img4 = (uint4 *)img;
+    const int n16 = (MF ? IMG_VAR : A.image_bytes) / 16;
+    for (int o = tid; o < n16; o += PIPE_THREADS) img4[o] = A.image[o];
+  }
   for (int e = tid; e < S * A.preload; e += PIPE_THREADS) {
     const int s = e / A.preload, n = e % A.preload;
     pcmbuf[s * FRAME + n] = A.pcm[(size_t)min(s0 + s, A.nstreams - 1) * A.N + n];
@@ -1414,8 +1523,8 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
    * registers of one role are not live in the other's code. */
   if (wv < SAMPLE_WAVES) {
     /* ======================= GRU_A role ================================== */
-    const uint4 *wq = (const uint4 *)lds;
-    const uint32_t *cq = (const uint32_t *)lds;
+    const uint4 *wq = (const uint4 *)img;
+    const uint32_t *cq = (const uint32_t *)img;
     const int i = tid;
     const int K4z = A.ga_K4[wv][0], K4r = A.ga_K4[wv][1], K4h = A.ga_K4[wv][2];
     const int qoff = A.ga_qoff[wv][0], coff = A.ga_coff[wv][0];
@@ -1432,8 +1541,51 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
       cr[s] = p->gru_a_cond[NA + i];
       ch[s] = p->gru_a_cond[2 * NA + i];
       gb_seed[s] = cvt_rne((A.gb_par[row] + p->gru_b_cond[row]) * kScale) + (SAT ? 0 : A.gb_wsum[row]);
+      if constexpr (MF) {
+        cnd[i * S + s] = cz[s];
+        cnd[(NA + i) * S + s] = cr[s];
+        cnd[(2 * NA + i) * S + s] = ch[s];
+        if (ks == 0) gbs[row * S + s] = gb_seed[s];
+      }
     }
     const int gb_seedr = cvt_rne(A.gb_par[GB_ROWS + row] * kScale) + (SAT ? 0 : A.gb_wsum[GB_ROWS + row]);
+    /* matrix-core path: this lane's weight rows and x offsets, for all N samples */
+    uint32_t wz[MF_ZMAX], wr[MF_ZMAX], wh[MF_HMAX], oz[MF_ZMAX / 2], orr[MF_ZMAX / 2], oh[MF_HMAX / 2];
+    uint32_t wgb[REG_GB], ogb[REG_GB / 2], wrec = 0, orec = 0;
+    int nzr = 0, nh = 0;
+    if constexpr (MF) {
+      const uint32_t *mt = A.mf + (size_t)wv * MF_LANE_U32 * 64 + lane;
+#pragma unroll
+      for (int t = 0; t < MF_ZMAX; t++) {
+        wz[t] = mt[t * 64];
+        wr[t] = mt[(MF_ZMAX + t) * 64];
+      }
+#pragma unroll
+      for (int t = 0; t < MF_HMAX; t++) wh[t] = mt[(2 * MF_ZMAX + t) * 64];
+#pragma unroll
+      for (int t = 0; t < REG_GB; t++) wgb[t] = mt[(MF_W_GB + t) * 64];
+      wrec = mt[MF_W_GBREC * 64];
+      uint32_t cw[MF_GA / 4], cg[4];
+#pragma unroll
+      for (int k = 0; k < MF_GA / 4; k++) cw[k] = mt[(MF_GA + k) * 64];
+#pragma unroll
+      for (int k = 0; k < 4; k++) cg[k] = mt[(MF_C_GB + k) * 64];
+      /* A operand of lane 4b+m = stream m (lanes m >= S duplicate stream S-1) */
+      const uint32_t mo = (uint32_t)min(lane & 3, S - 1) * 4;
+      auto off = [&](const uint32_t *c, int t) -> uint32_t { return ((c[t >> 2] >> (8 * (t & 3))) & 0xFF) * (S * 4) + mo; };
+#pragma unroll
+      for (int t = 0; t < MF_ZMAX / 2; t++) {
+        oz[t] = off(cw, 2 * t) | (off(cw, 2 * t + 1) << 16);
+        orr[t] = off(cw, MF_ZMAX + 2 * t) | (off(cw, MF_ZMAX + 2 * t + 1) << 16);
+      }
+#pragma unroll
+      for (int t = 0; t < MF_HMAX / 2; t++) oh[t] = off(cw, 2 * MF_ZMAX + 2 * t) | (off(cw, 2 * MF_ZMAX + 2 * t + 1) << 16);
+#pragma unroll
+      for (int t = 0; t < REG_GB / 2; t++) ogb[t] = off(cg, 2 * t) | (off(cg, 2 * t + 1) << 16);
+      orec = (uint32_t)L::x + off(cg, REG_GB);
+      nzr = A.mf_nzr[wv];
+      nh = A.mf_nh[wv];
+    }
     __syncthreads(); /* image in LDS */
     for (int s = 0; s < S; s++) xa[(i >> 2) * S * 4 + s * 4 + (i & 3)] = (unsigned char)quant_s8(st[s]);
     __syncthreads(); /* initial q(h_A), q(h_B), ix */
@@ -1441,12 +1593,26 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
 
     int az[S], ar[S], ah[S];
     auto recurrent = [&]() {
-      for (int s = 0; s < S; s++) {
-        az[s] = SAT ? 0 : wsz;
-        ar[s] = SAT ? 0 : wsr;
-        ah[s] = SAT ? 0 : wsh;
+      if constexpr (MF) {
+        v4i vz = {wsz, wsz, wsz, wsz}, vr = {wsr, wsr, wsr, wsr}, vh0 = {wsh, wsh, wsh, wsh}, vh1 = {0, 0, 0, 0};
+        mf_opaque(oz);
+        mf_opaque(orr);
+        mf_opaque(oh);
+        mf_zr(lds, wz, wr, oz, orr, nzr, vz, vr);
+        mf_run<MF_HMAX>(lds, wh, oh, nh, vh0, vh1);
+        for (int s = 0; s < S; s++) {
+          az[s] = vz[s];
+          ar[s] = vr[s];
+          ah[s] = vh0[s] + vh1[s];
+        }
+      } else {
+        for (int s = 0; s < S; s++) {
+          az[s] = SAT ? 0 : wsz;
+          ar[s] = SAT ? 0 : wsr;
+          ah[s] = SAT ? 0 : wsh;
+        }
+        gru_a_stream<S, SAT>(xa, wq, cq, qoff, coff, K4z, K4r, K4h, lane, az, ar, ah);
       }
-      gru_a_stream<S, SAT>(xa, wq, cq, qoff, coff, K4z, K4r, K4h, lane, az, ar, ah);
     };
     recurrent();
     for (int n = 0; n < A.N; n++) {
@@ -1472,9 +1638,12 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
         /* compute_sparse_gru elementwise (nnet.c:431-447) */
         float zrv[2 * S], hv[S], inh[S];
         for (int s = 0; s < S; s++) {
-          const float inz = ((cz[s] + e[s][0]) + e[s][3]) + e[s][6];
-          const float inr = ((cr[s] + e[s][1]) + e[s][4]) + e[s][7];
-          inh[s] = ((ch[s] + e[s][2]) + e[s][5]) + e[s][8];
+          const float czs = MF ? cnd[i * S + s] : cz[s];
+          const float crs = MF ? cnd[(NA + i) * S + s] : cr[s];
+          const float chs = MF ? cnd[(2 * NA + i) * S + s] : ch[s];
+          const float inz = ((czs + e[s][0]) + e[s][3]) + e[s][6];
+          const float inr = ((crs + e[s][1]) + e[s][4]) + e[s][7];
+          inh[s] = ((chs + e[s][2]) + e[s][5]) + e[s][8];
           zrv[s] = (float)(az[s] + cvt_rne(((bz + dz * st[s]) + inz) * kScale)) * kScale1;
           zrv[S + s] = (float)(ar[s] + cvt_rne(((br + dr * st[s]) + inr) * kScale)) * kScale1;
           hv[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
@@ -1493,11 +1662,22 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
       {
         /* GRU_B gate sums of row block rb (nnet.c:345-361) */
         int acc[S], accr[S];
-        for (int s = 0; s < S; s++) { acc[s] = 0; accr[s] = 0; }
-        gru_a_stream<S, SAT>(xa, wq, cq, A.gb_qoff[rb], A.gb_coff[rb], REG_GB / 4, 0, 0, lane, acc, acc, acc);
-        if (ks < NB / 4) {
-          const uint32_t w = ((const uint32_t *)(lds + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r8];
-          dot_streams<S, SAT>(xb, ks * S * 4, w, accr);
+        if constexpr (MF) {
+          v4i g0 = {0, 0, 0, 0}, g1 = {0, 0, 0, 0}, gr = {0, 0, 0, 0};
+          mf_opaque(ogb);
+          gr = mfma4(*(const uint32_t *)(lds + orec), wrec, gr);
+          mf_run<REG_GB>(lds, wgb, ogb, REG_GB / 4, g0, g1);
+          for (int s = 0; s < S; s++) {
+            acc[s] = g0[s] + g1[s];
+            accr[s] = gr[s];
+          }
+        } else {
+          for (int s = 0; s < S; s++) { acc[s] = 0; accr[s] = 0; }
+          gru_a_stream<S, SAT>(xa, wq, cq, A.gb_qoff[rb], A.gb_coff[rb], REG_GB / 4, 0, 0, lane, acc, acc, acc);
+          if (ks < NB / 4) {
+            const uint32_t w = ((const uint32_t *)(img + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r8];
+            dot_streams<S, SAT>(xb, ks * S * 4, w, accr);
+          }
         }
         for (int s = 0; s < S; s++) {
           acc[s] = sum_lanes_xor8_16_32(acc[s]);
@@ -1505,7 +1685,7 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
         }
         if (ks == 0) {
           for (int s = 0; s < S; s++) {
-            zr[s * 2 * GB_ROWS + row] = (float)(gb_seed[s] + acc[s]) * kScale1;
+            zr[s * 2 * GB_ROWS + row] = (float)((MF ? gbs[row * S + s] : gb_seed[s]) + acc[s]) * kScale1;
             zr[s * 2 * GB_ROWS + GB_ROWS + row] = (float)(gb_seedr + accr[s]) * kScale1;
           }
         }
@@ -1522,11 +1702,11 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
       if (active[s]) A.st[s0 + s].gru_a_state[i] = st[s];
   } else {
     /* ======================= sampler role ================================ */
-    const float *ulaw = (const float *)(lds + IMG_ULAW);
-    const float *logit_tab = (const float *)(lds + IMG_LOGIT);
-    const float *fcw = (const float *)(lds + IMG_FCW);
-    const float *fcb = (const float *)(lds + IMG_FCB);
-    const float *fcf = (const float *)(lds + IMG_FCF);
+    const float *ulaw = (const float *)(img + IMG_ULAW);
+    const float *logit_tab = (const float *)(img + IMG_LOGIT);
+    const float *fcw = (const float *)(img + IMG_FCW);
+    const float *fcb = (const float *)(img + IMG_FCB);
+    const float *fcf = (const float *)(img + IMG_FCF);
     /* with S=4 a sampler wave carries two streams, one per 32-lane half */
     const int sw = wv - SAMPLE_WAVES;
     const int half = lane >> 5, hl = lane & 31;
@@ -1721,27 +1901,34 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
   }
 }
 
-template <int S, bool SAT>
+template <int S, bool SAT, bool MF>
 static int launch_pipe_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
 {
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)pipe_kernel<S, SAT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-        hipSuccess)
+    if (hipFuncSetAttribute((const void *)pipe_kernel<S, SAT, MF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
       return -1;
     attr_set = true;
   }
   const int grid = (a.nstreams + S - 1) / S;
-  hipLaunchKernelGGL((pipe_kernel<S, SAT>), dim3(grid), dim3(PIPE_THREADS), lds_bytes, stream, a);
+  hipLaunchKernelGGL((pipe_kernel<S, SAT, MF>), dim3(grid), dim3(PIPE_THREADS), lds_bytes, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_pipe(const SampleArgs &a, int S, int sat, int lds_bytes, void *stream)
+template <int S>
+static int launch_pipe_s(const SampleArgs &a, int sat, int mf, int lds_bytes, hipStream_t st)
+{
+  if (mf) return sat ? -1 : launch_pipe_t<S, false, true>(a, lds_bytes, st);
+  return sat ? launch_pipe_t<S, true, false>(a, lds_bytes, st) : launch_pipe_t<S, false, false>(a, lds_bytes, st);
+}
+
+int launch_pipe(const SampleArgs &a, int S, int sat, int mf, int lds_bytes, void *stream)
 {
   hipStream_t st = (hipStream_t)stream;
-  if (S == 4) return sat ? launch_pipe_t<4, true>(a, lds_bytes, st) : launch_pipe_t<4, false>(a, lds_bytes, st);
-  if (S == 2) return sat ? launch_pipe_t<2, true>(a, lds_bytes, st) : launch_pipe_t<2, false>(a, lds_bytes, st);
-  return sat ? launch_pipe_t<1, true>(a, lds_bytes, st) : launch_pipe_t<1, false>(a, lds_bytes, st);
+  if (S == 4) return launch_pipe_s<4>(a, sat, mf, lds_bytes, st);
+  if (S == 2) return launch_pipe_s<2>(a, sat, mf, lds_bytes, st);
+  return launch_pipe_s<1>(a, sat, mf, lds_bytes, st);
 }
 
 template <int S, int V, bool SAT, bool REG>

@@ -31,16 +31,22 @@ def blobs():
 
 @pytest.mark.parametrize("name,kernel", [("streams_int8", 1), ("streams_fp32", 1), ("streams_int8_sat", 1),
                                          ("streams_int8", 2), ("streams_int8_sat", 2),
-                                         ("streams_int8", 3), ("streams_int8_sat", 3), ("streams_fp32", 3)])
+                                         ("streams_int8", 3), ("streams_int8_sat", 3), ("streams_fp32", 3),
+                                         ("streams_int8", 4), ("streams_int8_sat", 4), ("streams_fp32", 4),
+                                         ("streams_int8", 0)])
 def test_batch_matches_golden(require_gpu, blobs, name, kernel):
-    """kernel 1: lockstep sample_kernel, 2: wave-per-stream, 3: pipelined
-    (fp32 models always run the lockstep kernel)."""
+    """kernel 1: lockstep sample_kernel, 2: wave-per-stream, 3: pipelined,
+    4: pipelined on the matrix cores (saturating models fall back to 3),
+    0: automatic (4 for non-saturating int8).  fp32 models always run the
+    lockstep kernel."""
     G = np.load(os.path.join(GOLD, name + ".npz"))
     streams = list(G["streams"])
     F = G["pcm"].shape[1]
     b = L.LPCNetBatch(len(streams), 0, blobs[name])
     b.set_kernel(kernel)
-    expect = 1 if kernel == 1 or name == "streams_fp32" else kernel
+    expect = {0: 4, 1: 1, 2: 2, 3: 3, 4: 3 if name.endswith("_sat") else 4}[kernel]
+    if kernel != 1 and name.endswith("_sat") and kernel == 0:
+        expect = 3
     assert b.info().quad_path == (0 if name == "streams_fp32" else expect)
     info = b.info()
     assert info.variant == int(G["variant"])
@@ -77,7 +83,9 @@ def test_single_stream_api_matches_golden(require_gpu, blobs):
 @pytest.mark.parametrize("B,check,kernel", [(512, (0, 255, 511), 1), (1024, (0, 3, 517, 1023), 1),
                                             (1100, (1099, 1024, 5), 1), (1024, (0, 3, 517, 1023), 0),
                                             (1101, (1100, 1024, 5), 0), (300, (299, 7), 2),
-                                            (513, (512, 1, 300), 3), (1030, (1029, 1027, 2), 3)])
+                                            (513, (512, 1, 300), 3), (1030, (1029, 1027, 2), 3),
+                                            (513, (512, 1, 300), 4), (1030, (1029, 1027, 2), 4),
+                                            (1024, (0, 511, 1023), 4)])
 def test_large_batch_streams_match_oracle(require_gpu, blobs, B, check, kernel):
     """Lockstep kernel at 2 and 4 streams/workgroup, the wave-per-stream kernel
     (auto at >= 256 streams), ragged last workgroups, against the oracle."""
@@ -157,7 +165,7 @@ def test_full_size_properties(require_gpu, blobs):
     assert np.abs(o1[:, 2:].astype(np.float64)).mean() > 100
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3])
+@pytest.mark.parametrize("kernel", [1, 2, 3, 4])
 def test_preload_teacher_forcing_matches_oracle(require_gpu, blobs, kernel):
     """lpcnet_synthesize_impl with preload (lpcnet.c:256-259, the PLC entry)."""
     blob = blobs["streams_int8"]

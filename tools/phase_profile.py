@@ -28,7 +28,7 @@ def profile(B, variant=0, kernel=1):
     n = max(st[:, :, 7].max(), 1)
     per = st / n  # cycles per sample
     info = b.info()
-    k = 3 if info.quad_path == 3 else 1
+    k = 3 if info.quad_path in (3, 4) else 1
     print(f"B={B} variant={variant} kernel={info.kernel_name} groups={st.shape[0]}")
     for w in range(8):
         row = per[:, w, :].mean(0)
@@ -43,7 +43,9 @@ def profile(B, variant=0, kernel=1):
 
 
 if __name__ == "__main__":
-    for kern in (1, 3):
+    kerns = [int(k) for k in sys.argv[1].split(",")] if len(sys.argv) > 1 else [3, 4]
+    for kern in kerns:
         for B in (1, 1024):
             profile(B, 0, kern)
-    profile(1, 1)
+    if len(sys.argv) <= 2 or sys.argv[2] != "nofp32":
+        profile(1, 1)
