@@ -1762,11 +1762,34 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
 
     float thr[8];
     const bool tracing = A.trace_logits != nullptr;
+    /* Bookkeeping of sample n (lpcnet.c:260-270: LPC history shift,
+     * de-emphasis, output, q(h_B)) is deferred into the X->Y interval of
+     * sample n+1, where the sampler waves are otherwise idle; only the next
+     * indices ix(n+1) stay on the per-sample critical path. */
+    float pend_pcm = 0.f, pend_pred = 0.f;
+    int pend_exc = 0, pend_n = -1;
+    auto finish = [&]() {
+      if (pend_n < 0) return;
+#pragma unroll
+      for (int j = NLPC - 1; j > 0; j--) lsr[j] = lsr[j - 1];
+      lsr[0] = pend_pcm;
+      last_exc = pend_exc;
+      pred = pend_pred;
+      float o = pend_pcm + kPreemph * deemph;
+      deemph = o;
+      if (o < -32767) o = -32767;
+      if (o > 32767) o = 32767;
+      if (samp_w && hl == 0 && pend_n >= A.preload) pcmbuf[ms * FRAME + pend_n] = (short)round_half_up(o);
+      if (samp_w && hl < NB) xb[(hl >> 2) * S * 4 + ms * 4 + (hl & 3)] = (unsigned char)quant_s8(sbv);
+      pend_n = -1;
+    };
     for (int n = 0; n < A.N; n++) {
       stamp(4);
       __syncthreads(); /* X */
       stamp(5);
       if (samp) {
+        finish();
+        stamp(13);
         /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
         const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
         const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
@@ -1795,6 +1818,7 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
         sbv = zrb[0] * sbv + (1.f - zrb[0]) * h[0];
         if (samp_w && hl < NB) sbuf[s * NB + hl] = sbv;
       }
+      stamp(8);
       /* same-wave LDS exchange (measured faster than 32 v_readlane: gfx9
        * VALU ops read one SGPR each and SGPR hazards add wait states) */
       __builtin_amdgcn_wave_barrier();
@@ -1807,6 +1831,7 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
           xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
         }
       }
+      stamp(9);
       auto node_logit_w = [&](float bias, float factor, const float *w) -> float {
         float sum = bias;
 #pragma unroll
@@ -1831,6 +1856,23 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
           val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
         }
       }
+      stamp(10);
+      /* Speculation: with the top 4 bits of exc known, lane c of the half
+       * evaluates candidate exc = 16*val + c (c = lane & 15) -- its output
+       * sample, pred(n+1) and both u-law indices (lpcnet.c:252-254,
+       * 260-261) -- while levels 4..7 of the tree are walked; the walk then
+       * only selects a lane.  Same operations in the same order per candidate. */
+      const bool teach = n < A.preload;
+      float sp_pcm = 0.f, sp_pred = 0.f;
+      int sp_idx = 0;
+      if (!teach) {
+        sp_pcm = pred + ulaw[(val << 4) | (hl & 15)];
+        float p2 = 0.f - sp_pcm * lpr[0];
+#pragma unroll
+        for (int j = 1; j < NLPC; j++) p2 = p2 - lsr[j - 1] * lpr[j];
+        sp_pred = p2;
+        sp_idx = lin2ulaw_x86(sp_pcm) | (lin2ulaw_x86(sp_pred) << 8);
+      }
       {
         const int lvl = 4 + lvl_in;
         const int off = qq + 1 - (1 << (lvl - 4));
@@ -1845,26 +1887,30 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
           val = (val << 1) | (int)((m >> (2 * qi)) & 1ull);
         }
       }
-      int exc = val;
-      float pcm;
-      if (n < A.preload) {
+      stamp(11);
+      int exc = val, su, pu;
+      float pcm, pn;
+      if (teach) {
         /* teacher forcing (lpcnet.c:256-259) */
         const float o_in = (float)pcmbuf[s * FRAME + n];
         const float pd = kPreemph * deemph;
         exc = lin2ulaw_x86((o_in - pd) - pred);
         pcm = o_in - pd;
-      } else {
-        pcm = pred + ulaw[exc];
-      }
+        float p2 = 0.f - pcm * lpr[0];
 #pragma unroll
-      for (int j = NLPC - 1; j > 0; j--) lsr[j] = lsr[j - 1];
-      lsr[0] = pcm;
-      last_exc = exc;
-      float o = pcm + kPreemph * deemph;
-      deemph = o;
-      if (o < -32767) o = -32767;
-      if (o > 32767) o = 32767;
-      if (samp_w && hl == 0 && n >= A.preload) pcmbuf[s * FRAME + n] = (short)round_half_up(o);
+        for (int j = 1; j < NLPC; j++) p2 = p2 - lsr[j - 1] * lpr[j];
+        pn = p2;
+        su = lin2ulaw_x86(pcm);
+        pu = lin2ulaw_x86(pn);
+      } else {
+        const int src = hb + (exc & 15);
+        const int ic = __shfl(sp_idx, src);
+        su = ic & 0xFF;
+        pu = ic >> 8;
+        pcm = __shfl(sp_pcm, src);
+        pn = __shfl(sp_pred, src);
+      }
+      if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + s * 4) = make_int4(su, pu, exc, 0);
       if (tracing && samp_w && hl < 8 && my_active) {
         float v = lg[0];
 #pragma unroll
@@ -1872,9 +1918,13 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
         A.trace_logits[((size_t)(s0 + s) * A.N + n) * 8 + hl] = v;
       }
       if (A.trace_exc && samp_w && hl == 0 && my_active) A.trace_exc[(size_t)(s0 + s) * A.N + n] = exc;
-      if (samp_w && hl < NB) xb[(hl >> 2) * S * 4 + s * 4 + (hl & 3)] = (unsigned char)quant_s8(sbv);
-      if (n + 1 < A.N) pre_sample();
+      pend_pcm = pcm;
+      pend_pred = pn;
+      pend_exc = exc;
+      pend_n = n;
+      stamp(12);
     }
+    if (samp) finish();
     stamp(4);
     __syncthreads(); /* final */
     stamp(5);

@@ -35,6 +35,10 @@ def profile(B, variant=0, kernel=1):
         if row[6] == 0:
             continue
         print(f"  wave {w}: " + " ".join(f"{NAMES[k][j]}={row[j]:7.0f}" for j in range(6)) + f"  loop={row[6]:7.0f}")
+    if k == 3:
+        row = per[:, 6, :].mean(0)
+        print("  sampler detail (wave 6): Z->X gru_b=%.0f bcast=%.0f lvl0-3=%.0f lvl4-7+spec=%.0f select=%.0f | X->Y finish=%.0f" %
+              tuple(row[8:14]))
     if k == 1:
         row = per[:, 0, :].mean(0)
         print("  F detail (wave 0): gru_b=%.0f bcast=%.0f lvl0-3=%.0f lvl4-7=%.0f out=%.0f pre=%.0f" %
