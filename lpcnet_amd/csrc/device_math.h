@@ -1,0 +1,228 @@
+/*
+ * device_math.h -- exact x86 AVX2 numerics of the LPCNet synthesis path as
+ * CDNA4 device functions, shared by every sample-network kernel.
+ * Contract: SURVEY.md Appendix A.  Translation units including this header
+ * MUST be compiled with -ffp-contract=off.
+ */
+#ifndef LPCNET_DEVICE_MATH_H
+#define LPCNET_DEVICE_MATH_H
+
+#include <hip/hip_runtime.h>
+
+#include "lpcnet_engine.h"
+
+namespace lpcnet_mi355x {
+
+/* ------------------------------------------------------------------------ */
+/* numerics helpers                                                          */
+
+/* rcpps of a Pade denominator from its device table entry T = t + (127 << 23)
+ * (kRcpBias; t = rcpps(1.m), see rcp_x86): ldexp(t, 127 - e) as one integer
+ * subtraction of the exponent field, flushed to +0 below 2^-126 (a borrow
+ * into the sign reads negative).  Identical to the ldexp form for every den
+ * in [952.72, +inf] (oracle/checks/exact_identities.c (5)). */
+__device__ __forceinline__ float rcp_x86_fix(float x, uint32_t T)
+{
+  const int q = (int)(T - (__float_as_uint(x) & 0x7f800000u));
+  return q < 0x00800000 ? 0.f : __int_as_float(q);
+}
+
+/* clamp with _mm256_max_ps(lo, _mm256_min_ps(hi, v)) semantics: NaN stays
+ * NaN (the intrinsics return their second operand when unordered) */
+__device__ __forceinline__ float clamp_x86(float v, float lo, float hi)
+{
+  return v != v ? v : __builtin_amdgcn_fmed3f(v, lo, hi);
+}
+
+__device__ __forceinline__ float rcp_x86(float x, const uint32_t *tab)
+{
+  /* _mm256_rcp_ps of a Pade denominator (its only use, tanh8_approx and
+   * sigmoid8_approx): den = fma(fma(D2,X2,D1),X2,D0) with positive D's and
+   * X2 = X*X lies in [952.72, +inf] or is NaN.  rcpps there is the
+   * 2048-entry table of the top 11 mantissa bits, rebiased; results below
+   * 2^-126 (and rcp(+inf)) are +0.  ldexp + flush reproduces it for every
+   * such den (oracle/checks/exact_identities.c (4)); a NaN den only occurs
+   * with a NaN numerator, whose product stays NaN.  The table load is pinned
+   * (empty asm) so the select stays branch-free. */
+  const uint32_t u = __float_as_uint(x);
+  uint32_t t = tab[(u >> 12) & 0x7ff];
+  asm volatile("" : "+v"(t));
+  return rcp_x86_fix(x, t);
+}
+
+/* _mm256_min_ps / _mm256_max_ps return the second operand when unordered */
+__device__ __forceinline__ float mm_min(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float mm_max(float a, float b) { return a > b ? a : b; }
+
+/* vec_avx.h:393-411 tanh8_approx */
+__device__ __forceinline__ float tanh_x86(float X, const uint32_t *tab)
+{
+  float X2 = X * X;
+  float num = __builtin_fmaf(__builtin_fmaf(0.60863042f, X2, 96.39235687f), X2, 952.52801514f);
+  float den = __builtin_fmaf(__builtin_fmaf(11.88600922f, X2, 413.36801147f), X2, 952.72399902f);
+  num = num * X;
+  den = rcp_x86(den, tab);
+  num = num * den;
+  return clamp_x86(num, -1.f, 1.f);
+}
+
+/* vec_avx.h:421-440 sigmoid8_approx */
+__device__ __forceinline__ float sigmoid_x86(float X, const uint32_t *tab)
+{
+  float X2 = X * X;
+  float num = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
+  float den = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
+  num = num * X;
+  den = rcp_x86(den, tab);
+  num = __builtin_fmaf(num, den, 0.5f);
+  return clamp_x86(num, 0.f, 1.f);
+}
+
+/* N independent rcp_x86: all N table reads are issued before any is pinned,
+ * so their LDS latencies overlap (rcp_x86's pin alone serialises a chain). */
+template <int N>
+__device__ __forceinline__ void rcp_x86_n(float (&x)[N], const uint32_t *tab)
+{
+  uint32_t t[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) t[k] = tab[(__float_as_uint(x[k]) >> 12) & 0x7ff];
+#pragma unroll
+  for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
+#pragma unroll
+  for (int k = 0; k < N; k++) x[k] = rcp_x86_fix(x[k], t[k]);
+}
+
+/* N sigmoid8_approx / tanh8_approx lanes with one batched rcp (same
+ * arithmetic as sigmoid_x86 / tanh_x86, term for term) */
+template <int N>
+__device__ __forceinline__ void sigmoid_x86_n(float (&X)[N], const uint32_t *tab)
+{
+  float num[N], den[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const float X2 = X[k] * X[k];
+    num[k] = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
+    den[k] = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
+    num[k] = num[k] * X[k];
+  }
+  rcp_x86_n<N>(den, tab);
+#pragma unroll
+  for (int k = 0; k < N; k++) X[k] = clamp_x86(__builtin_fmaf(num[k], den[k], 0.5f), 0.f, 1.f);
+}
+
+template <int N>
+__device__ __forceinline__ void tanh_x86_n(float (&X)[N], const uint32_t *tab)
+{
+  float num[N], den[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const float X2 = X[k] * X[k];
+    num[k] = __builtin_fmaf(__builtin_fmaf(0.60863042f, X2, 96.39235687f), X2, 952.52801514f);
+    den[k] = __builtin_fmaf(__builtin_fmaf(11.88600922f, X2, 413.36801147f), X2, 952.72399902f);
+    num[k] = num[k] * X[k];
+  }
+  rcp_x86_n<N>(den, tab);
+#pragma unroll
+  for (int k = 0; k < N; k++) X[k] = clamp_x86(num[k] * den[k], -1.f, 1.f);
+}
+
+/* _mm256_cvtps_epi32: round to nearest even, out of range / NaN -> INT_MIN.
+ * v_cvt_i32_f32 saturates (-big -> INT_MIN, +big -> INT_MAX) and maps NaN
+ * to 0: only r >= 2^31 and NaN need the fix, and both fail r < 2^31. */
+__device__ __forceinline__ int cvt_rne(float v)
+{
+  const float r = __builtin_rintf(v);
+  int c;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(c) : "v"(r));
+  return r < 2147483648.f ? c : (int)0x80000000u;
+}
+
+/* vector_ps_to_epi8 (vec_avx.h:321-336) -> u8, returned XOR 0x80 (= u8-128,
+ * the signed form the int8 products consume): cvtps_epi32 then two unsigned
+ * saturating packs, i.e. 0 for NaN / r >= 2^31 (INT_MIN) and r <= 0,
+ * min(r, 255) otherwise. */
+__device__ __forceinline__ uint32_t quant_s8(float x)
+{
+  const float r = __builtin_rintf(__builtin_fmaf(x, 127.f, 127.f));
+  const uint32_t q = (uint32_t)__builtin_amdgcn_fmed3f(r, 0.f, 255.f);
+  return (r < 2147483648.f ? q : 0u) ^ 0x80u;
+}
+
+constexpr float kScale = 128.f * 127.f;          /* vec_avx.h:686 */
+constexpr float kScale1 = 1.f / 128.f / 127.f;   /* vec_avx.h:687 */
+constexpr float kLog256 = 5.5451774445f;         /* common.h:17 */
+constexpr float kRcpLog256 = 1.f / kLog256;       /* RN(1/log 256), see lin2ulaw_x86 */
+constexpr float kPreemph = 0.85f;                /* lpcnet.c:40 */
+
+/* common.h:18-33, 47-58 lin2ulaw */
+__device__ __forceinline__ int lin2ulaw_x86(float x)
+{
+  const float scale = 255.f / 32768.f;
+  int s = x >= 0 ? 1 : -1;
+  x = fabsf(x);
+  float y = 1 + scale * x;
+  uint32_t bits = __float_as_uint(y);
+  int integer = (int)(bits >> 23) - 127;
+  bits -= (uint32_t)integer << 23;
+  float frac = __uint_as_float(bits) - 1.5f;
+  frac = -0.41445418f + frac * (0.95909232f + frac * (-0.33951290f + frac * 0.16541097f));
+  float l2 = (float)(1 + integer) + frac;
+  /* RN(v / log(256)) by one FMA-corrected product: exact for every v in
+   * [2^-10, 2^15) (oracle/checks/exact_identities.c); v here is in
+   * [0.0395, 11500] */
+  const float v = 128.f * (0.69315f * l2);
+  const float q0 = v * kRcpLog256;
+  const float q = __builtin_fmaf(__builtin_fmaf(-q0, kLog256, v), kRcpLog256, q0);
+  float u = (float)s * q;
+  u = 128.f + u;
+  if (u < 0) u = 0;
+  if (u > 255) u = 255;
+  /* (int)floor(.5 + (double)u) for u in [0, 255] (exact_identities.c) */
+  const int k = (int)u;
+  return k + (u - (float)k >= .5f ? 1 : 0);
+}
+
+/* (int)floor(.5 + (double)o) for |o| <= 32767 (exact_identities.c) */
+__device__ __forceinline__ int round_half_up(float o)
+{
+  const float k = floorf(o);
+  return (int)k + (o - k >= .5f ? 1 : 0);
+}
+
+/* kiss99.c:59-81 */
+__device__ __forceinline__ uint32_t kiss99_next(uint32_t &z, uint32_t &w, uint32_t &jsr, uint32_t &jcong)
+{
+  uint32_t znew = 36969u * (z & 0xFFFF) + (z >> 16);
+  uint32_t wnew = 18000u * (w & 0xFFFF) + (w >> 16);
+  uint32_t mwc = (znew << 16) + wnew;
+  uint32_t shr3 = jsr ^ (jsr << 13);
+  shr3 ^= shr3 >> 17;
+  shr3 ^= shr3 << 5;
+  uint32_t cong = 69069u * jcong + 1234567u;
+  z = znew; w = wnew; jsr = shr3; jcong = cong;
+  return (mwc ^ cong) + shr3;
+}
+
+/* maddubs(u8 x, s8 w) pair sums with int16 saturation + madd(ones) for one
+ * 4-input group; x given in the XOR-0x80 signed form. */
+__device__ __forceinline__ int dot4_sat(uint32_t w, uint32_t xs)
+{
+  uint32_t xu = xs ^ 0x80808080u;
+  int x0 = xu & 0xff, x1 = (xu >> 8) & 0xff, x2 = (xu >> 16) & 0xff, x3 = xu >> 24;
+  int w0 = (int)(int8_t)(w & 0xff), w1 = (int)(int8_t)((w >> 8) & 0xff);
+  int w2 = (int)(int8_t)((w >> 16) & 0xff), w3 = (int)(int8_t)(w >> 24);
+  int p0 = min(max(x0 * w0 + x1 * w1, -32768), 32767);
+  int p1 = min(max(x2 * w2 + x3 * w3, -32768), 32767);
+  return p0 + p1;
+}
+
+template <bool SAT>
+__device__ __forceinline__ int dot4(uint32_t w, uint32_t xs, int acc)
+{
+  if constexpr (SAT) return acc + dot4_sat(w, xs);
+  else return __builtin_amdgcn_sdot4((int)w, (int)xs, acc, false);
+}
+
+}  // namespace lpcnet_mi355x
+
+#endif

@@ -288,9 +288,9 @@ struct LPCNetBatch {
   bool reg = false;
   int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 2 wave_kernel, 3 pipe_kernel, 4 matrix-core pipe_kernel */
   int wave_nw = 0;       /* >0: wave_kernel with this many streams per workgroup */
-  bool pipe = false;     /* pipe_kernel (modes 3, 4) */
+  bool pipe = false;     /* pipe_kernel (mode 3) */
   bool mf_ok = false;    /* model fits the matrix-core register tables */
-  bool mf = false;       /* pipe_kernel runs the matrix-core path */
+  bool mf = false;       /* mf_kernel (mode 4) */
   int image_bytes = 0;
   LPCNetModelInfo info{};
   std::vector<void *> model_bufs;
@@ -379,11 +379,10 @@ void choose_kernel(LPCNetBatch *b)
   const bool quad_int8 = b->variant == LPCNET_VARIANT_INT8 && b->reg;
   int mode = b->kernel_mode;
   if (mode == 0) mode = b->mf_ok ? 4 : (quad_int8 ? 3 : 1);
-  if (mode == 4 && b->mf_ok && pipe_lds_bytes(b->S, b->image_bytes, 1) <= 160 * 1024) {
-    b->pipe = true;
+  if (mode == 4 && b->mf_ok && mf_lds_bytes(b->S) <= 160 * 1024) {
     b->mf = true;
     b->info.streams_per_workgroup = b->S;
-    b->info.lds_bytes = pipe_lds_bytes(b->S, b->image_bytes, 1);
+    b->info.lds_bytes = mf_lds_bytes(b->S);
     b->info.quad_path = 4;
     return;
   }
@@ -399,10 +398,10 @@ void choose_kernel(LPCNetBatch *b)
       return;
     }
   }
-  if (mode == 3 && quad_int8 && pipe_lds_bytes(b->S, b->image_bytes, 0) <= 160 * 1024) {
+  if (mode == 3 && quad_int8 && pipe_lds_bytes(b->S, b->image_bytes) <= 160 * 1024) {
     b->pipe = true;
     b->info.streams_per_workgroup = b->S;
-    b->info.lds_bytes = pipe_lds_bytes(b->S, b->image_bytes, 0);
+    b->info.lds_bytes = pipe_lds_bytes(b->S, b->image_bytes);
     b->info.quad_path = 3;
     return;
   }
@@ -508,7 +507,9 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
 
   /* ---- LDS image ---- */
   std::vector<unsigned char> img(IMG_VAR, 0);
-  memcpy(&img[IMG_RCP], kRcpTable, sizeof(kRcpTable));
+  uint32_t rcp_dev[2048]; /* device form: t + (127 << 23), see rcp_x86_fix */
+  for (int i = 0; i < 2048; i++) rcp_dev[i] = kRcpTable[i] + kRcpBias;
+  memcpy(&img[IMG_RCP], rcp_dev, sizeof(rcp_dev));
   for (int i = 0; i < 256; i++) {
     float u = host_ulaw2lin((float)i);
     memcpy(&img[IMG_ULAW + 4 * i], &u, 4);
@@ -642,8 +643,8 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
     }
   align16();
 
-  /* ---- matrix-core register tables (non-saturating int8 models) ---- */
-  std::vector<uint32_t> mft;
+  /* ---- matrix-core tables (non-saturating int8 models, mf_kernel) ---- */
+  std::vector<uint32_t> mft, mfgb;
   bool mf_ok = int8 && !sat && !getenv("LPCNET_NO_MFMA");
   for (int w = 0; w < SAMPLE_WAVES && mf_ok; w++)
     for (int j = 0; j < 8; j++) {
@@ -651,10 +652,9 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
           (int)ga_blocks[2 * (NA / 8) + w * 8 + j].size() > MF_HMAX)
         mf_ok = false;
     }
-  for (int rb = 0; rb < GB_ROWS / 8 && mf_ok; rb++)
-    if ((int)gb_blocks[rb].size() > 8 * REG_GB) mf_ok = false;
   if (mf_ok) {
     const int8_t *wa = (const int8_t *)gaw->data, *wb = (const int8_t *)gbw, *wr = (const int8_t *)gbrec;
+    /* GRU_A: lane l of wave w = unit 64w + l, row l%8 of row block 8w + l/8 of each gate */
     mft.assign((size_t)SAMPLE_WAVES * MF_LANE_U32 * 64, 0);
     for (int w = 0; w < SAMPLE_WAVES; w++) {
       auto word = [&](int k, int l) -> uint32_t & { return mft[((size_t)w * MF_LANE_U32 + k) * 64 + l]; };
@@ -666,7 +666,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
       sa.mf_nzr[w] = (kz + 3) / 4;
       sa.mf_nh[w] = (kh + 3) / 4;
       for (int l = 0; l < 64; l++) {
-        const int j = l >> 3, r = l & 7, ks = l >> 3;
+        const int j = l >> 3, r = l & 7;
         for (int g = 0; g < 3; g++) {
           const int rb = g * (NA / 8) + w * 8 + j, base = g == 0 ? 0 : (g == 1 ? MF_ZMAX : 2 * MF_ZMAX);
           for (int t = 0; t < (int)ga_blocks[rb].size(); t++) {
@@ -674,19 +674,27 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
             word(MF_GA + (base + t) / 4, l) |= (uint32_t)(ga_blocks[rb][t] / 4) << (8 * ((base + t) & 3));
           }
         }
-        /* GRU_B row block w: input blocks ks + 8t, recurrent column block ks */
-        for (int t = 0; t < REG_GB; t++) {
-          const int k = ks + 8 * t;
-          if (k >= (int)gb_blocks[w].size()) continue;
-          memcpy(&word(MF_W_GB + t, l), wb + 32 * (gb_first[w] + k) + 4 * r, 4);
-          word(MF_C_GB + t / 4, l) |= (uint32_t)(gb_blocks[w][k] / 4) << (8 * (t & 3));
-        }
-        if (ks < NB / 4) {
-          memcpy(&word(MF_W_GBREC, l), wr + 32 * (w * (NB / 4) + ks) + 4 * r, 4);
-          word(MF_C_GB + REG_GB / 4, l) |= (uint32_t)ks;
-        }
       }
     }
+    /* GRU_B: dense A tiles, lane l = row 16g + l%16, k = 64kt + 16(l/16) + byte */
+    std::vector<int8_t> dense((size_t)GB_ROWS * NA, 0), drec((size_t)GB_ROWS * NB, 0);
+    for (int rb = 0; rb < GB_ROWS / 8; rb++)
+      for (int t = 0; t < (int)gb_blocks[rb].size(); t++)
+        for (int r = 0; r < 8; r++)
+          for (int c = 0; c < 4; c++)
+            dense[(size_t)(rb * 8 + r) * NA + gb_blocks[rb][t] + c] = wb[32 * (gb_first[rb] + t) + 4 * r + c];
+    for (int rb = 0; rb < GB_ROWS / 8; rb++)
+      for (int cb = 0; cb < NB / 4; cb++)
+        for (int r = 0; r < 8; r++)
+          for (int c = 0; c < 4; c++) drec[(rb * 8 + r) * NB + 4 * cb + c] = wr[32 * (rb * (NB / 4) + cb) + 4 * r + c];
+    mfgb.assign((size_t)MF_GB_TILES * 64 * 4, 0);
+    for (int g = 0; g < 3; g++)
+      for (int l = 0; l < 64; l++) {
+        const int row = 16 * g + (l & 15), k0 = 16 * (l >> 4);
+        for (int kt = 0; kt < 6; kt++)
+          memcpy((int8_t *)&mfgb[((size_t)(g * 6 + kt) * 64 + l) * 4], &dense[(size_t)row * NA + 64 * kt + k0], 16);
+        if (k0 == 0) memcpy((int8_t *)&mfgb[((size_t)(18 + g) * 64 + l) * 4], &drec[row * NB], 16);
+      }
   }
 
   /* choose streams per workgroup and check the LDS budget */
@@ -718,7 +726,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   UP(fa.gbdf_w, gbdf_w, COND * GB_ROWS * 4);
   UP(fa.gbdf_b, gbdf_b, GB_ROWS * 4);
   UP(fa.embed_pitch, embed_pitch, 256 * EP * 4);
-  UP(fa.rcp, kRcpTable, sizeof(kRcpTable));
+  UP(fa.rcp, rcp_dev, sizeof(rcp_dev));
   UP(sa.emb_sig, emb_sig, 256 * GA_ROWS * 4);
   UP(sa.emb_pred, emb_pred, 256 * GA_ROWS * 4);
   UP(sa.emb_exc, emb_exc, 256 * GA_ROWS * 4);
@@ -727,7 +735,10 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   UP(sa.gb_par, gb_par.data(), gb_par.size() * 4);
   UP(sa.gb_wsum, gb_wsum.data(), gb_wsum.size() * 4);
   UP(sa.image, img.data(), img.size());
-  if (mf_ok) UP(sa.mf, mft.data(), mft.size() * 4);
+  if (mf_ok) {
+    UP(sa.mf, mft.data(), mft.size() * 4);
+    UP(sa.mf_gb, mfgb.data(), mfgb.size() * 4);
+  }
   if (!int8) {
     UP(sa.ga_wf, ga_wf.data(), ga_wf.size() * sizeof(float4));
     UP(sa.gb_recf, gbrec, 3 * NB * NB * 4);
@@ -811,7 +822,8 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
   const int lrc = N <= 0 ? 0
-                : b->pipe  ? launch_pipe(sa, b->S, b->sat ? 1 : 0, b->mf ? 1 : 0, b->info.lds_bytes, b->stream)
+                : b->mf    ? launch_mf(sa, b->S, b->info.lds_bytes, b->stream)
+                : b->pipe  ? launch_pipe(sa, b->S, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
                 : b->wave_nw ? launch_wave(sa, b->wave_nw, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
                              : launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream);
   if (lrc) {

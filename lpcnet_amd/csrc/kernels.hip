@@ -22,203 +22,11 @@
  */
 #include <hip/hip_runtime.h>
 
+#include "device_math.h"
 #include "lpcnet_engine.h"
+#include "sampler.h"
 
 namespace lpcnet_mi355x {
-
-/* ------------------------------------------------------------------------ */
-/* numerics helpers                                                          */
-
-/* rcpps of a Pade denominator from its table entry t (see rcp_x86) */
-__device__ __forceinline__ float rcp_x86_fix(float x, uint32_t t)
-{
-  const int e = (int)((__float_as_uint(x) >> 23) & 0xff);
-  const float q = __builtin_ldexpf(__uint_as_float(t), 127 - e);
-  return q < 0x1p-126f ? 0.f : q;
-}
-
-__device__ __forceinline__ float rcp_x86(float x, const uint32_t *tab)
-{
-  /* _mm256_rcp_ps of a Pade denominator (its only use, tanh8_approx and
-   * sigmoid8_approx): den = fma(fma(D2,X2,D1),X2,D0) with positive D's and
-   * X2 = X*X lies in [952.72, +inf] or is NaN.  rcpps there is the
-   * 2048-entry table of the top 11 mantissa bits, rebiased; results below
-   * 2^-126 (and rcp(+inf)) are +0.  ldexp + flush reproduces it for every
-   * such den (oracle/checks/exact_identities.c (4)); a NaN den only occurs
-   * with a NaN numerator, whose product stays NaN.  The table load is pinned
-   * (empty asm) so the select stays branch-free. */
-  const uint32_t u = __float_as_uint(x);
-  uint32_t t = tab[(u >> 12) & 0x7ff];
-  asm volatile("" : "+v"(t));
-  return rcp_x86_fix(x, t);
-}
-
-/* _mm256_min_ps / _mm256_max_ps return the second operand when unordered */
-__device__ __forceinline__ float mm_min(float a, float b) { return a < b ? a : b; }
-__device__ __forceinline__ float mm_max(float a, float b) { return a > b ? a : b; }
-
-/* vec_avx.h:393-411 tanh8_approx */
-__device__ __forceinline__ float tanh_x86(float X, const uint32_t *tab)
-{
-  float X2 = X * X;
-  float num = __builtin_fmaf(__builtin_fmaf(0.60863042f, X2, 96.39235687f), X2, 952.52801514f);
-  float den = __builtin_fmaf(__builtin_fmaf(11.88600922f, X2, 413.36801147f), X2, 952.72399902f);
-  num = num * X;
-  den = rcp_x86(den, tab);
-  num = num * den;
-  return mm_max(-1.f, mm_min(1.f, num));
-}
-
-/* vec_avx.h:421-440 sigmoid8_approx */
-__device__ __forceinline__ float sigmoid_x86(float X, const uint32_t *tab)
-{
-  float X2 = X * X;
-  float num = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
-  float den = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
-  num = num * X;
-  den = rcp_x86(den, tab);
-  num = __builtin_fmaf(num, den, 0.5f);
-  return mm_max(0.f, mm_min(1.f, num));
-}
-
-/* N independent rcp_x86: all N table reads are issued before any is pinned,
- * so their LDS latencies overlap (rcp_x86's pin alone serialises a chain). */
-template <int N>
-__device__ __forceinline__ void rcp_x86_n(float (&x)[N], const uint32_t *tab)
-{
-  uint32_t t[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) t[k] = tab[(__float_as_uint(x[k]) >> 12) & 0x7ff];
-#pragma unroll
-  for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
-#pragma unroll
-  for (int k = 0; k < N; k++) x[k] = rcp_x86_fix(x[k], t[k]);
-}
-
-/* N sigmoid8_approx / tanh8_approx lanes with one batched rcp (same
- * arithmetic as sigmoid_x86 / tanh_x86, term for term) */
-template <int N>
-__device__ __forceinline__ void sigmoid_x86_n(float (&X)[N], const uint32_t *tab)
-{
-  float num[N], den[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) {
-    const float X2 = X[k] * X[k];
-    num[k] = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
-    den[k] = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
-    num[k] = num[k] * X[k];
-  }
-  rcp_x86_n<N>(den, tab);
-#pragma unroll
-  for (int k = 0; k < N; k++) X[k] = mm_max(0.f, mm_min(1.f, __builtin_fmaf(num[k], den[k], 0.5f)));
-}
-
-template <int N>
-__device__ __forceinline__ void tanh_x86_n(float (&X)[N], const uint32_t *tab)
-{
-  float num[N], den[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) {
-    const float X2 = X[k] * X[k];
-    num[k] = __builtin_fmaf(__builtin_fmaf(0.60863042f, X2, 96.39235687f), X2, 952.52801514f);
-    den[k] = __builtin_fmaf(__builtin_fmaf(11.88600922f, X2, 413.36801147f), X2, 952.72399902f);
-    num[k] = num[k] * X[k];
-  }
-  rcp_x86_n<N>(den, tab);
-#pragma unroll
-  for (int k = 0; k < N; k++) X[k] = mm_max(-1.f, mm_min(1.f, num[k] * den[k]));
-}
-
-/* _mm256_cvtps_epi32: round to nearest even, out of range / NaN -> INT_MIN */
-__device__ __forceinline__ int cvt_rne(float v)
-{
-  float r = __builtin_rintf(v);
-  return (r >= -2147483648.f && r < 2147483648.f) ? (int)r : (int)0x80000000u;
-}
-
-/* vector_ps_to_epi8 (vec_avx.h:321-336) -> u8, returned XOR 0x80 (= u8-128,
- * the signed form the dot4 path consumes) */
-__device__ __forceinline__ uint32_t quant_s8(float x)
-{
-  float r = __builtin_rintf(__builtin_fmaf(x, 127.f, 127.f));
-  uint32_t q = (r > 0.f && r < 2147483648.f) ? (uint32_t)fminf(r, 255.f) : 0u;
-  return q ^ 0x80u;
-}
-
-constexpr float kScale = 128.f * 127.f;          /* vec_avx.h:686 */
-constexpr float kScale1 = 1.f / 128.f / 127.f;   /* vec_avx.h:687 */
-constexpr float kLog256 = 5.5451774445f;         /* common.h:17 */
-constexpr float kRcpLog256 = 1.f / kLog256;       /* RN(1/log 256), see lin2ulaw_x86 */
-constexpr float kPreemph = 0.85f;                /* lpcnet.c:40 */
-
-/* common.h:18-33, 47-58 lin2ulaw */
-__device__ __forceinline__ int lin2ulaw_x86(float x)
-{
-  const float scale = 255.f / 32768.f;
-  int s = x >= 0 ? 1 : -1;
-  x = fabsf(x);
-  float y = 1 + scale * x;
-  uint32_t bits = __float_as_uint(y);
-  int integer = (int)(bits >> 23) - 127;
-  bits -= (uint32_t)integer << 23;
-  float frac = __uint_as_float(bits) - 1.5f;
-  frac = -0.41445418f + frac * (0.95909232f + frac * (-0.33951290f + frac * 0.16541097f));
-  float l2 = (float)(1 + integer) + frac;
-  /* RN(v / log(256)) by one FMA-corrected product: exact for every v in
-   * [2^-10, 2^15) (oracle/checks/exact_identities.c); v here is in
-   * [0.0395, 11500] */
-  const float v = 128.f * (0.69315f * l2);
-  const float q0 = v * kRcpLog256;
-  const float q = __builtin_fmaf(__builtin_fmaf(-q0, kLog256, v), kRcpLog256, q0);
-  float u = (float)s * q;
-  u = 128.f + u;
-  if (u < 0) u = 0;
-  if (u > 255) u = 255;
-  /* (int)floor(.5 + (double)u) for u in [0, 255] (exact_identities.c) */
-  const int k = (int)u;
-  return k + (u - (float)k >= .5f ? 1 : 0);
-}
-
-/* (int)floor(.5 + (double)o) for |o| <= 32767 (exact_identities.c) */
-__device__ __forceinline__ int round_half_up(float o)
-{
-  const float k = floorf(o);
-  return (int)k + (o - k >= .5f ? 1 : 0);
-}
-
-/* kiss99.c:59-81 */
-__device__ __forceinline__ uint32_t kiss99_next(uint32_t &z, uint32_t &w, uint32_t &jsr, uint32_t &jcong)
-{
-  uint32_t znew = 36969u * (z & 0xFFFF) + (z >> 16);
-  uint32_t wnew = 18000u * (w & 0xFFFF) + (w >> 16);
-  uint32_t mwc = (znew << 16) + wnew;
-  uint32_t shr3 = jsr ^ (jsr << 13);
-  shr3 ^= shr3 >> 17;
-  shr3 ^= shr3 << 5;
-  uint32_t cong = 69069u * jcong + 1234567u;
-  z = znew; w = wnew; jsr = shr3; jcong = cong;
-  return (mwc ^ cong) + shr3;
-}
-
-/* maddubs(u8 x, s8 w) pair sums with int16 saturation + madd(ones) for one
- * 4-input group; x given in the XOR-0x80 signed form. */
-__device__ __forceinline__ int dot4_sat(uint32_t w, uint32_t xs)
-{
-  uint32_t xu = xs ^ 0x80808080u;
-  int x0 = xu & 0xff, x1 = (xu >> 8) & 0xff, x2 = (xu >> 16) & 0xff, x3 = xu >> 24;
-  int w0 = (int)(int8_t)(w & 0xff), w1 = (int)(int8_t)((w >> 8) & 0xff);
-  int w2 = (int)(int8_t)((w >> 16) & 0xff), w3 = (int)(int8_t)(w >> 24);
-  int p0 = min(max(x0 * w0 + x1 * w1, -32768), 32767);
-  int p1 = min(max(x2 * w2 + x3 * w3, -32768), 32767);
-  return p0 + p1;
-}
-
-template <bool SAT>
-__device__ __forceinline__ int dot4(uint32_t w, uint32_t xs, int acc)
-{
-  if constexpr (SAT) return acc + dot4_sat(w, xs);
-  else return __builtin_amdgcn_sdot4((int)w, (int)xs, acc, false);
-}
 
 /* ------------------------------------------------------------------------ */
 /* frame network                                                             */
@@ -1341,7 +1149,7 @@ int launch_frame(const FrameArgs &a, void *stream)
  *      GRU_A waves: W·q(h_A(n)) for sample n+1
  *      sampler waves: GRU_B update, tree walk, output, pred(n+1) -> ix(n+1)
  * Same arithmetic as sample_kernel's quad path, term for term. */
-template <int S, bool MF>
+template <int S>
 struct PipeLds {
   static constexpr int x = (NA / 4) * S * 4;   /* quantized GRU_A state (single buffer) */
   static constexpr int xb = (NB / 4) * S * 4;  /* quantized GRU_B state */
@@ -1349,131 +1157,28 @@ struct PipeLds {
   static constexpr int zr = S * 2 * GB_ROWS * 4;
   static constexpr int ix = S * 4 * 4;
   static constexpr int pcm = ((S * FRAME * 2 + 15) / 16) * 16;
-  /* matrix-core path: frame constants kept out of registers -- GRU_A
-   * conditioning [3][NA][S] and GRU_B accumulator seeds [GB_ROWS][S] */
-  static constexpr int cnd = MF ? GA_ROWS * S * 4 : 0;
-  static constexpr int gbs = MF ? GB_ROWS * S * 4 : 0;
-  static constexpr int total = x + xb + sb + zr + ix + pcm + cnd + gbs;
+  static constexpr int total = x + xb + sb + zr + ix + pcm;
 };
 
-/* LDS: quad path = [image | regions]; matrix-core path = [regions | fixed
- * image sections] (x first, so every x address fits the 16-bit offsets the
- * lanes keep in registers; the GRU weights live in registers). */
-int pipe_lds_bytes(int S, int image_bytes, int mf)
+/* LDS: [image | regions] */
+int pipe_lds_bytes(int S, int image_bytes)
 {
-  if (mf) return IMG_VAR + (S == 4 ? PipeLds<4, true>::total : (S == 2 ? PipeLds<2, true>::total : PipeLds<1, true>::total));
-  return image_bytes + (S == 4 ? PipeLds<4, false>::total : (S == 2 ? PipeLds<2, false>::total : PipeLds<1, false>::total));
+  return image_bytes + (S == 4 ? PipeLds<4>::total : (S == 2 ? PipeLds<2>::total : PipeLds<1>::total));
 }
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-
-/* Keep packed offsets packed: without this the compiler hoists every
- * unpacked 16-bit offset out of the sample loop (one VGPR per slot). */
-template <int N>
-__device__ __forceinline__ void mf_opaque(uint32_t (&o)[N])
-{
-#pragma unroll
-  for (int k = 0; k < N; k++) asm volatile("" : "+v"(o[k]));
-}
-
-/* x word of slot t: the packed 16-bit LDS byte offsets o[t/2] */
-template <int NO>
-__device__ __forceinline__ uint32_t mf_x(const unsigned char *lds, const uint32_t (&o)[NO], int t)
-{
-  return *(const uint32_t *)(lds + ((o[t >> 1] >> (16 * (t & 1))) & 0xFFFF));
-}
-
-/* v_mfma_i32_4x4x4_16b_i8, 16 blocks: block b = lanes 4b..4b+3.
- * A (src0) lane 4b+m: 4 int8 of row m (= stream m's x quad of the block's
- * column block); B (src1) lane 4b+n: 4 int8 of column n (= weight row n);
- * D lane 4b+n, register m: sum over k of A[m][k] B[k][n] (exact int32).
- * Layout measured on gfx950 (tools/probes/mfma_i8_probe.hip). */
-__device__ __forceinline__ v4i mfma4(uint32_t x, uint32_t w, v4i acc)
-{
-  return __builtin_amdgcn_mfma_i32_4x4x4i8((int)x, (int)w, acc, 0, 0, 0);
-}
-
-/* GRU_A z and r products over ng 4-slot groups (wave-uniform ng): the two
- * gates interleave (independent accumulators), x words of group g+1 are
- * read from LDS while the MFMAs of group g run. */
-__device__ __forceinline__ void mf_zr(const unsigned char *lds, const uint32_t (&wz)[MF_ZMAX],
-                                      const uint32_t (&wr)[MF_ZMAX], const uint32_t (&oz)[MF_ZMAX / 2],
-                                      const uint32_t (&orr)[MF_ZMAX / 2], int ng, v4i &az, v4i &ar)
-{
-  uint32_t xz[4], xr[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    xz[k] = mf_x(lds, oz, k);
-    xr[k] = mf_x(lds, orr, k);
-  }
-#pragma unroll
-  for (int g = 0; g < MF_ZMAX / 4; g++) {
-    if (g < ng) {
-      uint32_t nz[4], nr[4];
-      if (g + 1 < MF_ZMAX / 4 && g + 1 < ng) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          nz[k] = mf_x(lds, oz, 4 * (g + 1) + k);
-          nr[k] = mf_x(lds, orr, 4 * (g + 1) + k);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        az = mfma4(xz[k], wz[4 * g + k], az);
-        ar = mfma4(xr[k], wr[4 * g + k], ar);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        xz[k] = nz[k];
-        xr[k] = nr[k];
-      }
-    }
-  }
-}
-
-/* NS-slot product over ng 4-slot groups, alternating two accumulators */
-template <int NS>
-__device__ __forceinline__ void mf_run(const unsigned char *lds, const uint32_t (&w)[NS], const uint32_t (&o)[NS / 2],
-                                       int ng, v4i &a0, v4i &a1)
-{
-  uint32_t x[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) x[k] = mf_x(lds, o, k);
-#pragma unroll
-  for (int g = 0; g < NS / 4; g++) {
-    if (g < ng) {
-      uint32_t n[4];
-      if (g + 1 < NS / 4 && g + 1 < ng) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) n[k] = mf_x(lds, o, 4 * (g + 1) + k);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        if (k & 1) a1 = mfma4(x[k], w[4 * g + k], a1);
-        else a0 = mfma4(x[k], w[4 * g + k], a0);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) x[k] = n[k];
-    }
-  }
-}
-
-template <int S, bool SAT, bool MF>
+template <int S, bool SAT>
 __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
 {
   extern __shared__ uint4 lds4[];
   unsigned char *lds = (unsigned char *)lds4;
-  using L = PipeLds<S, MF>;
-  static_assert(!(MF && SAT), "the matrix-core path has no int16 saturation");
-  unsigned char *img = MF ? lds + L::total : lds;
-  unsigned char *xa = MF ? lds : lds + A.image_bytes;
+  using L = PipeLds<S>;
+  unsigned char *img = lds;
+  unsigned char *xa = lds + A.image_bytes;
   unsigned char *xb = xa + L::x;
   float *sbuf = (float *)(xb + L::xb);
   float *zr = sbuf + S * NB;
   int *ix = (int *)(zr + S * 2 * GB_ROWS);
   short *pcmbuf = (short *)(ix + S * 4);
-  float *cnd = (float *)((unsigned char *)pcmbuf + L::pcm);
-  int *gbs = (int *)((unsigned char *)cnd + L::cnd);
 
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = blockIdx.x * S;
@@ -1495,7 +1200,7 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
   }
   {
     uint4 *img4 = (uint4 *)img;
-    const int n16 = (MF ? IMG_VAR : A.image_bytes) / 16;
+    const int n16 = A.image_bytes / 16;
     for (int o = tid; o < n16; o += PIPE_THREADS) img4[o] = A.image[o];
   }
   for (int e = tid; e < S * A.preload; e += PIPE_THREADS) {
@@ -1541,51 +1246,8 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
       cr[s] = p->gru_a_cond[NA + i];
       ch[s] = p->gru_a_cond[2 * NA + i];
       gb_seed[s] = cvt_rne((A.gb_par[row] + p->gru_b_cond[row]) * kScale) + (SAT ? 0 : A.gb_wsum[row]);
-      if constexpr (MF) {
-        cnd[i * S + s] = cz[s];
-        cnd[(NA + i) * S + s] = cr[s];
-        cnd[(2 * NA + i) * S + s] = ch[s];
-        if (ks == 0) gbs[row * S + s] = gb_seed[s];
-      }
     }
     const int gb_seedr = cvt_rne(A.gb_par[GB_ROWS + row] * kScale) + (SAT ? 0 : A.gb_wsum[GB_ROWS + row]);
-    /* matrix-core path: this lane's weight rows and x offsets, for all N samples */
-    uint32_t wz[MF_ZMAX], wr[MF_ZMAX], wh[MF_HMAX], oz[MF_ZMAX / 2], orr[MF_ZMAX / 2], oh[MF_HMAX / 2];
-    uint32_t wgb[REG_GB], ogb[REG_GB / 2], wrec = 0, orec = 0;
-    int nzr = 0, nh = 0;
-    if constexpr (MF) {
-      const uint32_t *mt = A.mf + (size_t)wv * MF_LANE_U32 * 64 + lane;
-#pragma unroll
-      for (int t = 0; t < MF_ZMAX; t++) {
-        wz[t] = mt[t * 64];
-        wr[t] = mt[(MF_ZMAX + t) * 64];
-      }
-#pragma unroll
-      for (int t = 0; t < MF_HMAX; t++) wh[t] = mt[(2 * MF_ZMAX + t) * 64];
-#pragma unroll
-      for (int t = 0; t < REG_GB; t++) wgb[t] = mt[(MF_W_GB + t) * 64];
-      wrec = mt[MF_W_GBREC * 64];
-      uint32_t cw[MF_GA / 4], cg[4];
-#pragma unroll
-      for (int k = 0; k < MF_GA / 4; k++) cw[k] = mt[(MF_GA + k) * 64];
-#pragma unroll
-      for (int k = 0; k < 4; k++) cg[k] = mt[(MF_C_GB + k) * 64];
-      /* A operand of lane 4b+m = stream m (lanes m >= S duplicate stream S-1) */
-      const uint32_t mo = (uint32_t)min(lane & 3, S - 1) * 4;
-      auto off = [&](const uint32_t *c, int t) -> uint32_t { return ((c[t >> 2] >> (8 * (t & 3))) & 0xFF) * (S * 4) + mo; };
-#pragma unroll
-      for (int t = 0; t < MF_ZMAX / 2; t++) {
-        oz[t] = off(cw, 2 * t) | (off(cw, 2 * t + 1) << 16);
-        orr[t] = off(cw, MF_ZMAX + 2 * t) | (off(cw, MF_ZMAX + 2 * t + 1) << 16);
-      }
-#pragma unroll
-      for (int t = 0; t < MF_HMAX / 2; t++) oh[t] = off(cw, 2 * MF_ZMAX + 2 * t) | (off(cw, 2 * MF_ZMAX + 2 * t + 1) << 16);
-#pragma unroll
-      for (int t = 0; t < REG_GB / 2; t++) ogb[t] = off(cg, 2 * t) | (off(cg, 2 * t + 1) << 16);
-      orec = (uint32_t)L::x + off(cg, REG_GB);
-      nzr = A.mf_nzr[wv];
-      nh = A.mf_nh[wv];
-    }
     __syncthreads(); /* image in LDS */
     for (int s = 0; s < S; s++) xa[(i >> 2) * S * 4 + s * 4 + (i & 3)] = (unsigned char)quant_s8(st[s]);
     __syncthreads(); /* initial q(h_A), q(h_B), ix */
@@ -1593,26 +1255,12 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
 
     int az[S], ar[S], ah[S];
     auto recurrent = [&]() {
-      if constexpr (MF) {
-        v4i vz = {wsz, wsz, wsz, wsz}, vr = {wsr, wsr, wsr, wsr}, vh0 = {wsh, wsh, wsh, wsh}, vh1 = {0, 0, 0, 0};
-        mf_opaque(oz);
-        mf_opaque(orr);
-        mf_opaque(oh);
-        mf_zr(lds, wz, wr, oz, orr, nzr, vz, vr);
-        mf_run<MF_HMAX>(lds, wh, oh, nh, vh0, vh1);
-        for (int s = 0; s < S; s++) {
-          az[s] = vz[s];
-          ar[s] = vr[s];
-          ah[s] = vh0[s] + vh1[s];
-        }
-      } else {
-        for (int s = 0; s < S; s++) {
-          az[s] = SAT ? 0 : wsz;
-          ar[s] = SAT ? 0 : wsr;
-          ah[s] = SAT ? 0 : wsh;
-        }
-        gru_a_stream<S, SAT>(xa, wq, cq, qoff, coff, K4z, K4r, K4h, lane, az, ar, ah);
+      for (int s = 0; s < S; s++) {
+        az[s] = SAT ? 0 : wsz;
+        ar[s] = SAT ? 0 : wsr;
+        ah[s] = SAT ? 0 : wsh;
       }
+      gru_a_stream<S, SAT>(xa, wq, cq, qoff, coff, K4z, K4r, K4h, lane, az, ar, ah);
     };
     recurrent();
     for (int n = 0; n < A.N; n++) {
@@ -1638,12 +1286,9 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
         /* compute_sparse_gru elementwise (nnet.c:431-447) */
         float zrv[2 * S], hv[S], inh[S];
         for (int s = 0; s < S; s++) {
-          const float czs = MF ? cnd[i * S + s] : cz[s];
-          const float crs = MF ? cnd[(NA + i) * S + s] : cr[s];
-          const float chs = MF ? cnd[(2 * NA + i) * S + s] : ch[s];
-          const float inz = ((czs + e[s][0]) + e[s][3]) + e[s][6];
-          const float inr = ((crs + e[s][1]) + e[s][4]) + e[s][7];
-          inh[s] = ((chs + e[s][2]) + e[s][5]) + e[s][8];
+          const float inz = ((cz[s] + e[s][0]) + e[s][3]) + e[s][6];
+          const float inr = ((cr[s] + e[s][1]) + e[s][4]) + e[s][7];
+          inh[s] = ((ch[s] + e[s][2]) + e[s][5]) + e[s][8];
           zrv[s] = (float)(az[s] + cvt_rne(((bz + dz * st[s]) + inz) * kScale)) * kScale1;
           zrv[S + s] = (float)(ar[s] + cvt_rne(((br + dr * st[s]) + inr) * kScale)) * kScale1;
           hv[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
@@ -1662,22 +1307,11 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
       {
         /* GRU_B gate sums of row block rb (nnet.c:345-361) */
         int acc[S], accr[S];
-        if constexpr (MF) {
-          v4i g0 = {0, 0, 0, 0}, g1 = {0, 0, 0, 0}, gr = {0, 0, 0, 0};
-          mf_opaque(ogb);
-          gr = mfma4(*(const uint32_t *)(lds + orec), wrec, gr);
-          mf_run<REG_GB>(lds, wgb, ogb, REG_GB / 4, g0, g1);
-          for (int s = 0; s < S; s++) {
-            acc[s] = g0[s] + g1[s];
-            accr[s] = gr[s];
-          }
-        } else {
-          for (int s = 0; s < S; s++) { acc[s] = 0; accr[s] = 0; }
-          gru_a_stream<S, SAT>(xa, wq, cq, A.gb_qoff[rb], A.gb_coff[rb], REG_GB / 4, 0, 0, lane, acc, acc, acc);
-          if (ks < NB / 4) {
-            const uint32_t w = ((const uint32_t *)(img + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r8];
-            dot_streams<S, SAT>(xb, ks * S * 4, w, accr);
-          }
+        for (int s = 0; s < S; s++) { acc[s] = 0; accr[s] = 0; }
+        gru_a_stream<S, SAT>(xa, wq, cq, A.gb_qoff[rb], A.gb_coff[rb], REG_GB / 4, 0, 0, lane, acc, acc, acc);
+        if (ks < NB / 4) {
+          const uint32_t w = ((const uint32_t *)(img + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r8];
+          dot_streams<S, SAT>(xb, ks * S * 4, w, accr);
         }
         for (int s = 0; s < S; s++) {
           acc[s] = sum_lanes_xor8_16_32(acc[s]);
@@ -1685,7 +1319,7 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
         }
         if (ks == 0) {
           for (int s = 0; s < S; s++) {
-            zr[s * 2 * GB_ROWS + row] = (float)((MF ? gbs[row * S + s] : gb_seed[s]) + acc[s]) * kScale1;
+            zr[s * 2 * GB_ROWS + row] = (float)(gb_seed[s] + acc[s]) * kScale1;
             zr[s * 2 * GB_ROWS + GB_ROWS + row] = (float)(gb_seedr + accr[s]) * kScale1;
           }
         }
@@ -1702,11 +1336,7 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
       if (active[s]) A.st[s0 + s].gru_a_state[i] = st[s];
   } else {
     /* ======================= sampler role ================================ */
-    const float *ulaw = (const float *)(img + IMG_ULAW);
     const float *logit_tab = (const float *)(img + IMG_LOGIT);
-    const float *fcw = (const float *)(img + IMG_FCW);
-    const float *fcb = (const float *)(img + IMG_FCB);
-    const float *fcf = (const float *)(img + IMG_FCF);
     /* with S=4 a sampler wave carries two streams, one per 32-lane half */
     const int sw = wv - SAMPLE_WAVES;
     const int half = lane >> 5, hl = lane & 31;
@@ -1715,10 +1345,6 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
     const bool samp_w = samp && (S == 4 || half == 0);  /* lanes owning the stream's outputs */
     const int ms = samp ? my_s : 0;
     const bool my_active = samp && s0 + ms < A.nstreams && A.st[s0 + ms].frame_count > FEATURES_DELAY;
-    const int q = hl >> 1, ch2 = lane & 1;
-    const int qq = q < 15 ? q : 0;
-    const int lvl_in = qq == 0 ? 0 : (qq < 3 ? 1 : (qq < 7 ? 2 : 3)); /* level of node qq+1 within 0..3 */
-    const int hb = 32 * half;                                          /* this half's bits in a ballot */
 
     float lsr[NLPC], lpr[NLPC];
     float sbv = 0.f, pred = 0.f, deemph = 0.f;
@@ -1737,26 +1363,20 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
       rz = p->rng[0]; rw = p->rng[1]; rj = p->rng[2]; rc = p->rng[3];
     }
     __syncthreads(); /* image in LDS */
-    /* dual_fc nodes 1..15 (tree levels 0..3) of this lane: registers */
-    float f03w[NB];
-#pragma unroll
-    for (int j = 0; j < NB; j++) f03w[j] = fcw[(qq + 1) * 32 + ch2 * 16 + j];
-    const float f03b = fcb[ch2 * 256 + qq + 1], f03f = fcf[ch2 * 256 + qq + 1];
-    auto pre_sample = [&]() {
-      /* pred and the u-law indices of the next sample (lpcnet.c:252-254) */
-      float p2 = 0.f;
-#pragma unroll
-      for (int j = 0; j < NLPC; j++) p2 = p2 - lsr[j] * lpr[j];
-      pred = p2;
-      const int su = lin2ulaw_x86(lsr[0]);
-      const int pu = lin2ulaw_x86(pred);
-      if (samp_w && hl == 0) *(int4 *)(ix + ms * 4) = make_int4(su, pu, last_exc, 0);
-    };
+    FcLane F;
+    F.init(img, lane);
     if (samp_w && hl < NB) {
       xb[(hl >> 2) * S * 4 + ms * 4 + (hl & 3)] = (unsigned char)quant_s8(sbv);
       sbuf[ms * NB + hl] = sbv;
     }
-    if (samp) pre_sample();
+    if (samp) {
+      /* pred and the u-law indices of the first sample (lpcnet.c:252-254) */
+      float p2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < NLPC; j++) p2 = p2 - lsr[j] * lpr[j];
+      pred = p2;
+      if (samp_w && hl == 0) *(int4 *)(ix + ms * 4) = make_int4(lin2ulaw_x86(lsr[0]), lin2ulaw_x86(pred), last_exc, 0);
+    }
     __syncthreads(); /* initial q(h_A), q(h_B), ix */
     stamp_start();
 
@@ -1832,95 +1452,21 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
         }
       }
       stamp(9);
-      auto node_logit_w = [&](float bias, float factor, const float *w) -> float {
-        float sum = bias;
-#pragma unroll
-        for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
-        float v[1] = {sum};
-        tanh_x86_n<1>(v, rcp);
-        const float vv = factor * v[0];
-        /* sum1 + sum2 (nnet.c:205); adjacent-lane swap through DPP quad_perm [1,0,3,2] */
-        const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(vv), 0xB1, 0xF, 0xF, false));
-        return ch2 ? o + vv : vv + o;
-      };
-      float lg[8];
-      int val = 0;
-      {
-        const float l = node_logit_w(f03b, f03f, f03w);
-        const float t = lvl_in == 0 ? thr[0] : (lvl_in == 1 ? thr[1] : (lvl_in == 2 ? thr[2] : thr[3]));
-        const unsigned long long m = __ballot(t < l) >> hb;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          const int nd = (1 << b) | val;
-          if (tracing) lg[b] = __shfl(l, hb + 2 * (nd - 1));
-          val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
-        }
-      }
-      stamp(10);
-      /* Speculation: with the top 4 bits of exc known, lane c of the half
-       * evaluates candidate exc = 16*val + c (c = lane & 15) -- its output
-       * sample, pred(n+1) and both u-law indices (lpcnet.c:252-254,
-       * 260-261) -- while levels 4..7 of the tree are walked; the walk then
-       * only selects a lane.  Same operations in the same order per candidate. */
       const bool teach = n < A.preload;
-      float sp_pcm = 0.f, sp_pred = 0.f;
-      int sp_idx = 0;
-      if (!teach) {
-        sp_pcm = pred + ulaw[(val << 4) | (hl & 15)];
-        float p2 = 0.f - sp_pcm * lpr[0];
-#pragma unroll
-        for (int j = 1; j < NLPC; j++) p2 = p2 - lsr[j - 1] * lpr[j];
-        sp_pred = p2;
-        sp_idx = lin2ulaw_x86(sp_pcm) | (lin2ulaw_x86(sp_pred) << 8);
-      }
-      {
-        const int lvl = 4 + lvl_in;
-        const int off = qq + 1 - (1 << (lvl - 4));
-        const int node = (1 << lvl) | (val << (lvl - 4)) | off;
-        const float l = node_logit_w(fcb[ch2 * 256 + node], fcf[ch2 * 256 + node], fcw + node * 32 + ch2 * 16);
-        const float t = lvl_in == 0 ? thr[4] : (lvl_in == 1 ? thr[5] : (lvl_in == 2 ? thr[6] : thr[7]));
-        const unsigned long long m = __ballot(t < l) >> hb;
-#pragma unroll
-        for (int b = 4; b < 8; b++) {
-          const int qi = (1 << (b - 4)) - 1 + (val & ((1 << (b - 4)) - 1));
-          if (tracing) lg[b] = __shfl(l, hb + 2 * qi);
-          val = (val << 1) | (int)((m >> (2 * qi)) & 1ull);
-        }
-      }
+      const WalkOut R = dual_fc_walk(F, thr, xv, pred, lsr, lpr, teach, teach ? (float)pcmbuf[s * FRAME + n] : 0.f,
+                                     deemph, tracing);
       stamp(11);
-      int exc = val, su, pu;
-      float pcm, pn;
-      if (teach) {
-        /* teacher forcing (lpcnet.c:256-259) */
-        const float o_in = (float)pcmbuf[s * FRAME + n];
-        const float pd = kPreemph * deemph;
-        exc = lin2ulaw_x86((o_in - pd) - pred);
-        pcm = o_in - pd;
-        float p2 = 0.f - pcm * lpr[0];
-#pragma unroll
-        for (int j = 1; j < NLPC; j++) p2 = p2 - lsr[j - 1] * lpr[j];
-        pn = p2;
-        su = lin2ulaw_x86(pcm);
-        pu = lin2ulaw_x86(pn);
-      } else {
-        const int src = hb + (exc & 15);
-        const int ic = __shfl(sp_idx, src);
-        su = ic & 0xFF;
-        pu = ic >> 8;
-        pcm = __shfl(sp_pcm, src);
-        pn = __shfl(sp_pred, src);
-      }
-      if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + s * 4) = make_int4(su, pu, exc, 0);
+      if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + s * 4) = make_int4(R.su, R.pu, R.exc, 0);
       if (tracing && samp_w && hl < 8 && my_active) {
-        float v = lg[0];
+        float v = R.lg[0];
 #pragma unroll
-        for (int b = 1; b < 8; b++) v = hl == b ? lg[b] : v;
+        for (int b = 1; b < 8; b++) v = hl == b ? R.lg[b] : v;
         A.trace_logits[((size_t)(s0 + s) * A.N + n) * 8 + hl] = v;
       }
-      if (A.trace_exc && samp_w && hl == 0 && my_active) A.trace_exc[(size_t)(s0 + s) * A.N + n] = exc;
-      pend_pcm = pcm;
-      pend_pred = pn;
-      pend_exc = exc;
+      if (A.trace_exc && samp_w && hl == 0 && my_active) A.trace_exc[(size_t)(s0 + s) * A.N + n] = R.exc;
+      pend_pcm = R.pcm;
+      pend_pred = R.pn;
+      pend_exc = R.exc;
       pend_n = n;
       stamp(12);
     }
@@ -1951,34 +1497,27 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
   }
 }
 
-template <int S, bool SAT, bool MF>
+template <int S, bool SAT>
 static int launch_pipe_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
 {
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)pipe_kernel<S, SAT, MF>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
+    if (hipFuncSetAttribute((const void *)pipe_kernel<S, SAT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+        hipSuccess)
       return -1;
     attr_set = true;
   }
   const int grid = (a.nstreams + S - 1) / S;
-  hipLaunchKernelGGL((pipe_kernel<S, SAT, MF>), dim3(grid), dim3(PIPE_THREADS), lds_bytes, stream, a);
+  hipLaunchKernelGGL((pipe_kernel<S, SAT>), dim3(grid), dim3(PIPE_THREADS), lds_bytes, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int S>
-static int launch_pipe_s(const SampleArgs &a, int sat, int mf, int lds_bytes, hipStream_t st)
-{
-  if (mf) return sat ? -1 : launch_pipe_t<S, false, true>(a, lds_bytes, st);
-  return sat ? launch_pipe_t<S, true, false>(a, lds_bytes, st) : launch_pipe_t<S, false, false>(a, lds_bytes, st);
-}
-
-int launch_pipe(const SampleArgs &a, int S, int sat, int mf, int lds_bytes, void *stream)
+int launch_pipe(const SampleArgs &a, int S, int sat, int lds_bytes, void *stream)
 {
   hipStream_t st = (hipStream_t)stream;
-  if (S == 4) return launch_pipe_s<4>(a, sat, mf, lds_bytes, st);
-  if (S == 2) return launch_pipe_s<2>(a, sat, mf, lds_bytes, st);
-  return launch_pipe_s<1>(a, sat, mf, lds_bytes, st);
+  if (S == 4) return sat ? launch_pipe_t<4, true>(a, lds_bytes, st) : launch_pipe_t<4, false>(a, lds_bytes, st);
+  if (S == 2) return sat ? launch_pipe_t<2, true>(a, lds_bytes, st) : launch_pipe_t<2, false>(a, lds_bytes, st);
+  return sat ? launch_pipe_t<1, true>(a, lds_bytes, st) : launch_pipe_t<1, false>(a, lds_bytes, st);
 }
 
 template <int S, int V, bool SAT, bool REG>

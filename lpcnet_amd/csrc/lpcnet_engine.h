@@ -31,24 +31,26 @@ constexpr int STAMP_WAVES = PIPE_WAVES; /* stamps are [workgroup][STAMP_WAVES][1
 constexpr int FRAME_THREADS = 256;
 constexpr int FRAME_STREAMS = 4;    /* streams per frame-network workgroup */
 constexpr int REG_GB = 12;          /* GRU_B input slots per lane: block k = ks + 8*j, j < 12 */
-/* Matrix-core (v_mfma_i32_4x4x4_16b_i8) pipe kernel: per-lane register
- * tables, one u32 word per slot.  Lane l of GRU_A wave w = (row group l/4 of
- * the wave's 64 units, row l%4 of the group): word k of the table holds
+/* Matrix-core kernel (mf_kernel.hip).
+ * GRU_A (v_mfma_i32_4x4x4_16b_i8): per-lane register tables, one u32 word
+ * per slot.  Lane l of GRU_A wave w = (row group l/4 of the wave's 64 units,
+ * row l%4 of the group); word k of the table holds
  *   [0, 16)   z-gate weight rows, slot t  (4 int8 = one row of an 8x4 block)
  *   [16, 32)  r-gate weight rows
- *   [32, 72)  h-gate weight rows
- *   [72, 90)  column-block bytes of those 72 slots (4 per word)
- *   [90, 102) GRU_B input weight rows (row block w, block ks + 8t, ks = l/8)
- *   [102]     GRU_B recurrent weight row (column block ks < 4, else 0)
- *   [103,107) column-block bytes of the 13 GRU_B slots
- * Unused slots hold zero weights and column block 0. */
+ *   [32, 64)  h-gate weight rows
+ *   [64, 80)  column-block bytes of those 64 slots (4 per word)
+ * Unused slots hold zero weights and column block 0.
+ * GRU_B (v_mfma_i32_16x16x64_i8, sampler waves): dense int8 A tiles, lane l
+ * = row 16g + l%16, bytes k = 64kt + 16(l/16) + 0..15: tiles [g*6 + kt]
+ * (input, 3 gates x 6 K tiles) then [18 + g] (recurrent, K = 16 in lanes
+ * 0..15), [MF_GB_TILES][64 lanes] uint4. */
 constexpr int MF_ZMAX = 16;         /* z / r slots per lane */
 constexpr int MF_HMAX = 32;         /* h slots per lane */
 constexpr int MF_GA = 2 * MF_ZMAX + MF_HMAX;
-constexpr int MF_W_GB = MF_GA + MF_GA / 4;
-constexpr int MF_W_GBREC = MF_W_GB + REG_GB;
-constexpr int MF_C_GB = MF_W_GBREC + 1;
-constexpr int MF_LANE_U32 = MF_C_GB + 4 + 1; /* 108 */
+constexpr int MF_LANE_U32 = MF_GA + MF_GA / 4; /* 80 */
+constexpr int MF_GB_TILES = 3 * 6 + 3;
+constexpr int MF_XSTR = 400;        /* LDS bytes per stream of the quantized GRU_A state (stream-major) */
+constexpr int MF_THREADS = 512;     /* 6 GRU_A waves + 2 sampler waves */
 
 /* Per-stream synthesis state in device memory (lpcnet_private.h:28-48). */
 struct alignas(16) StreamState {
@@ -67,6 +69,9 @@ struct alignas(16) StreamState {
   uint32_t rng[4];
   int pad[1];
 };
+
+/* The device rcpps table holds t + kRcpBias (device_math.h rcp_x86_fix). */
+constexpr uint32_t kRcpBias = 127u << 23;
 
 /* Fixed sections of the sample kernel's LDS image (byte offsets). */
 constexpr int IMG_RCP = 0;                       /* 2048 u32 rcpps table */
@@ -115,11 +120,13 @@ struct SampleArgs {
   int ga_K4[SAMPLE_WAVES][3];
   int ga_qoff[SAMPLE_WAVES][3];
   int gb_qoff[GB_ROWS / 8];
-  /* matrix-core path: per-lane register tables [wave][MF_LANE_U32][64 lanes],
-   * 4-slot groups per wave: z/r (padded to a common count), h */
+  /* matrix-core kernel: GRU_A per-lane register tables [wave][MF_LANE_U32][64
+   * lanes], 4-slot groups per wave (z/r padded to a common count, h); GRU_B
+   * A tiles [MF_GB_TILES][64] */
   const uint32_t *mf;
   int mf_nzr[SAMPLE_WAVES];
   int mf_nh[SAMPLE_WAVES];
+  const uint4 *mf_gb;
   const float4 *ga_wf;   /* fp32 variant: GRU_A blocks [chunk][k][64] float4 */
   const float4 *gb_wf;   /* fp32 variant: GRU_B blocks [rb][k][8 rows][2] float4 (in c) */
   const float *gb_recf;  /* fp32 variant: GRU_B recurrent [NB][GB_ROWS] */
@@ -137,12 +144,16 @@ int launch_sample(const SampleArgs &a, int S, int variant, int sat, int reg, int
 /* Wave-per-stream sample kernel (int8 quad layout): nw streams per workgroup. */
 int wave_lds_bytes(int nw, int image_bytes);
 int launch_wave(const SampleArgs &a, int nw, int sat, int lds_bytes, void *stream);
-/* Pipelined int8 kernel: the GRU_A recurrent product of sample n+1 overlaps
- * the sampling of sample n (fixed wave roles).  mf=0: quad LDS layout with
- * v_dot4 (any int8 model); mf=1: both int8 products on the matrix cores from
- * register-resident weights (non-saturating models within MF_* limits). */
-int pipe_lds_bytes(int S, int image_bytes, int mf);
-int launch_pipe(const SampleArgs &a, int S, int sat, int mf, int lds_bytes, void *stream);
+/* Pipelined int8 quad-layout kernel: the GRU_A recurrent product of sample
+ * n+1 overlaps the sampling of sample n (fixed wave roles). */
+int pipe_lds_bytes(int S, int image_bytes);
+int launch_pipe(const SampleArgs &a, int S, int sat, int lds_bytes, void *stream);
+/* Matrix-core kernel (non-saturating int8 models within the MF_* limits):
+ * GRU_A recurrent product on v_mfma_i32_4x4x4_16b_i8 in the GRU_A waves,
+ * GRU_B products on v_mfma_i32_16x16x64_i8 in the sampler waves, two
+ * workgroup barriers per sample. */
+int mf_lds_bytes(int S);
+int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream);
 
 /* Host LPC (lpc_host.cpp). */
 float lpc_from_cepstrum_host(float *lpc, const float *ceps);

@@ -1,0 +1,557 @@
+/*
+ * mf_kernel.hip -- the matrix-core sample kernel: lpcnet_synthesize_tail_impl
+ * (lpcnet.c:235-271) for S <= 4 streams per 512-thread workgroup, persistent
+ * over the N samples of one frame.  Default for non-saturating int8 models.
+ *
+ * Both int8 products run on the matrix cores, from register-resident weights,
+ * with exact int32 accumulation (bit-identical to maddubs/madd whenever no
+ * u8 x s8 pair can saturate int16 -- checked when the model is loaded):
+ *   GRU_A waves 0..5 (thread = unit): the recurrent product of
+ *     compute_sparse_gru (nnet.c:441, sparse_sgemv_accum8x4 vec_avx.h:790-858)
+ *     on v_mfma_i32_4x4x4_16b_i8 -- 16 independent 4x4x4 blocks per
+ *     instruction = 16 row groups x 4 streams of one 8x4-block slot;
+ *   sampler waves 6..7: both GRU_B products of compute_gruB (nnet.c:345-361)
+ *     on v_mfma_i32_16x16x64_i8 -- 3 gate tiles x 6 K tiles plus 3 recurrent
+ *     tiles, dense (zeros where the block-sparse index has no block), all S
+ *     streams as the N columns; each sampler wave computes them redundantly
+ *     and keeps the GRU_B state in registers, so no barrier separates the
+ *     GRU_B step from the sampling.
+ * Per sample n, two workgroup barriers:
+ *   X  ix(n) published: GRU_A waves gather the embedding rows and run the
+ *      GRU_A elementwise step -> q(h_A(n)); samplers: deferred bookkeeping of
+ *      n-1, kiss99 draws
+ *   Y  q(h_A(n)) complete: GRU_A waves: W q(h_A(n)) for sample n+1;
+ *      samplers: GRU_B products + update, dual-FC tree walk -> ix(n+1)
+ * The arithmetic is term for term the reference's (see device_math.h).
+ */
+#include <hip/hip_runtime.h>
+
+#include "device_math.h"
+#include "lpcnet_engine.h"
+#include "sampler.h"
+
+namespace lpcnet_mi355x {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+/* Keep packed offsets packed: without this the compiler hoists every
+ * unpacked 16-bit offset out of the sample loop (one VGPR per slot). */
+template <int N>
+__device__ __forceinline__ void mf_opaque(uint32_t (&o)[N])
+{
+#pragma unroll
+  for (int k = 0; k < N; k++) asm volatile("" : "+v"(o[k]));
+}
+
+/* x word of slot t: the packed 16-bit LDS byte offsets o[t/2] */
+template <int NO>
+__device__ __forceinline__ uint32_t mf_x(const unsigned char *lds, const uint32_t (&o)[NO], int t)
+{
+  return *(const uint32_t *)(lds + ((o[t >> 1] >> (16 * (t & 1))) & 0xFFFF));
+}
+
+/* v_mfma_i32_4x4x4_16b_i8, 16 blocks: block b = lanes 4b..4b+3.
+ * A (src0) lane 4b+m: 4 int8 of row m (= stream m's x quad of the block's
+ * column block); B (src1) lane 4b+n: 4 int8 of column n (= weight row n);
+ * D lane 4b+n, register m: sum over k of A[m][k] B[k][n] (exact int32).
+ * Layout measured on gfx950 (tools/probes/mfma_i8_probe.hip). */
+__device__ __forceinline__ v4i mfma4(uint32_t x, uint32_t w, v4i acc)
+{
+  return __builtin_amdgcn_mfma_i32_4x4x4i8((int)x, (int)w, acc, 0, 0, 0);
+}
+
+/* GRU_A z and r products over ng 4-slot groups (wave-uniform ng): the two
+ * gates interleave (independent accumulators), x words of group g+1 are
+ * read from LDS while the MFMAs of group g run. */
+__device__ __forceinline__ void mf_zr(const unsigned char *lds, const uint32_t (&wz)[MF_ZMAX],
+                                      const uint32_t (&wr)[MF_ZMAX], const uint32_t (&oz)[MF_ZMAX / 2],
+                                      const uint32_t (&orr)[MF_ZMAX / 2], int ng, v4i &az, v4i &ar)
+{
+  uint32_t xz[4], xr[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    xz[k] = mf_x(lds, oz, k);
+    xr[k] = mf_x(lds, orr, k);
+  }
+#pragma unroll
+  for (int g = 0; g < MF_ZMAX / 4; g++) {
+    if (g < ng) {
+      uint32_t nz[4], nr[4];
+      if (g + 1 < MF_ZMAX / 4 && g + 1 < ng) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          nz[k] = mf_x(lds, oz, 4 * (g + 1) + k);
+          nr[k] = mf_x(lds, orr, 4 * (g + 1) + k);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        az = mfma4(xz[k], wz[4 * g + k], az);
+        ar = mfma4(xr[k], wr[4 * g + k], ar);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        xz[k] = nz[k];
+        xr[k] = nr[k];
+      }
+    }
+  }
+}
+
+/* NS-slot product over ng 4-slot groups, alternating two accumulators */
+template <int NS>
+__device__ __forceinline__ void mf_run(const unsigned char *lds, const uint32_t (&w)[NS], const uint32_t (&o)[NS / 2],
+                                       int ng, v4i &a0, v4i &a1)
+{
+  uint32_t x[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) x[k] = mf_x(lds, o, k);
+#pragma unroll
+  for (int g = 0; g < NS / 4; g++) {
+    if (g < ng) {
+      uint32_t n[4];
+      if (g + 1 < NS / 4 && g + 1 < ng) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) n[k] = mf_x(lds, o, 4 * (g + 1) + k);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (k & 1) a1 = mfma4(x[k], w[4 * g + k], a1);
+        else a0 = mfma4(x[k], w[4 * g + k], a0);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) x[k] = n[k];
+    }
+  }
+}
+
+/* v_mfma_i32_16x16x64_i8: A (src0) lane l = row l%16, B (src1) lane l =
+ * column l%16, the 16 bytes of both = k 16(l/16) + 0..15 (any k permutation
+ * common to A and B is the same product); D lane l register i = row
+ * 4(l/16)+i, column l%16 (tools/probes/mfma16_probe.hip). */
+__device__ __forceinline__ v4i mfma16(const v4i &w, const v4i &x, v4i acc)
+{
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(w, x, acc, 0, 0, 0);
+}
+
+template <int S>
+struct MfLds {
+  static constexpr int x = S * MF_XSTR;      /* quantized GRU_A state [S][MF_XSTR] (signed form) */
+  static constexpr int xb = S * NB;          /* quantized GRU_B state [S][16] */
+  static constexpr int sb = S * NB * 4;      /* float GRU_B state [S][16] (tree-walk broadcast) */
+  static constexpr int ix = S * 16;          /* sig/pred/exc indices */
+  static constexpr int pcm = ((S * FRAME * 2 + 15) / 16) * 16;
+  static constexpr int cnd = GA_ROWS * S * 4; /* GRU_A conditioning [3][NA][S] */
+  static constexpr int gbs = S * GB_ROWS * 4; /* GRU_B input accumulator seeds [S][48] */
+  static constexpr int gbr = GB_ROWS * 4;     /* GRU_B recurrent accumulator seeds [48] */
+  static constexpr int total = x + xb + sb + ix + pcm + cnd + gbs + gbr;
+};
+
+int mf_lds_bytes(int S)
+{
+  return IMG_VAR + (S == 4 ? MfLds<4>::total : (S == 2 ? MfLds<2>::total : MfLds<1>::total));
+}
+
+template <int S>
+__global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
+{
+  extern __shared__ uint4 lds4[];
+  unsigned char *lds = (unsigned char *)lds4;
+  using L = MfLds<S>;
+  unsigned char *xa = lds; /* first: every x address fits the 16-bit offsets kept in registers */
+  unsigned char *xb = xa + L::x;
+  float *sbuf = (float *)(xb + L::xb);
+  int *ix = (int *)((unsigned char *)sbuf + L::sb);
+  short *pcmbuf = (short *)((unsigned char *)ix + L::ix);
+  float *cnd = (float *)((unsigned char *)pcmbuf + L::pcm);
+  int *gbs = (int *)((unsigned char *)cnd + L::cnd);
+  int *gbr = gbs + S * GB_ROWS;
+  unsigned char *img = lds + L::total; /* fixed image sections: tables and dual_fc */
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int s0 = blockIdx.x * S;
+  const uint32_t *rcp = (const uint32_t *)(img + IMG_RCP);
+
+  bool active[S];
+  bool any = false;
+  for (int s = 0; s < S; s++) {
+    const int sid = s0 + s;
+    active[s] = sid < A.nstreams && A.st[sid].frame_count > FEATURES_DELAY;
+    any |= active[s];
+  }
+  if (!any) {
+    for (int e = tid; e < S * A.N; e += MF_THREADS) {
+      const int s = e / A.N, n = e % A.N;
+      if (s0 + s < A.nstreams) A.pcm[(size_t)(s0 + s) * A.N + n] = 0;
+    }
+    return;
+  }
+  {
+    uint4 *img4 = (uint4 *)img;
+    for (int o = tid; o < IMG_VAR / 16; o += MF_THREADS) img4[o] = A.image[o];
+  }
+  for (int e = tid; e < S * A.preload; e += MF_THREADS) {
+    const int s = e / A.preload, n = e % A.preload;
+    pcmbuf[s * FRAME + n] = A.pcm[(size_t)min(s0 + s, A.nstreams - 1) * A.N + n];
+  }
+
+  const bool stamping = A.stamps != nullptr;
+  unsigned long long stp[16] = {};
+  unsigned long long t_prev = 0, t_loop0 = 0;
+  auto stamp = [&](int k) {
+    if (stamping) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      stp[k] += t - t_prev;
+      t_prev = t;
+    }
+  };
+  auto stamp_start = [&]() {
+    if (stamping) t_prev = t_loop0 = __builtin_amdgcn_s_memtime();
+  };
+
+  if (wv < SAMPLE_WAVES) {
+    /* ======================= GRU_A role ================================== */
+    const int i = tid;
+    const float bz = A.ga_par[i], br = A.ga_par[NA + i], bh = A.ga_par[2 * NA + i];
+    const float dz = A.ga_par[3 * NA + i], dr = A.ga_par[4 * NA + i], dh = A.ga_par[5 * NA + i];
+    const int wsz = A.ga_wsum[i], wsr = A.ga_wsum[NA + i], wsh = A.ga_wsum[2 * NA + i];
+    float st[S];
+    for (int s = 0; s < S; s++) {
+      const StreamState *p = &A.st[min(s0 + s, A.nstreams - 1)];
+      st[s] = p->gru_a_state[i];
+      cnd[i * S + s] = p->gru_a_cond[i];
+      cnd[(NA + i) * S + s] = p->gru_a_cond[NA + i];
+      cnd[(2 * NA + i) * S + s] = p->gru_a_cond[2 * NA + i];
+    }
+    /* GRU_B accumulator seeds, frame constants (nnet.c:347-356 with the
+     * offset-128 correction): cvt_rne((bias + cond) * SCALE) + 128 rowsum(w) */
+    for (int e = tid; e < S * GB_ROWS; e += SAMPLE_THREADS) {
+      const int s = e / GB_ROWS, r = e % GB_ROWS;
+      gbs[e] = cvt_rne((A.gb_par[r] + A.st[min(s0 + s, A.nstreams - 1)].gru_b_cond[r]) * kScale) + A.gb_wsum[r];
+    }
+    if (tid < GB_ROWS) gbr[tid] = cvt_rne(A.gb_par[GB_ROWS + tid] * kScale) + A.gb_wsum[GB_ROWS + tid];
+    /* this lane's GRU_A weight rows and x offsets, for all N samples */
+    uint32_t wz[MF_ZMAX], wr[MF_ZMAX], wh[MF_HMAX], oz[MF_ZMAX / 2], orr[MF_ZMAX / 2], oh[MF_HMAX / 2];
+    {
+      const uint32_t *mt = A.mf + (size_t)wv * MF_LANE_U32 * 64 + lane;
+#pragma unroll
+      for (int t = 0; t < MF_ZMAX; t++) {
+        wz[t] = mt[t * 64];
+        wr[t] = mt[(MF_ZMAX + t) * 64];
+      }
+#pragma unroll
+      for (int t = 0; t < MF_HMAX; t++) wh[t] = mt[(2 * MF_ZMAX + t) * 64];
+      uint32_t cw[MF_GA / 4];
+#pragma unroll
+      for (int k = 0; k < MF_GA / 4; k++) cw[k] = mt[(MF_GA + k) * 64];
+      /* A operand of lane 4b+m = stream m (lanes m >= S duplicate stream S-1) */
+      const uint32_t mo = (uint32_t)min(lane & 3, S - 1) * MF_XSTR;
+      auto off = [&](int t) -> uint32_t { return ((cw[t >> 2] >> (8 * (t & 3))) & 0xFF) * 4 + mo; };
+#pragma unroll
+      for (int t = 0; t < MF_ZMAX / 2; t++) {
+        oz[t] = off(2 * t) | (off(2 * t + 1) << 16);
+        orr[t] = off(MF_ZMAX + 2 * t) | (off(MF_ZMAX + 2 * t + 1) << 16);
+      }
+#pragma unroll
+      for (int t = 0; t < MF_HMAX / 2; t++) oh[t] = off(2 * MF_ZMAX + 2 * t) | (off(2 * MF_ZMAX + 2 * t + 1) << 16);
+    }
+    const int nzr = A.mf_nzr[wv], nh = A.mf_nh[wv];
+    __syncthreads(); /* image in LDS */
+    for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8(st[s]);
+    __syncthreads(); /* initial q(h_A), q(h_B), ix, seeds */
+    stamp_start();
+
+    /* per-sample terms that depend only on the state and the recurrent sums,
+     * computed right after the recurrent product (off the X->Y critical path):
+     * az/ar, the (subias + diag*state) terms of z and r, and the whole
+     * recurrent h-gate value (nnet.c:431-440) */
+    int az[S], ar[S], ah[S];
+    float tz[S], tr[S], hpre[S];
+    auto recurrent = [&]() {
+      v4i vz = {wsz, wsz, wsz, wsz}, vr = {wsr, wsr, wsr, wsr}, vh0 = {wsh, wsh, wsh, wsh}, vh1 = {0, 0, 0, 0};
+      mf_opaque(oz);
+      mf_opaque(orr);
+      mf_opaque(oh);
+      mf_zr(lds, wz, wr, oz, orr, nzr, vz, vr);
+      mf_run<MF_HMAX>(lds, wh, oh, nh, vh0, vh1);
+      for (int s = 0; s < S; s++) {
+        az[s] = vz[s];
+        ar[s] = vr[s];
+        ah[s] = vh0[s] + vh1[s];
+        tz[s] = bz + dz * st[s];
+        tr[s] = br + dr * st[s];
+        hpre[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
+      }
+    };
+    recurrent();
+    for (int n = 0; n < A.N; n++) {
+      stamp(4);
+      __syncthreads(); /* X */
+      stamp(5);
+      {
+        /* GRU_A input (nnet.c:484-491): all 9*S gathers in flight at once */
+        float e[S][9];
+        for (int s = 0; s < S; s++) {
+          /* the indices are the same in every lane: scalar row addresses */
+          const int4 v = *(const int4 *)(ix + s * 4);
+          const float *e1 = A.emb_sig + (__builtin_amdgcn_readfirstlane(v.x) & 0xFF) * GA_ROWS;
+          const float *e2 = A.emb_pred + (__builtin_amdgcn_readfirstlane(v.y) & 0xFF) * GA_ROWS;
+          const float *e3 = A.emb_exc + (__builtin_amdgcn_readfirstlane(v.z) & 0xFF) * GA_ROWS;
+#pragma unroll
+          for (int g = 0; g < 3; g++) {
+            e[s][g] = e1[g * NA + i];
+            e[s][3 + g] = e2[g * NA + i];
+            e[s][6 + g] = e3[g * NA + i];
+          }
+        }
+        if (stamping) {
+          /* diagnostic only: wait for every gather before the stamp */
+          float g = 0.f;
+          for (int s = 0; s < S; s++)
+#pragma unroll
+            for (int k = 0; k < 9; k++) g += e[s][k];
+          asm volatile("" ::"v"(g));
+          stamp(10);
+        }
+        /* compute_sparse_gru elementwise (nnet.c:431-447) */
+        float zrv[2 * S], hv[S], inh[S];
+        for (int s = 0; s < S; s++) {
+          const float inz = ((cnd[i * S + s] + e[s][0]) + e[s][3]) + e[s][6];
+          const float inr = ((cnd[(NA + i) * S + s] + e[s][1]) + e[s][4]) + e[s][7];
+          inh[s] = ((cnd[(2 * NA + i) * S + s] + e[s][2]) + e[s][5]) + e[s][8];
+          zrv[s] = (float)(az[s] + cvt_rne((tz[s] + inz) * kScale)) * kScale1;
+          zrv[S + s] = (float)(ar[s] + cvt_rne((tr[s] + inr) * kScale)) * kScale1;
+          hv[s] = hpre[s];
+        }
+        sigmoid_x86_n<2 * S>(zrv, rcp);
+        for (int s = 0; s < S; s++) hv[s] = hv[s] * zrv[S + s] + inh[s];
+        tanh_x86_n<S>(hv, rcp);
+        for (int s = 0; s < S; s++) {
+          st[s] = zrv[s] * st[s] + (1.f - zrv[s]) * hv[s];
+          xa[s * MF_XSTR + i] = (unsigned char)quant_s8(st[s]);
+        }
+      }
+      stamp(0);
+      __syncthreads(); /* Y */
+      stamp(1);
+      if (n + 1 < A.N) recurrent(); /* W q(h_A(n)) for sample n+1, beside GRU_B and the sampling of n */
+      stamp(2);
+    }
+    stamp(4);
+    __syncthreads(); /* final */
+    stamp(5);
+    for (int s = 0; s < S; s++)
+      if (active[s]) A.st[s0 + s].gru_a_state[i] = st[s];
+  } else {
+    /* ======================= sampler role ================================ */
+    const float *logit_tab = (const float *)(img + IMG_LOGIT);
+    /* tree walk: with S=4 a sampler wave carries two streams, one per 32-lane half */
+    const int sw = wv - SAMPLE_WAVES;
+    const int half = lane >> 5, hl = lane & 31;
+    const int my_s = S == 4 ? 2 * sw + half : sw;
+    const bool samp = my_s < S;                         /* wave-uniform */
+    const bool samp_w = samp && (S == 4 || half == 0);  /* lanes owning the stream's outputs */
+    const int ms = samp ? my_s : 0;
+    const bool my_active = samp && s0 + ms < A.nstreams && A.st[s0 + ms].frame_count > FEATURES_DELAY;
+    /* GRU_B: lane = (unit quad gq, stream gs, gi): unit gu = 4gq + gi of
+     * stream gs; the MFMA columns are (gs, gi), so D register gi of this lane
+     * holds row 4gq + gi.  gown: stream gs is one of this wave's. */
+    const int gq = lane >> 4, gs = (lane & 15) >> 2, gi = lane & 3, gu = 4 * gq + gi, sl = min(gs, S - 1);
+    const bool gown = gs < S && (S == 4 ? (gs >> 1) : gs) == sw;
+    const bool gact = gown && s0 + gs < A.nstreams && A.st[s0 + gs].frame_count > FEATURES_DELAY;
+
+    float lsr[NLPC], lpr[NLPC];
+    float pred = 0.f, deemph = 0.f;
+    uint32_t rz = 0, rw = 0, rj = 0, rc = 0;
+    int last_exc = 0;
+    {
+      const StreamState *p = &A.st[min(s0 + ms, A.nstreams - 1)];
+#pragma unroll
+      for (int j = 0; j < NLPC; j++) {
+        lsr[j] = p->last_sig[j];
+        lpr[j] = p->lpc[j];
+      }
+      deemph = p->deemph_mem;
+      last_exc = p->last_exc;
+      rz = p->rng[0]; rw = p->rng[1]; rj = p->rng[2]; rc = p->rng[3];
+    }
+    float sbv = A.st[min(s0 + sl, A.nstreams - 1)].gru_b_state[gu];
+    v4i wt[MF_GB_TILES];
+#pragma unroll
+    for (int t = 0; t < MF_GB_TILES; t++) {
+      const uint4 u = A.mf_gb[t * 64 + lane];
+      wt[t] = v4i{(int)u.x, (int)u.y, (int)u.z, (int)u.w};
+    }
+    auto put_xb = [&]() {
+      if (gown) xb[gs * NB + gu] = (unsigned char)quant_s8(sbv);
+    };
+    auto pick = [&](const v4i &a) -> int { return gi == 0 ? a[0] : (gi == 1 ? a[1] : (gi == 2 ? a[2] : a[3])); };
+    __syncthreads(); /* image in LDS */
+    FcLane F;
+    F.init(img, lane);
+    put_xb();
+    if (samp) {
+      /* pred and the u-law indices of the first sample (lpcnet.c:252-254) */
+      float p2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < NLPC; j++) p2 = p2 - lsr[j] * lpr[j];
+      pred = p2;
+      if (samp_w && hl == 0) *(int4 *)(ix + ms * 4) = make_int4(lin2ulaw_x86(lsr[0]), lin2ulaw_x86(pred), last_exc, 0);
+    }
+    __syncthreads(); /* initial q(h_A), q(h_B), ix, seeds */
+    stamp_start();
+    /* the sampler chain is the per-sample critical path; the GRU_A waves
+     * sharing these SIMDs have slack: issue the samplers' instructions first */
+    __builtin_amdgcn_s_setprio(3);
+
+    float thr[8];
+    const bool tracing = A.trace_logits != nullptr;
+    /* bookkeeping of sample n deferred into the X->Y interval of n+1 */
+    float pend_pcm = 0.f, pend_pred = 0.f;
+    int pend_exc = 0, pend_n = -1;
+    auto finish = [&]() {
+      if (pend_n < 0) return;
+#pragma unroll
+      for (int j = NLPC - 1; j > 0; j--) lsr[j] = lsr[j - 1];
+      lsr[0] = pend_pcm;
+      last_exc = pend_exc;
+      pred = pend_pred;
+      float o = pend_pcm + kPreemph * deemph;
+      deemph = o;
+      if (o < -32767) o = -32767;
+      if (o > 32767) o = 32767;
+      if (samp_w && hl == 0 && pend_n >= A.preload) pcmbuf[ms * FRAME + pend_n] = (short)round_half_up(o);
+      put_xb();
+      pend_n = -1;
+    };
+    for (int n = 0; n < A.N; n++) {
+      stamp(4);
+      __syncthreads(); /* X */
+      stamp(5);
+      v4i acc[3], accr[3];
+      if (samp) {
+        finish();
+        stamp(13);
+        /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
+        const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
+        const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          thr[b] = logit_tab[(r0 >> (8 * b)) & 0xFF];
+          thr[b + 4] = logit_tab[(r1 >> (8 * b)) & 0xFF];
+        }
+        /* GRU_B recurrent product (nnet.c:355-361) needs only q(h_B(n-1)):
+         * before barrier Y.  Seeds are the accumulator inputs. */
+        const v4i xr = *(const v4i *)(xb + sl * NB);
+#pragma unroll
+        for (int g = 0; g < 3; g++) {
+          acc[g] = *(const v4i *)(gbs + sl * GB_ROWS + 16 * g + 4 * gq);
+          accr[g] = *(const v4i *)(gbr + 16 * g + 4 * gq);
+        }
+#pragma unroll
+        for (int g = 0; g < 3; g++) accr[g] = mfma16(wt[18 + g], xr, accr[g]);
+      }
+      stamp(0);
+      __syncthreads(); /* Y */
+      stamp(1);
+      if (!samp) continue;
+      {
+        /* GRU_B input product (nnet.c:345-353), 48 x 384, all S streams */
+        v4i xk[6];
+#pragma unroll
+        for (int kt = 0; kt < 6; kt++) xk[kt] = *(const v4i *)(xa + sl * MF_XSTR + 64 * kt + 16 * gq);
+#pragma unroll
+        for (int kt = 0; kt < 6; kt++)
+#pragma unroll
+          for (int g = 0; g < 3; g++) acc[g] = mfma16(wt[g * 6 + kt], xk[kt], acc[g]);
+        stamp(10);
+        /* GRU_B elementwise (nnet.c:362-371), unit gu of stream sl */
+        float zrb[2] = {(float)pick(acc[0]) * kScale1 + (float)pick(accr[0]) * kScale1,
+                        (float)pick(acc[1]) * kScale1 + (float)pick(accr[1]) * kScale1};
+        sigmoid_x86_n<2>(zrb, rcp);
+        float hh[1] = {(float)pick(acc[2]) * kScale1 + ((float)pick(accr[2]) * kScale1) * zrb[1]};
+        stamp(14);
+        tanh_x86_n<1>(hh, rcp);
+        sbv = zrb[0] * sbv + (1.f - zrb[0]) * hh[0];
+        if (gown) sbuf[gs * NB + gu] = sbv;
+      }
+      stamp(8);
+      /* same-wave LDS exchange: the half of stream ms reads its 16 GRU_B units */
+      __builtin_amdgcn_wave_barrier();
+      float xv[NB];
+      {
+        const float4 *b4 = (const float4 *)(sbuf + ms * NB);
+#pragma unroll
+        for (int j = 0; j < NB / 4; j++) {
+          const float4 v = b4[j];
+          xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
+        }
+      }
+      stamp(9);
+      const bool teach = n < A.preload;
+      const WalkOut R = dual_fc_walk(F, thr, xv, pred, lsr, lpr, teach, teach ? (float)pcmbuf[ms * FRAME + n] : 0.f,
+                                     deemph, tracing);
+      stamp(11);
+      if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + ms * 4) = make_int4(R.su, R.pu, R.exc, 0);
+      if (tracing && samp_w && hl < 8 && my_active) {
+        float v = R.lg[0];
+#pragma unroll
+        for (int b = 1; b < 8; b++) v = hl == b ? R.lg[b] : v;
+        A.trace_logits[((size_t)(s0 + ms) * A.N + n) * 8 + hl] = v;
+      }
+      if (A.trace_exc && samp_w && hl == 0 && my_active) A.trace_exc[(size_t)(s0 + ms) * A.N + n] = R.exc;
+      pend_pcm = R.pcm;
+      pend_pred = R.pn;
+      pend_exc = R.exc;
+      pend_n = n;
+      stamp(12);
+    }
+    if (samp) finish();
+    stamp(4);
+    __syncthreads(); /* final */
+    stamp(5);
+    if (samp_w && my_active && hl == 0) {
+      StreamState *p = &A.st[s0 + ms];
+#pragma unroll
+      for (int j = 0; j < NLPC; j++) p->last_sig[j] = lsr[j];
+      p->deemph_mem = deemph;
+      p->last_exc = last_exc;
+      p->rng[0] = rz; p->rng[1] = rw; p->rng[2] = rj; p->rng[3] = rc;
+    }
+    if (gact) A.st[s0 + gs].gru_b_state[gu] = sbv;
+  }
+  if (stamping && lane == 0) {
+    stp[6] = __builtin_amdgcn_s_memtime() - t_loop0;
+    stp[7] = (unsigned long long)A.N;
+    for (int k = 0; k < 16; k++) A.stamps[((size_t)blockIdx.x * STAMP_WAVES + wv) * 16 + k] = stp[k];
+  }
+  for (int e = tid; e < S * A.N; e += MF_THREADS) {
+    const int s = e / A.N, n = e % A.N;
+    if (s0 + s < A.nstreams) A.pcm[(size_t)(s0 + s) * A.N + n] = active[s] ? pcmbuf[s * FRAME + n] : (short)0;
+  }
+}
+
+template <int S>
+static int launch_mf_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
+{
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void *)mf_kernel<S>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+        hipSuccess)
+      return -1;
+    attr_set = true;
+  }
+  const int grid = (a.nstreams + S - 1) / S;
+  hipLaunchKernelGGL((mf_kernel<S>), dim3(grid), dim3(MF_THREADS), lds_bytes, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream)
+{
+  hipStream_t st = (hipStream_t)stream;
+  if (S == 4) return launch_mf_t<4>(a, lds_bytes, st);
+  if (S == 2) return launch_mf_t<2>(a, lds_bytes, st);
+  return launch_mf_t<1>(a, lds_bytes, st);
+}
+
+}  // namespace lpcnet_mi355x

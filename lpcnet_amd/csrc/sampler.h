@@ -1,0 +1,141 @@
+/*
+ * sampler.h -- dual-FC tree sampling of one output sample (sample_mdense,
+ * nnet.c:163-214) and the next sample's indices (lpcnet.c:252-261), for one
+ * stream per 32-lane half-wave.  Shared by the pipelined sample kernels.
+ *
+ * Lane hl of a half evaluates (node qq+1, channel ch2) of tree levels 0..3
+ * (qq = hl/2 < 15), then the node of levels 4..7 under the chosen 4-bit
+ * prefix.  While levels 4..7 are walked, lane c = hl & 15 speculatively
+ * evaluates candidate exc = 16*prefix + c: its output sample, pred(n+1) and
+ * both u-law indices -- the same operations in the same order as the
+ * reference, so the walk then only selects a lane.
+ */
+#ifndef LPCNET_SAMPLER_H
+#define LPCNET_SAMPLER_H
+
+#include "device_math.h"
+
+namespace lpcnet_mi355x {
+
+struct FcLane {
+  const uint32_t *rcp;
+  const float *ulaw, *fcw, *fcb, *fcf;
+  float w03[NB];   /* weights of this lane's level 0..3 node and channel (registers) */
+  float b03, f03;
+  int qq, lvl_in, ch2, hb, half, hl;
+
+  __device__ __forceinline__ void init(const unsigned char *img, int lane)
+  {
+    rcp = (const uint32_t *)(img + IMG_RCP);
+    ulaw = (const float *)(img + IMG_ULAW);
+    fcw = (const float *)(img + IMG_FCW);
+    fcb = (const float *)(img + IMG_FCB);
+    fcf = (const float *)(img + IMG_FCF);
+    half = lane >> 5;
+    hl = lane & 31;
+    hb = 32 * half;
+    ch2 = lane & 1;
+    const int q = hl >> 1;
+    qq = q < 15 ? q : 0;
+    lvl_in = qq == 0 ? 0 : (qq < 3 ? 1 : (qq < 7 ? 2 : 3)); /* level of node qq+1 within 0..3 */
+#pragma unroll
+    for (int j = 0; j < NB; j++) w03[j] = fcw[(qq + 1) * 32 + ch2 * 16 + j];
+    b03 = fcb[ch2 * 256 + qq + 1];
+    f03 = fcf[ch2 * 256 + qq + 1];
+  }
+
+  /* factor*tanh(bias + w.x) of this lane, plus the other channel's term
+   * (nnet.c:196-205: sum1 + sum2 through DPP quad_perm [1,0,3,2]) */
+  __device__ __forceinline__ float node_logit(float bias, float factor, const float *w, const float (&xv)[NB]) const
+  {
+    float sum = bias;
+#pragma unroll
+    for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
+    float v[1] = {sum};
+    tanh_x86_n<1>(v, rcp);
+    const float vv = factor * v[0];
+    const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(vv), 0xB1, 0xF, 0xF, false));
+    return ch2 ? o + vv : vv + o;
+  }
+};
+
+/* Result of one sample: excitation, output before de-emphasis, pred(n+1),
+ * u-law indices of the next sample (lpcnet.c:252-261) and, when tracing,
+ * the 8 pre-sampling logits along the path. */
+struct WalkOut {
+  int exc, su, pu;
+  float pcm, pn;
+  float lg[8];
+};
+
+/* One sample of stream (half): thr = the 8 logit thresholds of this
+ * sample's two kiss99 draws, xv = GRU_B state, pred = pred(n), lsr/lpr =
+ * LPC history and coefficients.  teach: teacher forcing with input o_in
+ * (lpcnet.c:256-259).  Uniform per half. */
+__device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, const float (&thr)[8], const float (&xv)[NB], float pred,
+                                                const float (&lsr)[NLPC], const float (&lpr)[NLPC], bool teach,
+                                                float o_in, float deemph, bool tracing)
+{
+  WalkOut R;
+  int val = 0;
+  {
+    const float l = F.node_logit(F.b03, F.f03, F.w03, xv);
+    const float t = F.lvl_in == 0 ? thr[0] : (F.lvl_in == 1 ? thr[1] : (F.lvl_in == 2 ? thr[2] : thr[3]));
+    const unsigned long long m = __ballot(t < l) >> F.hb;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int nd = (1 << b) | val;
+      if (tracing) R.lg[b] = __shfl(l, F.hb + 2 * (nd - 1));
+      val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
+    }
+  }
+  float sp_pcm = 0.f, sp_pred = 0.f;
+  int sp_idx = 0;
+  if (!teach) {
+    sp_pcm = pred + F.ulaw[(val << 4) | (F.hl & 15)];
+    float p2 = 0.f - sp_pcm * lpr[0];
+#pragma unroll
+    for (int j = 1; j < NLPC; j++) p2 = p2 - lsr[j - 1] * lpr[j];
+    sp_pred = p2;
+    sp_idx = lin2ulaw_x86(sp_pcm) | (lin2ulaw_x86(sp_pred) << 8);
+  }
+  {
+    const int lvl = 4 + F.lvl_in;
+    const int off = F.qq + 1 - (1 << (lvl - 4));
+    const int node = (1 << lvl) | (val << (lvl - 4)) | off;
+    const float l = F.node_logit(F.fcb[F.ch2 * 256 + node], F.fcf[F.ch2 * 256 + node], F.fcw + node * 32 + F.ch2 * 16, xv);
+    const float t = F.lvl_in == 0 ? thr[4] : (F.lvl_in == 1 ? thr[5] : (F.lvl_in == 2 ? thr[6] : thr[7]));
+    const unsigned long long m = __ballot(t < l) >> F.hb;
+#pragma unroll
+    for (int b = 4; b < 8; b++) {
+      const int qi = (1 << (b - 4)) - 1 + (val & ((1 << (b - 4)) - 1));
+      if (tracing) R.lg[b] = __shfl(l, F.hb + 2 * qi);
+      val = (val << 1) | (int)((m >> (2 * qi)) & 1ull);
+    }
+  }
+  R.exc = val;
+  if (teach) {
+    /* teacher forcing (lpcnet.c:256-259) */
+    const float pd = kPreemph * deemph;
+    R.exc = lin2ulaw_x86((o_in - pd) - pred);
+    R.pcm = o_in - pd;
+    float p2 = 0.f - R.pcm * lpr[0];
+#pragma unroll
+    for (int j = 1; j < NLPC; j++) p2 = p2 - lsr[j - 1] * lpr[j];
+    R.pn = p2;
+    R.su = lin2ulaw_x86(R.pcm);
+    R.pu = lin2ulaw_x86(R.pn);
+  } else {
+    const int src = F.hb + (R.exc & 15);
+    const int ic = __shfl(sp_idx, src);
+    R.su = ic & 0xFF;
+    R.pu = ic >> 8;
+    R.pcm = __shfl(sp_pcm, src);
+    R.pn = __shfl(sp_pred, src);
+  }
+  return R;
+}
+
+}  // namespace lpcnet_mi355x
+
+#endif

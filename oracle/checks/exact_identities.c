@@ -14,7 +14,10 @@
  *      ldexp(table[m], 127 - e) flushed to +0 below 2^-126 equals the
  *      general emulation (sign | table mantissa | rebiased exponent, 0 for
  *      denormal results, 0 for +inf) for every such finite or infinite den
- *      (argv[1] = the 2048-entry table, tests/golden/rcp_x86.bin).
+ *      (argv[1] = the 2048-entry table, tests/golden/rcp_x86.bin);
+ *  (5) the integer form of (4) the kernels use: q = (table[m] + (127 << 23))
+ *      - (bits(den) & 0x7f800000) as int32, +0 when q < 2^23, for the same
+ *      den range.
  * Build: gcc -O2 -ffp-contract=off exact_identities.c -lm; exit status 0 = all hold. */
 #include <math.h>
 #include <stdint.h>
@@ -70,8 +73,12 @@ int main(int argc, char **argv)
       float q = ldexpf(f_of(t), 127 - e);
       q = q < 0x1p-126f ? 0.f : q;
       if (r != u_of(q)) bad4++;
+      /* integer form */
+      const int32_t qi = (int32_t)((t + (127u << 23)) - (u & 0x7f800000u));
+      const uint32_t r5 = qi < 0x00800000 ? 0u : (uint32_t)qi;
+      if (r5 != u_of(q)) bad4++;
     }
-    printf("rcp pade: %llu mismatches\n", bad4);
+    printf("rcp pade (ldexp and integer forms): %llu mismatches\n", bad4);
   }
   return (bad || bad2 || bad3 || bad4) ? 1 : 0;
 }

@@ -11,7 +11,8 @@ sys.path.insert(0, ROOT)
 import lpcnet_amd as L  # noqa: E402
 
 NAMES = {1: ["B(gru_a)", "wait1", "C(gru_b)", "wait2", "F(sample)", "wait3"],
-         3: ["X->Y", "waitY", "Y->Z", "waitZ", "Z->X", "waitX"]}
+         3: ["X->Y", "waitY", "Y->Z", "waitZ", "Z->X", "waitX"],
+         4: ["X->Y", "waitY", "Y->X", "-", "rest", "waitX"]}
 
 
 def profile(B, variant=0, kernel=1):
@@ -28,17 +29,19 @@ def profile(B, variant=0, kernel=1):
     n = max(st[:, :, 7].max(), 1)
     per = st / n  # cycles per sample
     info = b.info()
-    k = 3 if info.quad_path in (3, 4) else 1
+    k = {3: 3, 4: 4}.get(info.quad_path, 1)
     print(f"B={B} variant={variant} kernel={info.kernel_name} groups={st.shape[0]}")
     for w in range(8):
         row = per[:, w, :].mean(0)
         if row[6] == 0:
             continue
         print(f"  wave {w}: " + " ".join(f"{NAMES[k][j]}={row[j]:7.0f}" for j in range(6)) + f"  loop={row[6]:7.0f}")
-    if k == 3:
+    if k == 4:
+        print("  GRU_A X->Y gathers (to last arrival): " + " ".join("w%d=%.0f" % (w, per[:, w, 10].mean()) for w in range(6)))
+    if k in (3, 4):
         row = per[:, 6, :].mean(0)
-        print("  sampler detail (wave 6): Z->X gru_b=%.0f bcast=%.0f lvl0-3=%.0f lvl4-7+spec=%.0f select=%.0f | X->Y finish=%.0f" %
-              tuple(row[8:14]))
+        print("  sampler detail (wave 6): gru_b=%.0f [mfma %.0f sig %.0f tanh+ %.0f] bcast=%.0f walk=%.0f post=%.0f | X->Y finish=%.0f" %
+              (row[8] + row[10] + row[14], row[10], row[14], row[8], row[9], row[11], row[12], row[13]))
     if k == 1:
         row = per[:, 0, :].mean(0)
         print("  F detail (wave 0): gru_b=%.0f bcast=%.0f lvl0-3=%.0f lvl4-7=%.0f out=%.0f pre=%.0f" %
