@@ -107,9 +107,9 @@ class ModelInfo(C.Structure):
         if self.quad_path == 2:
             return f"wave_kernel<{self.streams_per_workgroup}, {sat}>"
         if self.quad_path == 3:
-            return f"pipe_kernel<{self.streams_per_workgroup}, {sat}>"
+            return f"pipe_kernel<{self.streams_per_workgroup}, {sat}, false>"
         if self.quad_path == 4:
-            return f"mf_kernel<{self.streams_per_workgroup}>"
+            return f"mf_kernel<{self.streams_per_workgroup}, false>"
         quad = "true" if self.quad_path == 1 else "false"
         return f"sample_kernel<{self.streams_per_workgroup}, {self.variant}, {sat}, {quad}>"
 

@@ -1166,7 +1166,7 @@ int pipe_lds_bytes(int S, int image_bytes)
   return image_bytes + (S == 4 ? PipeLds<4>::total : (S == 2 ? PipeLds<2>::total : PipeLds<1>::total));
 }
 
-template <int S, bool SAT>
+template <int S, bool SAT, bool TRACE>
 __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
 {
   extern __shared__ uint4 lds4[];
@@ -1380,8 +1380,8 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
     __syncthreads(); /* initial q(h_A), q(h_B), ix */
     stamp_start();
 
-    float thr[8];
-    const bool tracing = A.trace_logits != nullptr;
+    float t03 = 0.f, t47 = 0.f;
+    constexpr bool tracing = TRACE;
     /* Bookkeeping of sample n (lpcnet.c:260-270: LPC history shift,
      * de-emphasis, output, q(h_B)) is deferred into the X->Y interval of
      * sample n+1, where the sampler waves are otherwise idle; only the next
@@ -1413,11 +1413,7 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
         /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
         const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
         const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          thr[b] = logit_tab[(r0 >> (8 * b)) & 0xFF];
-          thr[b + 4] = logit_tab[(r1 >> (8 * b)) & 0xFF];
-        }
+        lane_thresholds(F, logit_tab, r0, r1, t03, t47);
       }
       stamp(0);
       __syncthreads(); /* Y */
@@ -1452,9 +1448,8 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
         }
       }
       stamp(9);
-      const bool teach = n < A.preload;
-      const WalkOut R = dual_fc_walk(F, thr, xv, pred, lsr, lpr, teach, teach ? (float)pcmbuf[s * FRAME + n] : 0.f,
-                                     deemph, tracing);
+      const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + s * FRAME + n : nullptr,
+                                            deemph);
       stamp(11);
       if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + s * 4) = make_int4(R.su, R.pu, R.exc, 0);
       if (tracing && samp_w && hl < 8 && my_active) {
@@ -1497,27 +1492,33 @@ __global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
   }
 }
 
-template <int S, bool SAT>
+template <int S, bool SAT, bool TRACE>
 static int launch_pipe_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
 {
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)pipe_kernel<S, SAT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-        hipSuccess)
+    if (hipFuncSetAttribute((const void *)pipe_kernel<S, SAT, TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
       return -1;
     attr_set = true;
   }
   const int grid = (a.nstreams + S - 1) / S;
-  hipLaunchKernelGGL((pipe_kernel<S, SAT>), dim3(grid), dim3(PIPE_THREADS), lds_bytes, stream, a);
+  hipLaunchKernelGGL((pipe_kernel<S, SAT, TRACE>), dim3(grid), dim3(PIPE_THREADS), lds_bytes, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <int S, bool SAT>
+static int launch_pipe_s(const SampleArgs &a, int lds_bytes, hipStream_t st)
+{
+  return a.trace_logits ? launch_pipe_t<S, SAT, true>(a, lds_bytes, st) : launch_pipe_t<S, SAT, false>(a, lds_bytes, st);
 }
 
 int launch_pipe(const SampleArgs &a, int S, int sat, int lds_bytes, void *stream)
 {
   hipStream_t st = (hipStream_t)stream;
-  if (S == 4) return sat ? launch_pipe_t<4, true>(a, lds_bytes, st) : launch_pipe_t<4, false>(a, lds_bytes, st);
-  if (S == 2) return sat ? launch_pipe_t<2, true>(a, lds_bytes, st) : launch_pipe_t<2, false>(a, lds_bytes, st);
-  return sat ? launch_pipe_t<1, true>(a, lds_bytes, st) : launch_pipe_t<1, false>(a, lds_bytes, st);
+  if (S == 4) return sat ? launch_pipe_s<4, true>(a, lds_bytes, st) : launch_pipe_s<4, false>(a, lds_bytes, st);
+  if (S == 2) return sat ? launch_pipe_s<2, true>(a, lds_bytes, st) : launch_pipe_s<2, false>(a, lds_bytes, st);
+  return sat ? launch_pipe_s<1, true>(a, lds_bytes, st) : launch_pipe_s<1, false>(a, lds_bytes, st);
 }
 
 template <int S, int V, bool SAT, bool REG>

@@ -152,7 +152,7 @@ int mf_lds_bytes(int S)
   return IMG_VAR + (S == 4 ? MfLds<4>::total : (S == 2 ? MfLds<2>::total : MfLds<1>::total));
 }
 
-template <int S>
+template <int S, bool TRACE>
 __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
 {
   extern __shared__ uint4 lds4[];
@@ -404,8 +404,8 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
      * sharing these SIMDs have slack: issue the samplers' instructions first */
     __builtin_amdgcn_s_setprio(3);
 
-    float thr[8];
-    const bool tracing = A.trace_logits != nullptr;
+    float t03 = 0.f, t47 = 0.f;
+    constexpr bool tracing = TRACE;
     /* bookkeeping of sample n deferred into the X->Y interval of n+1 */
     float pend_pcm = 0.f, pend_pred = 0.f;
     int pend_exc = 0, pend_n = -1;
@@ -435,11 +435,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
         const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
         const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          thr[b] = logit_tab[(r0 >> (8 * b)) & 0xFF];
-          thr[b + 4] = logit_tab[(r1 >> (8 * b)) & 0xFF];
-        }
+        lane_thresholds(F, logit_tab, r0, r1, t03, t47);
         /* GRU_B recurrent product (nnet.c:355-361) needs only q(h_B(n-1)):
          * before barrier Y.  Seeds are the accumulator inputs. */
         const v4i xr = *(const v4i *)(xb + sl * NB);
@@ -460,10 +456,13 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         v4i xk[6];
 #pragma unroll
         for (int kt = 0; kt < 6; kt++) xk[kt] = *(const v4i *)(xa + sl * MF_XSTR + 64 * kt + 16 * gq);
+        /* z and r tiles first: their sigmoids overlap the h tile's MFMAs */
 #pragma unroll
         for (int kt = 0; kt < 6; kt++)
 #pragma unroll
-          for (int g = 0; g < 3; g++) acc[g] = mfma16(wt[g * 6 + kt], xk[kt], acc[g]);
+          for (int g = 0; g < 2; g++) acc[g] = mfma16(wt[g * 6 + kt], xk[kt], acc[g]);
+#pragma unroll
+        for (int kt = 0; kt < 6; kt++) acc[2] = mfma16(wt[12 + kt], xk[kt], acc[2]);
         stamp(10);
         /* GRU_B elementwise (nnet.c:362-371), unit gu of stream sl */
         float zrb[2] = {(float)pick(acc[0]) * kScale1 + (float)pick(accr[0]) * kScale1,
@@ -488,9 +487,8 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         }
       }
       stamp(9);
-      const bool teach = n < A.preload;
-      const WalkOut R = dual_fc_walk(F, thr, xv, pred, lsr, lpr, teach, teach ? (float)pcmbuf[ms * FRAME + n] : 0.f,
-                                     deemph, tracing);
+      const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
+                                            deemph);
       stamp(11);
       if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + ms * 4) = make_int4(R.su, R.pu, R.exc, 0);
       if (tracing && samp_w && hl < 8 && my_active) {
@@ -531,27 +529,33 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   }
 }
 
-template <int S>
+template <int S, bool TRACE>
 static int launch_mf_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
 {
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)mf_kernel<S>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+    if (hipFuncSetAttribute((const void *)mf_kernel<S, TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
         hipSuccess)
       return -1;
     attr_set = true;
   }
   const int grid = (a.nstreams + S - 1) / S;
-  hipLaunchKernelGGL((mf_kernel<S>), dim3(grid), dim3(MF_THREADS), lds_bytes, stream, a);
+  hipLaunchKernelGGL((mf_kernel<S, TRACE>), dim3(grid), dim3(MF_THREADS), lds_bytes, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <int S>
+static int launch_mf_s(const SampleArgs &a, int lds_bytes, hipStream_t st)
+{
+  return a.trace_logits ? launch_mf_t<S, true>(a, lds_bytes, st) : launch_mf_t<S, false>(a, lds_bytes, st);
 }
 
 int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream)
 {
   hipStream_t st = (hipStream_t)stream;
-  if (S == 4) return launch_mf_t<4>(a, lds_bytes, st);
-  if (S == 2) return launch_mf_t<2>(a, lds_bytes, st);
-  return launch_mf_t<1>(a, lds_bytes, st);
+  if (S == 4) return launch_mf_s<4>(a, lds_bytes, st);
+  if (S == 2) return launch_mf_s<2>(a, lds_bytes, st);
+  return launch_mf_s<1>(a, lds_bytes, st);
 }
 
 }  // namespace lpcnet_mi355x

@@ -68,30 +68,42 @@ struct WalkOut {
   float lg[8];
 };
 
-/* One sample of stream (half): thr = the 8 logit thresholds of this
- * sample's two kiss99 draws, xv = GRU_B state, pred = pred(n), lsr/lpr =
- * LPC history and coefficients.  teach: teacher forcing with input o_in
- * (lpcnet.c:256-259).  Uniform per half. */
-__device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, const float (&thr)[8], const float (&xv)[NB], float pred,
-                                                const float (&lsr)[NLPC], const float (&lpr)[NLPC], bool teach,
-                                                float o_in, float deemph, bool tracing)
+/* The two thresholds a lane compares against (its node's level within
+ * levels 0..3 and 4..7): thr = logit_table[byte] of this sample's two
+ * kiss99 draws (nnet.c:178-184).  Off the critical path: called when the
+ * draws are made. */
+__device__ __forceinline__ void lane_thresholds(const FcLane &F, const float *logit_tab, uint32_t r0, uint32_t r1,
+                                                float &t03, float &t47)
+{
+  t03 = logit_tab[(r0 >> (8 * F.lvl_in)) & 0xFF];
+  t47 = logit_tab[(r1 >> (8 * F.lvl_in)) & 0xFF];
+}
+
+/* One sample of stream (half): t03/t47 = this lane's thresholds
+ * (lane_thresholds), xv = GRU_B state, pred = pred(n), lsr/lpr = LPC
+ * history and coefficients.  teach != nullptr: teacher forcing with input
+ * *teach (lpcnet.c:256-259).  Uniform per half.  TRACE: also return the
+ * 8 logits along the path. */
+template <bool TRACE>
+__device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, float t47, const float (&xv)[NB], float pred,
+                                                const float (&lsr)[NLPC], const float (&lpr)[NLPC], const short *teach,
+                                                float deemph)
 {
   WalkOut R;
   int val = 0;
   {
     const float l = F.node_logit(F.b03, F.f03, F.w03, xv);
-    const float t = F.lvl_in == 0 ? thr[0] : (F.lvl_in == 1 ? thr[1] : (F.lvl_in == 2 ? thr[2] : thr[3]));
-    const unsigned long long m = __ballot(t < l) >> F.hb;
+    const unsigned long long m = __ballot(t03 < l) >> F.hb;
 #pragma unroll
     for (int b = 0; b < 4; b++) {
       const int nd = (1 << b) | val;
-      if (tracing) R.lg[b] = __shfl(l, F.hb + 2 * (nd - 1));
+      if (TRACE) R.lg[b] = __shfl(l, F.hb + 2 * (nd - 1));
       val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
     }
   }
   float sp_pcm = 0.f, sp_pred = 0.f;
   int sp_idx = 0;
-  if (!teach) {
+  if (teach == nullptr) {
     sp_pcm = pred + F.ulaw[(val << 4) | (F.hl & 15)];
     float p2 = 0.f - sp_pcm * lpr[0];
 #pragma unroll
@@ -104,18 +116,18 @@ __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, const float (&t
     const int off = F.qq + 1 - (1 << (lvl - 4));
     const int node = (1 << lvl) | (val << (lvl - 4)) | off;
     const float l = F.node_logit(F.fcb[F.ch2 * 256 + node], F.fcf[F.ch2 * 256 + node], F.fcw + node * 32 + F.ch2 * 16, xv);
-    const float t = F.lvl_in == 0 ? thr[4] : (F.lvl_in == 1 ? thr[5] : (F.lvl_in == 2 ? thr[6] : thr[7]));
-    const unsigned long long m = __ballot(t < l) >> F.hb;
+    const unsigned long long m = __ballot(t47 < l) >> F.hb;
 #pragma unroll
     for (int b = 4; b < 8; b++) {
       const int qi = (1 << (b - 4)) - 1 + (val & ((1 << (b - 4)) - 1));
-      if (tracing) R.lg[b] = __shfl(l, F.hb + 2 * qi);
+      if (TRACE) R.lg[b] = __shfl(l, F.hb + 2 * qi);
       val = (val << 1) | (int)((m >> (2 * qi)) & 1ull);
     }
   }
   R.exc = val;
-  if (teach) {
+  if (teach != nullptr) {
     /* teacher forcing (lpcnet.c:256-259) */
+    const float o_in = (float)*teach;
     const float pd = kPreemph * deemph;
     R.exc = lin2ulaw_x86((o_in - pd) - pred);
     R.pcm = o_in - pd;
