@@ -112,6 +112,10 @@ LPCNET_EXPORT int lpcnet_batch_get_trace(LPCNetBatch *b, float *logits, int *exc
  * [4] Z->X work, [5] wait per wave).  Returns #workgroups. */
 LPCNET_EXPORT int lpcnet_batch_set_stamps(LPCNetBatch *b, int enable);
 LPCNET_EXPORT int lpcnet_batch_get_stamps(LPCNetBatch *b, unsigned long long *out);
+/* Frame-kernel phase stamps of the last launch: [B/4 workgroups][16]
+ * (0 prologue, 1 conv1, 2 conv2, 3 dense1, 4 dense2, 5 projections,
+ * 6 epilogue, 7 total), cycles. */
+LPCNET_EXPORT int lpcnet_batch_get_frame_stamps(LPCNetBatch *b, unsigned long long *out);
 
 /* Per-stream state snapshot: any pointer may be NULL. */
 LPCNET_EXPORT int lpcnet_batch_get_state(LPCNetBatch *b, int stream, float *gru_a_cond /*1152*/, float *gru_b_cond /*48*/,

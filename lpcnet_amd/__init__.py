@@ -72,6 +72,7 @@ def _load():
         "lpcnet_batch_kernel_ms": (C.c_double, [vp, i, C.POINTER(C.c_int)]),
         "lpcnet_batch_set_stamps": (i, [vp, i]),
         "lpcnet_batch_get_stamps": (i, [vp, vp]),
+        "lpcnet_batch_get_frame_stamps": (i, [vp, vp]),
         "lpcnet_batch_set_trace": (i, [vp, i]),
         "lpcnet_batch_get_trace": (i, [vp, vp, vp]),
         "lpcnet_batch_get_state": (i, [vp, i, vp, vp, vp, vp, vp, vp]),
@@ -298,6 +299,14 @@ class LPCNetBatch:
         """[workgroups, 8 waves, 16] s_memtime sums of the last sample-kernel launch."""
         out = np.zeros((self.B, 8, 16), np.uint64)
         g = lib.lpcnet_batch_get_stamps(self._b, out.ctypes.data)
+        if g < 0:
+            raise LPCNetError("stamps not enabled")
+        return out[:g]
+
+    def get_frame_stamps(self) -> np.ndarray:
+        """[workgroups, 16] s_memtime phase durations of the last frame-kernel launch."""
+        out = np.zeros(((self.B + 3) // 4, 16), np.uint64)
+        g = lib.lpcnet_batch_get_frame_stamps(self._b, out.ctypes.data)
         if g < 0:
             raise LPCNetError("stamps not enabled")
         return out[:g]

@@ -713,18 +713,39 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   free_model(b);
   FrameArgs &fa = b->fa;
 #define UP(dst, src, n) if (!(dst = dev_upload<std::remove_const<std::remove_pointer<decltype(dst)>::type>::type>(b, src, n))) { set_err("device upload failed"); free_model(b); return -1; }
-  UP(fa.conv1_w, conv1_w, 3 * FIN * COND * 4);
+  /* frame-network weights keep the blob's [in][out] layout, padded with
+   * FRAME_PREFETCH zero input rows: frame_kernel reads that far ahead */
+  auto padded = [](const float *w, int nin, int nout) {
+    std::vector<float> v((size_t)(nin + FRAME_PREFETCH) * nout, 0.f);
+    memcpy(v.data(), w, (size_t)nin * nout * 4);
+    return v;
+  };
+  std::vector<float> c1p = padded(conv1_w, 3 * FIN, COND), c2p = padded(conv2_w, 3 * COND, COND);
+  std::vector<float> d1p = padded(dense1_w, COND, COND), d2p = padded(dense2_w, COND, COND);
+  UP(fa.conv1_w, c1p.data(), c1p.size() * 4);
   UP(fa.conv1_b, conv1_b, COND * 4);
-  UP(fa.conv2_w, conv2_w, 3 * COND * COND * 4);
+  UP(fa.conv2_w, c2p.data(), c2p.size() * 4);
   UP(fa.conv2_b, conv2_b, COND * 4);
-  UP(fa.dense1_w, dense1_w, COND * COND * 4);
+  UP(fa.dense1_w, d1p.data(), d1p.size() * 4);
   UP(fa.dense1_b, dense1_b, COND * 4);
-  UP(fa.dense2_w, dense2_w, COND * COND * 4);
+  UP(fa.dense2_w, d2p.data(), d2p.size() * 4);
   UP(fa.dense2_b, dense2_b, COND * 4);
   UP(fa.gadf_w, gadf_w, COND * GA_ROWS * 4);
   UP(fa.gadf_b, gadf_b, GA_ROWS * 4);
   UP(fa.gbdf_w, gbdf_w, COND * GB_ROWS * 4);
   UP(fa.gbdf_b, gbdf_b, GB_ROWS * 4);
+  {
+    /* the two conditioning projections as one [COND][GA_ROWS + GB_ROWS] matrix */
+    std::vector<float> pw((size_t)(COND + FRAME_PREFETCH) * (GA_ROWS + GB_ROWS), 0.f), pb(GA_ROWS + GB_ROWS);
+    for (int j = 0; j < COND; j++) {
+      memcpy(&pw[(size_t)j * (GA_ROWS + GB_ROWS)], gadf_w + (size_t)j * GA_ROWS, GA_ROWS * 4);
+      memcpy(&pw[(size_t)j * (GA_ROWS + GB_ROWS) + GA_ROWS], gbdf_w + (size_t)j * GB_ROWS, GB_ROWS * 4);
+    }
+    memcpy(pb.data(), gadf_b, GA_ROWS * 4);
+    memcpy(pb.data() + GA_ROWS, gbdf_b, GB_ROWS * 4);
+    UP(fa.proj_w, pw.data(), pw.size() * 4);
+    UP(fa.proj_b, pb.data(), pb.size() * 4);
+  }
   UP(fa.embed_pitch, embed_pitch, 256 * EP * 4);
   UP(fa.rcp, rcp_dev, sizeof(rcp_dev));
   UP(sa.emb_sig, emb_sig, 256 * GA_ROWS * 4);
@@ -814,6 +835,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   sa.pcm = d_pcm;
   sa.preload = std::max(0, std::min(preload, N));
   sa.stamps = b->d_stamps;
+  fa.stamps = b->d_stamps ? b->d_stamps + (size_t)b->B * STAMP_WAVES * 16 : nullptr;
   hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
   if (b->timing)
     for (int i = 0; i < 4; i++) e[i] = get_event(b);
@@ -1122,7 +1144,9 @@ LPCNET_EXPORT int lpcnet_batch_set_stamps(LPCNetBatch *b, int enable)
   if (b->d_stamps) (void)hipFree(b->d_stamps);
   b->d_stamps = nullptr;
   if (enable) {
-    size_t n = (size_t)b->B * STAMP_WAVES * 16; /* enough for any S */
+    /* sample kernel [groups][STAMP_WAVES][16] (enough for any S), then the
+     * frame kernel [B / FRAME_STREAMS][16] */
+    size_t n = (size_t)b->B * STAMP_WAVES * 16 + (size_t)(b->B / FRAME_STREAMS + 1) * 16;
     HIPCHK(hipMalloc(&b->d_stamps, n * 8));
     HIPCHK(hipMemset(b->d_stamps, 0, n * 8));
   }
@@ -1135,6 +1159,15 @@ LPCNET_EXPORT int lpcnet_batch_get_stamps(LPCNetBatch *b, unsigned long long *ou
   HIPCHK(hipStreamSynchronize(b->stream));
   int g = stamp_groups(b);
   HIPCHK(hipMemcpy(out, b->d_stamps, (size_t)g * STAMP_WAVES * 16 * 8, hipMemcpyDeviceToHost));
+  return g;
+}
+
+LPCNET_EXPORT int lpcnet_batch_get_frame_stamps(LPCNetBatch *b, unsigned long long *out)
+{
+  if (!b || !b->d_stamps || !b->have_model || b->set_device()) return -1;
+  HIPCHK(hipStreamSynchronize(b->stream));
+  const int g = (b->B + FRAME_STREAMS - 1) / FRAME_STREAMS;
+  HIPCHK(hipMemcpy(out, b->d_stamps + (size_t)b->B * STAMP_WAVES * 16, (size_t)g * 16 * 8, hipMemcpyDeviceToHost));
   return g;
 }
 

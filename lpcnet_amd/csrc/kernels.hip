@@ -7,10 +7,8 @@
  * reference issues _mm256_fmadd_ps, and _mm256_rcp_ps is emulated through the
  * 2048-entry table (rcp_x86 below).
  *
- * Kernels
- *   frame_kernel  -- run_frame_network (lpcnet.c:82-120) for 4 streams per
- *                    256-thread workgroup: conv1d x2, dense x2, the GRU_A/GRU_B
- *                    conditioning projections and the LPC ring.
+ * Kernels (frame_kernel.hip: the frame network; mf_kernel.hip: the
+ * matrix-core sample kernel)
  *   sample_kernel -- lpcnet_synthesize_tail_impl (lpcnet.c:235-271) for one
  *                    frame: S streams per 384-thread workgroup, persistent over
  *                    the N samples.  Thread i owns GRU_A unit i (its z, r and h
@@ -27,175 +25,6 @@
 #include "sampler.h"
 
 namespace lpcnet_mi355x {
-
-/* ------------------------------------------------------------------------ */
-/* frame network                                                             */
-
-/* out[i] = act(bias[i] + sum_j W[j*nout+i] x[j]) for a pair of streams, with
- * the per-row sequential FMA chain of sgemv_accum16 (vec_avx.h:618-643). */
-__device__ __forceinline__ float2 chain2(const float *__restrict__ W, float b, int nout, int i, const float4 *x, int nin,
-                                         int half)
-{
-  float a0 = b, a1 = b;
-  const float *wp = W + i;
-  int j = 0;
-  for (; j + 4 <= nin; j += 4) {
-    float w0 = wp[(j + 0) * nout], w1 = wp[(j + 1) * nout], w2 = wp[(j + 2) * nout], w3 = wp[(j + 3) * nout];
-    float4 x0 = x[j], x1 = x[j + 1], x2 = x[j + 2], x3 = x[j + 3];
-    float2 y0 = half ? make_float2(x0.z, x0.w) : make_float2(x0.x, x0.y);
-    float2 y1 = half ? make_float2(x1.z, x1.w) : make_float2(x1.x, x1.y);
-    float2 y2 = half ? make_float2(x2.z, x2.w) : make_float2(x2.x, x2.y);
-    float2 y3 = half ? make_float2(x3.z, x3.w) : make_float2(x3.x, x3.y);
-    a0 = __builtin_fmaf(w0, y0.x, a0); a1 = __builtin_fmaf(w0, y0.y, a1);
-    a0 = __builtin_fmaf(w1, y1.x, a0); a1 = __builtin_fmaf(w1, y1.y, a1);
-    a0 = __builtin_fmaf(w2, y2.x, a0); a1 = __builtin_fmaf(w2, y2.y, a1);
-    a0 = __builtin_fmaf(w3, y3.x, a0); a1 = __builtin_fmaf(w3, y3.y, a1);
-  }
-  for (; j < nin; j++) {
-    float w0 = wp[j * nout];
-    float4 x0 = x[j];
-    float2 y0 = half ? make_float2(x0.z, x0.w) : make_float2(x0.x, x0.y);
-    a0 = __builtin_fmaf(w0, y0.x, a0); a1 = __builtin_fmaf(w0, y0.y, a1);
-  }
-  return make_float2(a0, a1);
-}
-
-__device__ __forceinline__ float4 chain4(const float *__restrict__ W, float b, int nout, int i, const float4 *x, int nin)
-{
-  float4 a = make_float4(b, b, b, b);
-  const float *wp = W + i;
-  for (int j = 0; j < nin; j += 4) {
-    float w0 = wp[(j + 0) * nout], w1 = wp[(j + 1) * nout], w2 = wp[(j + 2) * nout], w3 = wp[(j + 3) * nout];
-    float4 x0 = x[j], x1 = x[j + 1], x2 = x[j + 2], x3 = x[j + 3];
-    a.x = __builtin_fmaf(w0, x0.x, a.x); a.y = __builtin_fmaf(w0, x0.y, a.y); a.z = __builtin_fmaf(w0, x0.z, a.z); a.w = __builtin_fmaf(w0, x0.w, a.w);
-    a.x = __builtin_fmaf(w1, x1.x, a.x); a.y = __builtin_fmaf(w1, x1.y, a.y); a.z = __builtin_fmaf(w1, x1.z, a.z); a.w = __builtin_fmaf(w1, x1.w, a.w);
-    a.x = __builtin_fmaf(w2, x2.x, a.x); a.y = __builtin_fmaf(w2, x2.y, a.y); a.z = __builtin_fmaf(w2, x2.z, a.z); a.w = __builtin_fmaf(w2, x2.w, a.w);
-    a.x = __builtin_fmaf(w3, x3.x, a.x); a.y = __builtin_fmaf(w3, x3.y, a.y); a.z = __builtin_fmaf(w3, x3.z, a.z); a.w = __builtin_fmaf(w3, x3.w, a.w);
-  }
-  return a;
-}
-
-__device__ __forceinline__ float get4(const float4 &v, int s) { return s == 0 ? v.x : (s == 1 ? v.y : (s == 2 ? v.z : v.w)); }
-__device__ __forceinline__ void set4(float4 &v, int s, float x)
-{
-  if (s == 0) v.x = x; else if (s == 1) v.y = x; else if (s == 2) v.z = x; else v.w = x;
-}
-
-__global__ __launch_bounds__(FRAME_THREADS) void frame_kernel(FrameArgs A)
-{
-  /* activations stored [input j][stream 0..3] so one ds_read_b128 feeds 4 chains */
-  __shared__ float4 x1[3 * FIN];    /* conv1 input window: mem (2 frames) + current */
-  __shared__ float4 x2[3 * COND];   /* conv2 input window */
-  __shared__ float4 ya[COND], yb[COND];
-  __shared__ int fc[FRAME_STREAMS];
-  const int tid = threadIdx.x;
-  const int s0 = blockIdx.x * FRAME_STREAMS;
-  const uint32_t *rcp = A.rcp;
-
-  if (tid < FRAME_STREAMS) {
-    int sid = s0 + tid;
-    fc[tid] = sid < A.nstreams ? A.st[sid].frame_count : 1000;
-  }
-  for (int e = tid; e < FRAME_STREAMS * 3 * FIN; e += FRAME_THREADS) {
-    int s = e / (3 * FIN), j = e % (3 * FIN);
-    int sid = min(s0 + s, A.nstreams - 1);
-    const StreamState *p = &A.st[sid];
-    float v;
-    if (j < 2 * FIN) {
-      v = p->conv1_mem[j];
-    } else if (j < 2 * FIN + NF) {
-      v = A.features[sid * NF + (j - 2 * FIN)];
-    } else {
-      /* lpcnet.c:93-94: the 0.1 avoids rounding issues */
-      float f18 = A.features[sid * NF + 18];
-      int pitch = (int)floor(.1 + (double)(50.f * f18) + 100);
-      pitch = min(255, max(33, pitch));
-      v = A.embed_pitch[pitch * EP + (j - 2 * FIN - NF)];
-    }
-    set4(x1[j], s, v);
-  }
-  for (int e = tid; e < FRAME_STREAMS * 2 * COND; e += FRAME_THREADS) {
-    int s = e / (2 * COND), j = e % (2 * COND);
-    int sid = min(s0 + s, A.nstreams - 1);
-    set4(x2[j], s, A.st[sid].conv2_mem[j]);
-  }
-  __syncthreads();
-
-  const int i = tid & (COND - 1), half = tid >> 7;
-  /* conv1 (nnet.c:452-470): 252 inputs -> 128, tanh; cleared while frame_count < 1 */
-  {
-    float2 a = chain2(A.conv1_w, A.conv1_b[i], COND, i, x1, 3 * FIN, half);
-    a.x = tanh_x86(a.x, rcp);
-    a.y = tanh_x86(a.y, rcp);
-    if (fc[2 * half] < 1) a.x = 0.f;
-    if (fc[2 * half + 1] < 1) a.y = 0.f;
-    set4(x2[2 * COND + i], 2 * half, a.x);
-    set4(x2[2 * COND + i], 2 * half + 1, a.y);
-  }
-  __syncthreads();
-  /* conv2: 384 inputs -> 128, tanh; cleared while frame_count < FEATURES_DELAY */
-  {
-    float2 a = chain2(A.conv2_w, A.conv2_b[i], COND, i, x2, 3 * COND, half);
-    a.x = tanh_x86(a.x, rcp);
-    a.y = tanh_x86(a.y, rcp);
-    if (fc[2 * half] < FEATURES_DELAY) a.x = 0.f;
-    if (fc[2 * half + 1] < FEATURES_DELAY) a.y = 0.f;
-    set4(ya[i], 2 * half, a.x);
-    set4(ya[i], 2 * half + 1, a.y);
-  }
-  __syncthreads();
-  {
-    float2 a = chain2(A.dense1_w, A.dense1_b[i], COND, i, ya, COND, half);
-    set4(yb[i], 2 * half, tanh_x86(a.x, rcp));
-    set4(yb[i], 2 * half + 1, tanh_x86(a.y, rcp));
-  }
-  __syncthreads();
-  {
-    float2 a = chain2(A.dense2_w, A.dense2_b[i], COND, i, yb, COND, half);
-    set4(ya[i], 2 * half, tanh_x86(a.x, rcp));
-    set4(ya[i], 2 * half + 1, tanh_x86(a.y, rcp));
-  }
-  __syncthreads();
-  /* conditioning projections (linear) */
-  for (int o = tid; o < GA_ROWS + GB_ROWS; o += FRAME_THREADS) {
-    float4 a = o < GA_ROWS ? chain4(A.gadf_w, A.gadf_b[o], GA_ROWS, o, ya, COND)
-                           : chain4(A.gbdf_w, A.gbdf_b[o - GA_ROWS], GB_ROWS, o - GA_ROWS, ya, COND);
-    for (int s = 0; s < FRAME_STREAMS; s++) {
-      int sid = s0 + s;
-      if (sid >= A.nstreams) break;
-      if (o < GA_ROWS) A.st[sid].gru_a_cond[o] = get4(a, s);
-      else A.st[sid].gru_b_cond[o - GA_ROWS] = get4(a, s);
-    }
-  }
-  /* conv memories (nnet.c:469) */
-  for (int e = tid; e < FRAME_STREAMS * 2 * FIN; e += FRAME_THREADS) {
-    int s = e / (2 * FIN), j = e % (2 * FIN);
-    if (s0 + s < A.nstreams) A.st[s0 + s].conv1_mem[j] = get4(x1[FIN + j], s);
-  }
-  for (int e = tid; e < FRAME_STREAMS * 2 * COND; e += FRAME_THREADS) {
-    int s = e / (2 * COND), j = e % (2 * COND);
-    if (s0 + s < A.nstreams) A.st[s0 + s].conv2_mem[j] = get4(x2[COND + j], s);
-  }
-  /* LPC ring (lpcnet.c:110-118; LPC_GAMMA = 1 -> lpc_weighting multiplies by 1.0f) */
-  if (tid < FRAME_STREAMS * NLPC) {
-    int s = tid / NLPC, k = tid % NLPC, sid = s0 + s;
-    if (sid < A.nstreams) {
-      StreamState *p = &A.st[sid];
-      float cur = p->old_lpc[FEATURES_DELAY - 1][k];
-      float nxt = p->old_lpc[0][k];
-      float g = 1.0f, gi = g;
-      for (int q = 0; q < k; q++) gi *= g;
-      p->lpc[k] = cur * gi;
-      p->old_lpc[1][k] = nxt;
-      p->old_lpc[0][k] = A.lpc_new[sid * NLPC + k];
-    }
-  }
-  __syncthreads();
-  if (tid < FRAME_STREAMS) {
-    int sid = s0 + tid;
-    if (sid < A.nstreams && fc[tid] < 1000) A.st[sid].frame_count = fc[tid] + 1;
-  }
-}
 
 /* ------------------------------------------------------------------------ */
 /* sample network                                                            */
@@ -1122,13 +951,6 @@ int launch_wave(const SampleArgs &a, int nw, int sat, int lds_bytes, void *strea
 }
 
 /* ------------------------------------------------------------------------ */
-int launch_frame(const FrameArgs &a, void *stream)
-{
-  int grid = (a.nstreams + FRAME_STREAMS - 1) / FRAME_STREAMS;
-  hipLaunchKernelGGL(frame_kernel, dim3(grid), dim3(FRAME_THREADS), 0, (hipStream_t)stream, a);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 /* ------------------------------------------------------------------------ */
 /* pipe_kernel: fixed wave roles, the GRU_A recurrent product of sample n+1
  * overlapping the sampling of sample n.

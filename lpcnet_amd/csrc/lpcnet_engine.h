@@ -28,8 +28,8 @@ constexpr int SAMPLE_WAVES = SAMPLE_THREADS / 64;
 constexpr int PIPE_THREADS = 512;   /* pipe_kernel: 6 GRU_A waves + 2 sampler waves */
 constexpr int PIPE_WAVES = PIPE_THREADS / 64;
 constexpr int STAMP_WAVES = PIPE_WAVES; /* stamps are [workgroup][STAMP_WAVES][16] */
-constexpr int FRAME_THREADS = 256;
 constexpr int FRAME_STREAMS = 4;    /* streams per frame-network workgroup */
+constexpr int FRAME_PREFETCH = 64;  /* zero input rows padding each frame-network weight matrix */
 constexpr int REG_GB = 12;          /* GRU_B input slots per lane: block k = ks + 8*j, j < 12 */
 /* Matrix-core kernel (mf_kernel.hip).
  * GRU_A (v_mfma_i32_4x4x4_16b_i8): per-lane register tables, one u32 word
@@ -90,8 +90,10 @@ struct FrameArgs {
   const float *conv1_w, *conv1_b, *conv2_w, *conv2_b;
   const float *dense1_w, *dense1_b, *dense2_w, *dense2_b;
   const float *gadf_w, *gadf_b, *gbdf_w, *gbdf_b;
+  const float *proj_w, *proj_b; /* gadf | gbdf as one [COND][GA_ROWS + GB_ROWS] matrix, bias */
   const float *embed_pitch;
   const uint32_t *rcp; /* 2048-entry table in global memory */
+  unsigned long long *stamps; /* optional diagnostics [grid][16] s_memtime per phase */
 };
 
 struct SampleArgs {

@@ -36,6 +36,9 @@ def profile(B, variant=0, kernel=1):
         if row[6] == 0:
             continue
         print(f"  wave {w}: " + " ".join(f"{NAMES[k][j]}={row[j]:7.0f}" for j in range(6)) + f"  loop={row[6]:7.0f}")
+    fs = b.get_frame_stamps().astype(np.float64).mean(0)
+    print("  frame kernel (cycles): prologue=%.0f conv1=%.0f conv2=%.0f dense1=%.0f dense2=%.0f proj=%.0f epilogue=%.0f total=%.0f" %
+          tuple(fs[:8]))
     if k == 4:
         print("  GRU_A X->Y gathers (to last arrival): " + " ".join("w%d=%.0f" % (w, per[:, w, 10].mean()) for w in range(6)))
     if k in (3, 4):
