@@ -27,13 +27,15 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: int8 MFMA dense = 2x the ~2.5 PF bf16 rate
 
 
-def measured_traffic(kernel_prefix):
-    """HBM bytes per launch of the sample kernel from the committed rocprofv3
-    FETCH_SIZE/WRITE_SIZE passes of this same command (tools/gpu_profile.sh ->
-    tools/pmc_summary.py -> profiles/<round>/pmc_traffic.json); PMC counters
-    cannot be read in-process.  None when no profile matches the kernel."""
+def measured_pmc(kernel_prefix):
+    """PMC record of the sample kernel from the committed rocprofv3 passes of
+    this same command (tools/gpu_profile.sh -> tools/pmc_summary.py ->
+    profiles/<round>/pmc_traffic.json: HBM bytes per launch from
+    FETCH_SIZE/WRITE_SIZE, MFMA busy fraction); PMC counters cannot be read
+    in-process.  ({}, None) when no profile matches the kernel."""
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
         try:
@@ -42,8 +44,8 @@ def measured_traffic(kernel_prefix):
             continue
         for k, v in d.items():
             if kernel_prefix in k:
-                return v["hbm_bytes_per_launch_corrected"], os.path.relpath(f, ROOT), k
-    return None, None, None
+                return v, os.path.relpath(f, ROOT)
+    return {}, None
 
 
 def parse():
@@ -179,7 +181,8 @@ def main():
     bytes_launch = 160 * info.bytes_shared_per_sample + B * 160 * info.bytes_per_stream_sample
     achieved = bytes_launch / (sample_ms * 1e-3) / 1e9
     kname = info.kernel_name
-    traffic, tsrc, _ = measured_traffic(kname) if B == 1024 else (None, None, None)
+    pmc, tsrc = measured_pmc(kname) if B == 1024 else ({}, None)
+    traffic = pmc.get("hbm_bytes_per_launch_corrected")
     out = {
         "metric": "real-time 16 kHz streams/GPU; samples/s at batch=1 and batch=1024",
         "value": value,
@@ -203,6 +206,15 @@ def main():
                      "kernel": kname, "avg_launch_ms": sample_ms, "launches": kn,
                      "algorithmic_bytes_per_launch": bytes_launch},
         "frame_kernel_avg_ms": fs / max(fn, 1),
+        # matrix-core work of the sample kernel (north_star: MFMA at batch >= 256):
+        # int8 ops issued per launch / launch time, and the PMC busy fraction
+        "mfma": ({"achieved_tops": info.mfma_ops_per_group_sample * ((B + info.streams_per_workgroup - 1)
+                                                                    // info.streams_per_workgroup) * 160
+                                   / (sample_ms * 1e-3) / 1e12,
+                  "peak_tops": I8_PEAK_TOPS, "busy_frac_pmc": pmc.get("mfma_util"),
+                  "ops_per_launch": info.mfma_ops_per_group_sample * ((B + info.streams_per_workgroup - 1)
+                                                                     // info.streams_per_workgroup) * 160}
+                 if info.mfma_ops_per_group_sample > 0 else None),
         "kernel_config": {"streams_per_workgroup": info.streams_per_workgroup, "quad_path": info.quad_path,
                           "lds_bytes": info.lds_bytes, "gru_a_blocks": info.gru_a_blocks},
         "pcm_checksum": int(np.abs(pcm[-1].astype(np.int64)).sum()),

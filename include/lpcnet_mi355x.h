@@ -36,6 +36,8 @@ typedef struct {
   int quad_path;                  /* 0 per-slot LDS, 1 quad LDS (lockstep), 2 wave-per-stream, 3 pipelined,
                                      4 pipelined on the matrix cores */
   int lds_bytes;                  /* dynamic LDS of the sample kernel */
+  double mfma_ops_per_group_sample; /* int8 matrix-core ops issued per workgroup per sample
+                                       (mf_kernel; padding included), 0 otherwise */
 } LPCNetModelInfo;
 
 /* Create a batch of nb_streams streams on HIP device `device`.

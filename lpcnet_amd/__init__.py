@@ -98,7 +98,7 @@ class ModelInfo(C.Structure):
                 ("may_saturate", C.c_int), ("bytes_shared_per_frame", C.c_double),
                 ("bytes_shared_per_sample", C.c_double), ("bytes_per_stream_sample", C.c_double),
                 ("ops_per_sample", C.c_double), ("streams_per_workgroup", C.c_int), ("quad_path", C.c_int),
-                ("lds_bytes", C.c_int)]
+                ("lds_bytes", C.c_int), ("mfma_ops_per_group_sample", C.c_double)]
 
     @property
     def kernel_name(self) -> str:

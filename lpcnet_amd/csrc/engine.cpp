@@ -790,6 +790,14 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   in.bytes_shared_per_sample = 32.0 * nba * wbytes + 4.0 * (nba + GA_ROWS / 8) /* idx */ + 6.0 * NA * 4 /* bias+diag */ +
                                32.0 * nbb * wbytes + 4.0 * (nbb + GB_ROWS / 8) + 3.0 * NB * NB * wbytes + 2.0 * GB_ROWS * 4;
   in.bytes_per_stream_sample = 3.0 * GA_ROWS * 4 /* embedding rows */ + 8 * (32 + 2 * 4 + 2 * 4) /* dual_fc path */ + 2;
+  /* mf_kernel matrix-core work: per GRU_A wave 8 nzr + 4 nh 4x4x4 MFMAs of
+   * 16 x 4x4x4 MACs; per sampler wave 21 16x16x64 MFMAs (2 sampler waves) */
+  in.mfma_ops_per_group_sample = 0;
+  if (mf_ok) {
+    double n4 = 0;
+    for (int w = 0; w < SAMPLE_WAVES; w++) n4 += 8.0 * sa.mf_nzr[w] + 4.0 * sa.mf_nh[w];
+    in.mfma_ops_per_group_sample = 2.0 * (n4 * 1024.0 + 2.0 * MF_GB_TILES * 16384.0);
+  }
   in.ops_per_sample = 2.0 * (32.0 * nba + 32.0 * nbb + 3 * NB * NB + 8 * 2 * NB + NLPC) +
                       2.0 * (3.0 * FIN * COND + 3.0 * COND * COND + 2.0 * COND * COND + COND * GA_ROWS + COND * GB_ROWS) / FRAME;
   return 0;

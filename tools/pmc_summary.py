@@ -43,6 +43,17 @@ def main(outdir):
         wm = sorted(w)[len(w) // 2] if w else None
         res[k] = {"launches": len(f), "fetch_kb_median": fm, "write_kb_median": wm,
                   "hbm_bytes_per_launch_corrected": (2 * fm * 1024 if fm is not None else 0) + (wm * 1024 if wm is not None else 0)}
+    # MFMA utilisation: busy cycles of all SIMDs over (elapsed cycles x 1024
+    # SIMDs); elapsed = GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs)
+    mf = rows(os.path.join(ROOT, "gpurun_out/pmc_mfma/**/*counter_collection.csv"))
+    busy, gui, sqb = per_kernel(mf, "SQ_VALU_MFMA_BUSY_CYCLES"), per_kernel(mf, "GRBM_GUI_ACTIVE"), per_kernel(mf, "SQ_BUSY_CYCLES")
+    for k in set(busy) & set(gui):
+        b, g = sorted(busy[k]), sorted(gui[k])
+        bm, gm = b[len(b) // 2], g[len(g) // 2]
+        res.setdefault(k, {})
+        res[k].update({"mfma_busy_cycles_median": bm, "grbm_gui_active_median": gm,
+                       "sq_busy_cycles_median": sorted(sqb.get(k, [0]))[len(sqb.get(k, [0])) // 2],
+                       "mfma_util": bm / max(1.0, gm / 8 * 1024)})
     json.dump(res, open(os.path.join(outdir, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
