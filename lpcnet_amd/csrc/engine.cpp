@@ -286,11 +286,14 @@ struct LPCNetBatch {
   int variant = 0;
   bool sat = false;
   bool reg = false;
-  int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 2 wave_kernel, 3 pipe_kernel, 4 matrix-core pipe_kernel */
+  int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 2 wave_kernel, 3 pipe_kernel, 4 matrix-core pipe_kernel,
+                            5 fp32 latency kernel */
   int wave_nw = 0;       /* >0: wave_kernel with this many streams per workgroup */
   bool pipe = false;     /* pipe_kernel (mode 3) */
   bool mf_ok = false;    /* model fits the matrix-core register tables */
   bool mf = false;       /* mf_kernel (mode 4) */
+  bool fp_ok = false;    /* fp32 model fits the fp_kernel tables */
+  bool fp = false;       /* fp_kernel (mode 5) */
   int image_bytes = 0;
   LPCNetModelInfo info{};
   std::vector<void *> model_bufs;
@@ -376,9 +379,18 @@ void choose_kernel(LPCNetBatch *b)
   b->wave_nw = 0;
   b->pipe = false;
   b->mf = false;
+  b->fp = false;
   const bool quad_int8 = b->variant == LPCNET_VARIANT_INT8 && b->reg;
   int mode = b->kernel_mode;
-  if (mode == 0) mode = b->mf_ok ? 4 : (quad_int8 ? 3 : 1);
+  if (mode == 0) mode = b->fp_ok ? 5 : (b->mf_ok ? 4 : (quad_int8 ? 3 : 1));
+  if (mode == 5 && b->fp_ok && fp_lds_bytes() <= 160 * 1024) {
+    b->fp = true;
+    b->info.streams_per_workgroup = 1;
+    b->info.lds_bytes = fp_lds_bytes();
+    b->info.quad_path = 5;
+    return;
+  }
+  if (mode == 5) mode = b->mf_ok ? 4 : (quad_int8 ? 3 : 1);
   if (mode == 4 && b->mf_ok && mf_lds_bytes(b->S) <= 160 * 1024) {
     b->mf = true;
     b->info.streams_per_workgroup = b->S;
@@ -697,6 +709,74 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
       }
   }
 
+  /* ---- fp32 latency-kernel tables (fp_kernel, see FP_ZF) ---- */
+  std::vector<float4> fpzr, fph, fpgb;
+  std::vector<uint32_t> fpoff;
+  int fp_nzr[SAMPLE_WAVES] = {}, fp_nh[SAMPLE_WAVES] = {};
+  bool fp_ok = !int8 && !getenv("LPCNET_NO_FPK");
+  for (int rb = 0; rb < GB_ROWS / 8 && fp_ok; rb++) {
+    /* dense GRU_B only: blocks 0, 4, ..., NA-4 in order */
+    if ((int)gb_blocks[rb].size() != NA / 4) fp_ok = false;
+    for (int k = 0; k < (int)gb_blocks[rb].size() && fp_ok; k++)
+      if (gb_blocks[rb][k] != 4 * k) fp_ok = false;
+  }
+  for (int w = 0; w < SAMPLE_WAVES && fp_ok; w++)
+    for (int j = 0; j < 8; j++) {
+      if ((int)ga_blocks[w * 8 + j].size() > FP_ZF || (int)ga_blocks[NA / 8 + w * 8 + j].size() > FP_ZF ||
+          (int)ga_blocks[2 * (NA / 8) + w * 8 + j].size() > FP_HF)
+        fp_ok = false;
+    }
+  if (fp_ok) {
+    const float *wa = (const float *)gaw->data, *wb = (const float *)gbw;
+    const float nz = -0.f;
+    fpzr.assign((size_t)SAMPLE_WAVES * 2 * FP_ZF * 64, make_float4(nz, nz, nz, nz));
+    fph.assign((size_t)SAMPLE_WAVES * FP_HF * 64, make_float4(nz, nz, nz, nz));
+    fpoff.assign((size_t)SAMPLE_WAVES * FP_OFF_WORDS * 64, 0x60606060u); /* column quad NA/4 = 96: the +0 quad */
+    for (int w = 0; w < SAMPLE_WAVES; w++) {
+      int kz = 0, kh = 0;
+      for (int j = 0; j < 8; j++) {
+        kz = std::max(kz, (int)std::max(ga_blocks[w * 8 + j].size(), ga_blocks[NA / 8 + w * 8 + j].size()));
+        kh = std::max(kh, (int)ga_blocks[2 * (NA / 8) + w * 8 + j].size());
+      }
+      fp_nzr[w] = kz;
+      fp_nh[w] = kh;
+      for (int l = 0; l < 64; l++) {
+        const int j = l >> 3, r = l & 7;
+        for (int g = 0; g < 3; g++) {
+          const int rb = g * (NA / 8) + w * 8 + j;
+          for (int t = 0; t < (int)ga_blocks[rb].size(); t++) {
+            const float *src = wa + 32 * (size_t)(ga_first[rb] + t);
+            const float4 v = make_float4(src[0 * 8 + r], src[1 * 8 + r], src[2 * 8 + r], src[3 * 8 + r]);
+            if (g < 2) {
+              /* packed (z, r) pairs: slot t = [z.x r.x z.y r.y] [z.z r.z z.w r.w] */
+              float4 &lo = fpzr[((size_t)w * 2 * FP_ZF + t) * 64 + l], &hi = fpzr[((size_t)w * 2 * FP_ZF + FP_ZF + t) * 64 + l];
+              (g == 0 ? lo.x : lo.y) = v.x;
+              (g == 0 ? lo.z : lo.w) = v.y;
+              (g == 0 ? hi.x : hi.y) = v.z;
+              (g == 0 ? hi.z : hi.w) = v.w;
+            } else {
+              fph[((size_t)w * FP_HF + t) * 64 + l] = v;
+            }
+            const int slot = g * FP_ZF + t, word = slot / 4, sh = 8 * (slot & 3);
+            uint32_t &o = fpoff[((size_t)w * FP_OFF_WORDS + word) * 64 + l];
+            o = (o & ~(0xFFu << sh)) | ((uint32_t)(ga_blocks[rb][t] / 4) << sh);
+          }
+        }
+      }
+    }
+    fpgb.resize((size_t)(NA / 4) * GB_ROWS);
+    for (int rb = 0; rb < GB_ROWS / 8; rb++)
+      for (int k = 0; k < NA / 4; k++)
+        for (int r = 0; r < 8; r++) {
+          const float *src = wb + 32 * (size_t)(gb_first[rb] + k);
+          fpgb[(size_t)k * GB_ROWS + rb * 8 + r] = make_float4(src[0 * 8 + r], src[1 * 8 + r], src[2 * 8 + r], src[3 * 8 + r]);
+        }
+    for (int w = 0; w < SAMPLE_WAVES; w++) {
+      sa.fp_nzr[w] = fp_nzr[w];
+      sa.fp_nh[w] = fp_nh[w];
+    }
+  }
+
   /* choose streams per workgroup and check the LDS budget */
   int S = b->B >= 1024 ? 4 : (b->B >= 512 ? 2 : 1);
   int lds = sample_lds_bytes(S, variant, (int)img.size());
@@ -760,6 +840,12 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
     UP(sa.mf, mft.data(), mft.size() * 4);
     UP(sa.mf_gb, mfgb.data(), mfgb.size() * 4);
   }
+  if (fp_ok) {
+    UP(sa.fp_zr, fpzr.data(), fpzr.size() * sizeof(float4));
+    UP(sa.fp_h, fph.data(), fph.size() * sizeof(float4));
+    UP(sa.fp_gb, fpgb.data(), fpgb.size() * sizeof(float4));
+    UP(sa.fp_off, fpoff.data(), fpoff.size() * 4);
+  }
   if (!int8) {
     UP(sa.ga_wf, ga_wf.data(), ga_wf.size() * sizeof(float4));
     UP(sa.gb_recf, gbrec, 3 * NB * NB * 4);
@@ -770,6 +856,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   b->sat = sat;
   b->reg = reg;
   b->mf_ok = mf_ok;
+  b->fp_ok = fp_ok;
   b->image_bytes = (int)img.size();
   b->S = S;
   b->lds_bytes = lds;
@@ -852,6 +939,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
   const int lrc = N <= 0 ? 0
+                : b->fp    ? launch_fp(sa, b->stream)
                 : b->mf    ? launch_mf(sa, b->S, b->info.lds_bytes, b->stream)
                 : b->pipe  ? launch_pipe(sa, b->S, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
                 : b->wave_nw ? launch_wave(sa, b->wave_nw, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
@@ -967,7 +1055,7 @@ LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *d
 
 LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode)
 {
-  if (!b || mode < 0 || mode > 4) return -1;
+  if (!b || mode < 0 || mode > 5) return -1;
   b->kernel_mode = mode;
   if (b->have_model) choose_kernel(b);
   return 0;

@@ -51,6 +51,23 @@ constexpr int MF_LANE_U32 = MF_GA + MF_GA / 4; /* 80 */
 constexpr int MF_GB_TILES = 3 * 6 + 3;
 constexpr int MF_XSTR = 400;        /* LDS bytes per stream of the quantized GRU_A state (stream-major) */
 constexpr int MF_THREADS = 512;     /* 6 GRU_A waves + 2 sampler waves */
+/* fp32 latency kernel (fp_kernel.hip), one stream per workgroup.
+ * GRU_A per-lane tables (lane l of wave w = unit 64w + l = row l%8 of row
+ * block 8w + l/8 of each gate; slot t = the t-th 8x4 block of that row block,
+ * as the float4 of this row's 4 columns):
+ *   fp_zr [wave][2][FP_ZF][64] float4: slot t as packed (z, r) pairs,
+ *         [z.x r.x z.y r.y] then [z.z r.z z.w r.w] (registers)
+ *   fp_h  [wave][FP_HF][64] float4: h slots (streamed from L2 every sample)
+ *   fp_off [wave][FP_OFF_WORDS][64] u32: column-quad bytes, 4 per word, of
+ *         the z, r and h slots
+ * Unused slots hold -0.0 weights and column quad NA/4, which the kernel
+ * keeps at +0.0: fma(-0, +0, y) = y for every y, NaN and -0 included.
+ * fp_gb [NA/4][GB_ROWS] float4: dense GRU_B input weights (column quad,
+ * row), copied to LDS. */
+constexpr int FP_ZF = 16;           /* z / r slots per lane */
+constexpr int FP_HF = 32;           /* h slots per lane */
+constexpr int FP_OFF_WORDS = (2 * FP_ZF + FP_HF) / 4;
+constexpr int FP_THREADS = 448;     /* 6 GRU_A waves + 1 sampler wave */
 
 /* Per-stream synthesis state in device memory (lpcnet_private.h:28-48). */
 struct alignas(16) StreamState {
@@ -129,6 +146,10 @@ struct SampleArgs {
   int mf_nzr[SAMPLE_WAVES];
   int mf_nh[SAMPLE_WAVES];
   const uint4 *mf_gb;
+  const float4 *fp_zr, *fp_h, *fp_gb; /* fp_kernel tables (see FP_ZF) */
+  const uint32_t *fp_off;
+  int fp_nzr[SAMPLE_WAVES];    /* slots of the z/r chains per GRU_A wave */
+  int fp_nh[SAMPLE_WAVES];     /* slots of the h chains */
   const float4 *ga_wf;   /* fp32 variant: GRU_A blocks [chunk][k][64] float4 */
   const float4 *gb_wf;   /* fp32 variant: GRU_B blocks [rb][k][8 rows][2] float4 (in c) */
   const float *gb_recf;  /* fp32 variant: GRU_B recurrent [NB][GB_ROWS] */
@@ -156,6 +177,10 @@ int launch_pipe(const SampleArgs &a, int S, int sat, int lds_bytes, void *stream
  * workgroup barriers per sample. */
 int mf_lds_bytes(int S);
 int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream);
+/* fp32 latency kernel: one stream per workgroup, LDS flags instead of
+ * workgroup barriers (fp32 models within the FP_* limits, dense GRU_B). */
+int fp_lds_bytes();
+int launch_fp(const SampleArgs &a, void *stream);
 
 /* Host LPC (lpc_host.cpp). */
 float lpc_from_cepstrum_host(float *lpc, const float *ceps);

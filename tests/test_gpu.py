@@ -33,21 +33,26 @@ def blobs():
                                          ("streams_int8", 2), ("streams_int8_sat", 2),
                                          ("streams_int8", 3), ("streams_int8_sat", 3), ("streams_fp32", 3),
                                          ("streams_int8", 4), ("streams_int8_sat", 4), ("streams_fp32", 4),
-                                         ("streams_int8", 0)])
+                                         ("streams_fp32", 5), ("streams_int8", 5), ("streams_int8_sat", 5),
+                                         ("streams_int8", 0), ("streams_fp32", 0)])
 def test_batch_matches_golden(require_gpu, blobs, name, kernel):
     """kernel 1: lockstep sample_kernel, 2: wave-per-stream, 3: pipelined,
     4: pipelined on the matrix cores (saturating models fall back to 3),
-    0: automatic (4 for non-saturating int8).  fp32 models always run the
-    lockstep kernel."""
+    5: fp32 latency kernel (int8 models fall back to 4 / 3),
+    0: automatic (4 for non-saturating int8, 5 for fp32).  fp32 models run
+    the lockstep kernel for every mode but 5 and 0."""
     G = np.load(os.path.join(GOLD, name + ".npz"))
     streams = list(G["streams"])
     F = G["pcm"].shape[1]
     b = L.LPCNetBatch(len(streams), 0, blobs[name])
     b.set_kernel(kernel)
-    expect = {0: 4, 1: 1, 2: 2, 3: 3, 4: 3 if name.endswith("_sat") else 4}[kernel]
-    if kernel != 1 and name.endswith("_sat") and kernel == 0:
-        expect = 3
-    assert b.info().quad_path == (0 if name == "streams_fp32" else expect)
+    if name == "streams_fp32":
+        expect = {0: 5, 1: 0, 3: 0, 4: 0, 5: 5}[kernel]
+    elif name.endswith("_sat"):
+        expect = {0: 3, 1: 1, 2: 2, 3: 3, 4: 3, 5: 3}[kernel]
+    else:
+        expect = {0: 4, 1: 1, 2: 2, 3: 3, 4: 4, 5: 4}[kernel]
+    assert b.info().quad_path == expect
     info = b.info()
     assert info.variant == int(G["variant"])
     if name.endswith("_sat"):
@@ -100,6 +105,29 @@ def test_large_batch_streams_match_oracle(require_gpu, blobs, B, check, kernel):
         assert np.array_equal(out[s], ref), s
     assert np.all(out[:, :2] == 0)  # FEATURES_DELAY silent frames
     assert np.abs(out[:, 2:]).mean() > 100
+
+
+@pytest.mark.parametrize("B,check", [(1, (0,)), (70, (0, 37, 69))])
+def test_fp32_latency_kernel_matches_oracle(require_gpu, blobs, B, check):
+    """fp_kernel (one stream per workgroup) against the fp32 oracle, with a
+    partial frame (N = 80) and a per-stream reset in the middle."""
+    F = 7
+    blob = blobs["streams_fp32"]
+    b = L.LPCNetBatch(B, 0, blob)
+    b.set_kernel(5)
+    assert b.info().quad_path == 5
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    refs = {s: O.Oracle(blob, 1) for s in check}
+    for f in range(F):
+        if f == 5:
+            b.reset(check[-1])
+            refs[check[-1]] = O.Oracle(blob, 1)
+        n = 80 if f == 4 else 160
+        out = b.synthesize(allf[f], n)
+        for s in check:
+            assert np.array_equal(out[s], refs[s].synthesize(allf[f, s], n)), (f, s)
+        if f == 3:
+            assert np.abs(out.astype(np.float64)).mean() > 100
 
 
 def test_device_resident_frames_equal_host_path(require_gpu, blobs):
@@ -165,15 +193,15 @@ def test_full_size_properties(require_gpu, blobs):
     assert np.abs(o1[:, 2:].astype(np.float64)).mean() > 100
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3, 4])
-def test_preload_teacher_forcing_matches_oracle(require_gpu, blobs, kernel):
+@pytest.mark.parametrize("kernel,variant", [(1, 0), (2, 0), (3, 0), (4, 0), (5, 1), (1, 1)])
+def test_preload_teacher_forcing_matches_oracle(require_gpu, blobs, kernel, variant):
     """lpcnet_synthesize_impl with preload (lpcnet.c:256-259, the PLC entry)."""
-    blob = blobs["streams_int8"]
+    blob = blobs["streams_fp32" if variant else "streams_int8"]
     B, F = 3, 9
     allf = np.stack([feats(s, F) for s in range(B)], 1)
     b = L.LPCNetBatch(B, 0, blob)
     b.set_kernel(kernel)
-    refs = [O.Oracle(blob, 0) for _ in range(B)]
+    refs = [O.Oracle(blob, variant) for _ in range(B)]
     t = np.arange(160)
     for f in range(F):
         if f in (4, 6):
