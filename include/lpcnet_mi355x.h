@@ -100,7 +100,9 @@ LPCNET_EXPORT int lpcnet_batch_memcpy_d2h(LPCNetBatch *b, void *dst, const void 
 
 /* Kernel timing (HIP events on the batch's stream, recorded around every
  * launch since the last reset_timers): which = 0 sample-network kernel,
- * 1 frame-network kernel.  Returns total ms and the number of launches. */
+ * 1 frame-network kernel.  Returns total ms and the number of launches.
+ * enable: 0 off, 1 events around the sample kernel only, 2 (or more) around
+ * both kernels. */
 LPCNET_EXPORT void lpcnet_batch_reset_timers(LPCNetBatch *b, int enable);
 LPCNET_EXPORT double lpcnet_batch_kernel_ms(LPCNetBatch *b, int which, int *launches);
 

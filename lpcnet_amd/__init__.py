@@ -286,8 +286,9 @@ class LPCNetBatch:
         if lib.lpcnet_batch_sync(self._b) != 0:
             raise LPCNetError(last_error())
 
-    def reset_timers(self, enable: bool = True) -> None:
-        lib.lpcnet_batch_reset_timers(self._b, 1 if enable else 0)
+    def reset_timers(self, enable: bool | int = True) -> None:
+        """0/False off, 1 sample kernel only, 2/True sample and frame kernels."""
+        lib.lpcnet_batch_reset_timers(self._b, 2 if enable is True else int(enable))
 
     def kernel_ms(self, which: int = 0) -> tuple[float, int]:
         n = C.c_int(0)

@@ -306,6 +306,7 @@ struct LPCNetBatch {
   short *d_pcm = nullptr;
   float *d_lpc[2] = {nullptr, nullptr};
   float *h_lpc[2] = {nullptr, nullptr};
+  float *h_lpc_dev[2] = {nullptr, nullptr}; /* device view of the pinned h_lpc */
   hipEvent_t ev_lpc[2] = {nullptr, nullptr};
   bool ev_lpc_used[2] = {false, false};
   /* trace */
@@ -316,7 +317,8 @@ struct LPCNetBatch {
   /* diagnostics */
   unsigned long long *d_stamps = nullptr;
   /* timing */
-  bool timing = false;
+  int timing = 0;        /* 0 off, 1 sample kernel, 2 sample + frame kernel */
+  std::vector<hipEvent_t> ev_taken; /* events handed out since the last reset */
   std::vector<hipEvent_t> ev_pairs[2];
   std::vector<hipEvent_t> ev_free;
   Pool *pool = nullptr;
@@ -931,13 +933,17 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   sa.preload = std::max(0, std::min(preload, N));
   sa.stamps = b->d_stamps;
   fa.stamps = b->d_stamps ? b->d_stamps + (size_t)b->B * STAMP_WAVES * 16 : nullptr;
-  hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
-  if (b->timing)
-    for (int i = 0; i < 4; i++) e[i] = get_event(b);
+  /* timing 1: events around the sample kernel only; 2: the frame kernel too
+   * (one event between the two kernels serves both pairs) */
+  hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+  if (b->timing >= 2) e[0] = get_event(b);
+  if (b->timing >= 1) {
+    e[1] = get_event(b);
+    e[2] = get_event(b);
+  }
   if (e[0]) HIPCHK(hipEventRecord(e[0], b->stream));
   if (launch_frame(fa, b->stream)) { set_err("frame kernel launch failed"); return -1; }
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
-  if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
   const int lrc = N <= 0 ? 0
                 : b->fp    ? launch_fp(sa, b->stream)
                 : b->mf    ? launch_mf(sa, b->S, b->info.lds_bytes, b->stream)
@@ -948,13 +954,17 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
     set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     return -1;
   }
-  if (e[3]) HIPCHK(hipEventRecord(e[3], b->stream));
-  if (b->timing) {
+  if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
+  if (e[0]) {
     b->ev_pairs[1].push_back(e[0]);
     b->ev_pairs[1].push_back(e[1]);
-    b->ev_pairs[0].push_back(e[2]);
-    b->ev_pairs[0].push_back(e[3]);
   }
+  if (e[1]) {
+    b->ev_pairs[0].push_back(e[1]);
+    b->ev_pairs[0].push_back(e[2]);
+  }
+  for (hipEvent_t x : e)
+    if (x) b->ev_taken.push_back(x);
   return 0;
 }
 
@@ -1006,7 +1016,8 @@ LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
   ok = ok && hipMalloc(&b->d_pcm, sizeof(short) * FRAME * (size_t)nb_streams) == hipSuccess;
   for (int i = 0; i < 2 && ok; i++) {
     ok = ok && hipMalloc(&b->d_lpc[i], sizeof(float) * NLPC * (size_t)nb_streams) == hipSuccess;
-    ok = ok && hipHostMalloc(&b->h_lpc[i], sizeof(float) * NLPC * (size_t)nb_streams, hipHostMallocDefault) == hipSuccess;
+    ok = ok && hipHostMalloc(&b->h_lpc[i], sizeof(float) * NLPC * (size_t)nb_streams, hipHostMallocMapped) == hipSuccess;
+    ok = ok && hipHostGetDevicePointer((void **)&b->h_lpc_dev[i], b->h_lpc[i], 0) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&b->ev_lpc[i], hipEventDisableTiming) == hipSuccess;
   }
   if (!ok) {
@@ -1037,8 +1048,7 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
     if (b->h_lpc[i]) (void)hipHostFree(b->h_lpc[i]);
     if (b->ev_lpc[i]) (void)hipEventDestroy(b->ev_lpc[i]);
   }
-  for (int k = 0; k < 2; k++)
-    for (hipEvent_t e : b->ev_pairs[k]) (void)hipEventDestroy(e);
+  for (hipEvent_t e : b->ev_taken) (void)hipEventDestroy(e);
   for (hipEvent_t e : b->ev_free) (void)hipEventDestroy(e);
   if (b->stream) (void)hipStreamDestroy(b->stream);
   delete b->pool;
@@ -1149,10 +1159,11 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
   compute_lpc(b, h_features, NF, b->h_lpc[0]);
   for (int f = 0; f < nframes; f++) {
     slot = f & 1;
-    HIPCHK(hipMemcpyAsync(b->d_lpc[slot], b->h_lpc[slot], sizeof(float) * NLPC * b->B, hipMemcpyHostToDevice, b->stream));
+    /* zero copy: the frame kernel reads the pinned host LPC directly (64 B
+     * per stream); the slot is rewritten only after that kernel finished */
+    if (launch_frame_step(b, d_features + f * fstride, b->h_lpc_dev[slot], d_pcm + (size_t)f * b->B * N, N)) return -1;
     HIPCHK(hipEventRecord(b->ev_lpc[slot], b->stream));
     b->ev_lpc_used[slot] = true;
-    if (launch_frame_step(b, d_features + f * fstride, b->d_lpc[slot], d_pcm + (size_t)f * b->B * N, N)) return -1;
     if (f + 1 < nframes) {
       /* host LPC of the next frame overlaps this frame's kernels */
       if (wait_slot(slot ^ 1)) return -1;
@@ -1205,11 +1216,10 @@ LPCNET_EXPORT void lpcnet_batch_reset_timers(LPCNetBatch *b, int enable)
   if (!b) return;
   b->set_device();
   (void)hipStreamSynchronize(b->stream);
-  for (int k = 0; k < 2; k++) {
-    for (hipEvent_t e : b->ev_pairs[k]) b->ev_free.push_back(e);
-    b->ev_pairs[k].clear();
-  }
-  b->timing = enable != 0;
+  for (int k = 0; k < 2; k++) b->ev_pairs[k].clear();
+  for (hipEvent_t e : b->ev_taken) b->ev_free.push_back(e);
+  b->ev_taken.clear();
+  b->timing = enable < 0 ? 0 : (enable > 2 ? 2 : enable);
 }
 
 LPCNET_EXPORT double lpcnet_batch_kernel_ms(LPCNetBatch *b, int which, int *launches)

@@ -113,19 +113,23 @@ __device__ __forceinline__ void chain_deep(const float *__restrict__ W, int row,
   }
 }
 
+/* NS streams per workgroup: 4 (FRAME_STREAMS) for batches, 1 for a single
+ * stream, where the three idle chains per thread would only cost issue slots
+ * on the latency-bound chains. */
+template <int NS>
 __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
 {
   /* activations [stream][input], rows 16-byte aligned */
-  __shared__ float4 x1_[FRAME_STREAMS][3 * FIN / 4]; /* conv1 window: 2 memory frames + current */
-  __shared__ float4 x2_[FRAME_STREAMS][3 * COND / 4]; /* conv2 window */
-  __shared__ float4 ya_[FRAME_STREAMS][COND / 4], yb_[FRAME_STREAMS][COND / 4];
-  __shared__ int fc[FRAME_STREAMS];
+  __shared__ float4 x1_[NS][3 * FIN / 4]; /* conv1 window: 2 memory frames + current */
+  __shared__ float4 x2_[NS][3 * COND / 4]; /* conv2 window */
+  __shared__ float4 ya_[NS][COND / 4], yb_[NS][COND / 4];
+  __shared__ int fc[NS];
   float(*x1)[3 * FIN] = (float(*)[3 * FIN])x1_;
   float(*x2)[3 * COND] = (float(*)[3 * COND])x2_;
   float(*ya)[COND] = (float(*)[COND])ya_;
   float(*yb)[COND] = (float(*)[COND])yb_;
   const int tid = threadIdx.x;
-  const int s0 = blockIdx.x * FRAME_STREAMS;
+  const int s0 = blockIdx.x * NS;
   const uint32_t *rcp = A.rcp;
   unsigned long long t_prev = A.stamps ? __builtin_amdgcn_s_memtime() : 0, t_first = t_prev;
   unsigned long long stp[8] = {};
@@ -137,19 +141,23 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
     }
   };
 
-  if (tid < FRAME_STREAMS) {
+  if (tid < NS) {
     const int sid = s0 + tid;
     fc[tid] = sid < A.nstreams ? A.st[sid].frame_count : 1000;
   }
+  /* this frame's new LPC (host-computed; possibly pinned host memory read
+   * over PCIe): fetched first, used in the epilogue */
+  float lpc_in = 0.f;
+  if (tid < NS * NLPC && s0 + tid / NLPC < A.nstreams) lpc_in = A.lpc_new[(s0 + tid / NLPC) * NLPC + tid % NLPC];
   /* inputs (lpcnet.c:91-99): conv1 window = conv1 memory | features | pitch
    * embedding; conv2 memory.  All loads of a thread in flight, then stores. */
   {
-    constexpr int N1 = (FRAME_STREAMS * 3 * FIN + FK_THREADS - 1) / FK_THREADS;
-    constexpr int N2 = (FRAME_STREAMS * 2 * COND + FK_THREADS - 1) / FK_THREADS;
+    constexpr int N1 = (NS * 3 * FIN + FK_THREADS - 1) / FK_THREADS;
+    constexpr int N2 = (NS * 2 * COND + FK_THREADS - 1) / FK_THREADS;
     float v1[N1], v2[N2];
 #pragma unroll
     for (int q = 0; q < N1; q++) {
-      const int e = min(tid + q * FK_THREADS, FRAME_STREAMS * 3 * FIN - 1);
+      const int e = min(tid + q * FK_THREADS, NS * 3 * FIN - 1);
       const int s = e / (3 * FIN), j = e % (3 * FIN);
       const int sid = min(s0 + s, A.nstreams - 1);
       if (j < 2 * FIN) {
@@ -166,18 +174,18 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
     }
 #pragma unroll
     for (int q = 0; q < N2; q++) {
-      const int e = min(tid + q * FK_THREADS, FRAME_STREAMS * 2 * COND - 1);
+      const int e = min(tid + q * FK_THREADS, NS * 2 * COND - 1);
       v2[q] = A.st[min(s0 + e / (2 * COND), A.nstreams - 1)].conv2_mem[e % (2 * COND)];
     }
 #pragma unroll
     for (int q = 0; q < N1; q++) {
       const int e = tid + q * FK_THREADS;
-      if (e < FRAME_STREAMS * 3 * FIN) x1[e / (3 * FIN)][e % (3 * FIN)] = v1[q];
+      if (e < NS * 3 * FIN) x1[e / (3 * FIN)][e % (3 * FIN)] = v1[q];
     }
 #pragma unroll
     for (int q = 0; q < N2; q++) {
       const int e = tid + q * FK_THREADS;
-      if (e < FRAME_STREAMS * 2 * COND) x2[e / (2 * COND)][e % (2 * COND)] = v2[q];
+      if (e < NS * 2 * COND) x2[e / (2 * COND)][e % (2 * COND)] = v2[q];
     }
   }
   __syncthreads();
@@ -187,17 +195,22 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
    * others wait at the barrier) -- one weight load feeds 4 FMAs, each
    * weight fetched once per workgroup */
   const int i = tid;
-  const float *xs1[4] = {x1[0], x1[1], x1[2], x1[3]};
-  const float *xs2[4] = {x2[0], x2[1], x2[2], x2[3]};
-  const float *xsa[4] = {ya[0], ya[1], ya[2], ya[3]};
-  const float *xsb[4] = {yb[0], yb[1], yb[2], yb[3]};
+  const float *xs1[NS], *xs2[NS], *xsa[NS], *xsb[NS];
+#pragma unroll
+  for (int q = 0; q < NS; q++) {
+    xs1[q] = x1[q];
+    xs2[q] = x2[q];
+    xsa[q] = ya[q];
+    xsb[q] = yb[q];
+  }
   /* conv1 (nnet.c:452-470): 252 inputs -> 128, tanh; cleared while frame_count < 1 (lpcnet.c:99) */
   if (tid < COND) {
-    float a[4];
-    a[0] = a[1] = a[2] = a[3] = A.conv1_b[i];
-    chain_deep<3 * FIN, COND, 4>(A.conv1_w, i, xs1, a);
+    float a[NS];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < NS; q++) a[q] = A.conv1_b[i];
+    chain_deep<3 * FIN, COND, NS>(A.conv1_w, i, xs1, a);
+#pragma unroll
+    for (int q = 0; q < NS; q++) {
       const float t = tanh_x86(a[q], rcp);
       x2[q][2 * COND + i] = fc[q] < 1 ? 0.f : t;
     }
@@ -206,11 +219,12 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
   stamp(1);
   /* conv2: 384 inputs -> 128, tanh; cleared while frame_count < FEATURES_DELAY (lpcnet.c:101) */
   if (tid < COND) {
-    float a[4];
-    a[0] = a[1] = a[2] = a[3] = A.conv2_b[i];
-    chain_deep<3 * COND, COND, 4>(A.conv2_w, i, xs2, a);
+    float a[NS];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < NS; q++) a[q] = A.conv2_b[i];
+    chain_deep<3 * COND, COND, NS>(A.conv2_w, i, xs2, a);
+#pragma unroll
+    for (int q = 0; q < NS; q++) {
       const float t = tanh_x86(a[q], rcp);
       ya[q][i] = fc[q] < FEATURES_DELAY ? 0.f : t;
     }
@@ -218,20 +232,22 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
   __syncthreads();
   stamp(2);
   if (tid < COND) {
-    float a[4];
-    a[0] = a[1] = a[2] = a[3] = A.dense1_b[i];
-    chain_deep<COND, COND, 4>(A.dense1_w, i, xsa, a);
+    float a[NS];
 #pragma unroll
-    for (int q = 0; q < 4; q++) yb[q][i] = tanh_x86(a[q], rcp); /* lpcnet.c:104 */
+    for (int q = 0; q < NS; q++) a[q] = A.dense1_b[i];
+    chain_deep<COND, COND, NS>(A.dense1_w, i, xsa, a);
+#pragma unroll
+    for (int q = 0; q < NS; q++) yb[q][i] = tanh_x86(a[q], rcp); /* lpcnet.c:104 */
   }
   __syncthreads();
   stamp(3);
   if (tid < COND) {
-    float a[4];
-    a[0] = a[1] = a[2] = a[3] = A.dense2_b[i];
-    chain_deep<COND, COND, 4>(A.dense2_w, i, xsb, a);
+    float a[NS];
 #pragma unroll
-    for (int q = 0; q < 4; q++) ya[q][i] = tanh_x86(a[q], rcp); /* lpcnet.c:105 */
+    for (int q = 0; q < NS; q++) a[q] = A.dense2_b[i];
+    chain_deep<COND, COND, NS>(A.dense2_w, i, xsb, a);
+#pragma unroll
+    for (int q = 0; q < NS; q++) ya[q][i] = tanh_x86(a[q], rcp); /* lpcnet.c:105 */
   }
   __syncthreads();
   stamp(4);
@@ -239,17 +255,18 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
    * gru_b_dense_feature as one [128][1200] matrix; thread = row tid + 512p
    * (3 passes), all 4 streams: every weight fetched once per workgroup */
   {
-    const float *xs[4] = {ya[0], ya[1], ya[2], ya[3]};
+    const float *const(&xs)[NS] = xsa;
 #pragma unroll 1
     for (int p = 0; p < (FK_PROJ + FK_THREADS - 1) / FK_THREADS; p++) {
       if (p * FK_THREADS + (tid & ~63) >= FK_PROJ) break; /* whole wave past the end */
       const int row = min(tid + p * FK_THREADS, FK_PROJ - 1);
-      float acc[4];
-      acc[0] = acc[1] = acc[2] = acc[3] = A.proj_b[row];
-      chain_deep<COND, FK_PROJ, 4>(A.proj_w, row, xs, acc);
+      float acc[NS];
+#pragma unroll
+      for (int k = 0; k < NS; k++) acc[k] = A.proj_b[row];
+      chain_deep<COND, FK_PROJ, NS>(A.proj_w, row, xs, acc);
       if (tid + p * FK_THREADS >= FK_PROJ) continue;
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
+      for (int k = 0; k < NS; k++) {
         const int sid = s0 + k;
         if (sid >= A.nstreams) continue;
         if (row < GA_ROWS) A.st[sid].gru_a_cond[row] = acc[k];
@@ -259,16 +276,16 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
   }
   stamp(5);
   /* conv memories (nnet.c:469) */
-  for (int e = tid; e < FRAME_STREAMS * 2 * FIN; e += FK_THREADS) {
+  for (int e = tid; e < NS * 2 * FIN; e += FK_THREADS) {
     const int q = e / (2 * FIN), j = e % (2 * FIN);
     if (s0 + q < A.nstreams) A.st[s0 + q].conv1_mem[j] = x1[q][FIN + j];
   }
-  for (int e = tid; e < FRAME_STREAMS * 2 * COND; e += FK_THREADS) {
+  for (int e = tid; e < NS * 2 * COND; e += FK_THREADS) {
     const int q = e / (2 * COND), j = e % (2 * COND);
     if (s0 + q < A.nstreams) A.st[s0 + q].conv2_mem[j] = x2[q][COND + j];
   }
   /* LPC ring (lpcnet.c:110-118; LPC_GAMMA = 1 -> lpc_weighting multiplies by 1.0f) */
-  if (tid < FRAME_STREAMS * NLPC) {
+  if (tid < NS * NLPC) {
     const int q = tid / NLPC, k = tid % NLPC, sid = s0 + q;
     if (sid < A.nstreams) {
       StreamState *p = &A.st[sid];
@@ -278,11 +295,11 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
       for (int m = 0; m < k; m++) gi *= g;
       p->lpc[k] = cur * gi;
       p->old_lpc[1][k] = nxt;
-      p->old_lpc[0][k] = A.lpc_new[sid * NLPC + k];
+      p->old_lpc[0][k] = lpc_in;
     }
   }
   __syncthreads();
-  if (tid < FRAME_STREAMS) {
+  if (tid < NS) {
     const int sid = s0 + tid;
     if (sid < A.nstreams && fc[tid] < 1000) A.st[sid].frame_count = fc[tid] + 1;
   }
@@ -295,8 +312,12 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
 
 int launch_frame(const FrameArgs &a, void *stream)
 {
-  const int grid = (a.nstreams + FRAME_STREAMS - 1) / FRAME_STREAMS;
-  hipLaunchKernelGGL(frame_kernel, dim3(grid), dim3(FK_THREADS), 0, (hipStream_t)stream, a);
+  if (a.nstreams == 1) {
+    hipLaunchKernelGGL(frame_kernel<1>, dim3(1), dim3(FK_THREADS), 0, (hipStream_t)stream, a);
+  } else {
+    const int grid = (a.nstreams + FRAME_STREAMS - 1) / FRAME_STREAMS;
+    hipLaunchKernelGGL(frame_kernel<FRAME_STREAMS>, dim3(grid), dim3(FK_THREADS), 0, (hipStream_t)stream, a);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

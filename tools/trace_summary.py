@@ -11,14 +11,24 @@ from collections import defaultdict
 
 def main(path, out=None):
     d = defaultdict(list)
+    spans = []
     for r in csv.DictReader(open(path)):
-        d[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        d[r["Kernel_Name"]].append((t1 - t0) / 1e3)
+        spans.append((t0, t1))
     res = {}
     for k, v in d.items():
-        full = [x for x in v if x > 50.0]  # us; silent launches take a few us
+        full = [x for x in v if x > 0.2 * max(v)]  # silent launches return at once
         res[k] = {"launches": len(v), "mean_us_all": sum(v) / len(v),
                   "launches_non_silent": len(full), "mean_us_non_silent": sum(full) / len(full) if full else None,
                   "min_us": min(v), "max_us": max(v)}
+    # idle time of the device between consecutive kernels (host / launch gaps)
+    spans.sort()
+    gaps = [(b[0] - a[1]) / 1e3 for a, b in zip(spans, spans[1:]) if b[0] > a[1]]
+    if gaps:
+        gaps.sort()
+        res["_gaps_between_kernels_us"] = {"count": len(gaps), "median": gaps[len(gaps) // 2],
+                                           "mean": sum(gaps) / len(gaps), "max": gaps[-1]}
     s = json.dumps(res, indent=1)
     print(s)
     if out:
