@@ -37,7 +37,10 @@ def measured_pmc(kernel_prefix):
     FETCH_SIZE/WRITE_SIZE, MFMA busy fraction); PMC counters cannot be read
     in-process.  ({}, None) when no profile matches the kernel."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
+    # a pass just made on this box (tools/gpu_evidence.sh) first, then the committed ones
+    cands = [os.path.join(ROOT, "gpurun_out", "pmc_traffic.json")]
+    cands += sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True)
+    for f in cands:
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
@@ -240,6 +243,11 @@ def main():
         dt2, (k2, n2, _, _), _, _ = run_batch(L, blob32, 1, 0, args.warmup, nf, None, args.timers)
         out["batch1_fp32"] = {"samples_per_s": nf * 160 / dt2, "x_realtime": nf * 160 / dt2 / 16000.0,
                               "ms_per_frame": dt2 / nf * 1e3, "sample_kernel_avg_ms": k2 / max(n2, 1)}
+        # BASELINE configs[2]: 256 streams on one GPU (int8 products on the matrix cores)
+        dt3, (k3, n3, _, _), info3, _ = run_batch(L, blob, 256, 0, args.warmup, nf, None, args.timers)
+        out["batch256"] = {"samples_per_s": 256 * nf * 160 / dt3, "rt_streams": 256 * nf * 160 / dt3 / 16000.0,
+                           "ms_per_frame": dt3 / nf * 1e3, "sample_kernel_avg_ms": k3 / max(n3, 1),
+                           "kernel": info3.kernel_name}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

@@ -40,14 +40,21 @@ namespace lpcnet_mi355x {
 constexpr int FP_SLOTS = NA / 4 + 1; /* column quads of the GRU_A state + one +0 quad (padding) */
 constexpr int FP_HD = 8;             /* h-gate weight blocks in flight per lane */
 constexpr int FP_XD = 3;             /* GRU_A state quads in flight per chain (LDS) */
+#ifndef FP_SAMPLER_HW
+#define FP_SAMPLER_HW 3
+#endif
 /* Hardware wave w runs on SIMD w % 4 (waves w and w+4 share one; wave 3 is
  * alone).  The z/r phase is VALU-issue bound where two GRU_A waves share a
  * SIMD, and GRU_B consumes the GRU_A waves' units in order g = 0..5, each
  * 64 columns (~700 cycles) after the previous: g = 0 gets SIMD 3 to itself,
  * g = 1, 2 share theirs with the least urgent g = 4, 3, and the sampler
  * (busy while the GRU_A waves wait, and vice versa) shares with g = 5. */
-constexpr int FP_SAMPLER_WAVE = 0;
-__device__ __forceinline__ int fp_gru_a_wave(int hw) { return hw == 3 ? 0 : (hw < 3 ? hw : 9 - hw); }
+constexpr int FP_SAMPLER_WAVE = FP_SAMPLER_HW;
+__device__ __forceinline__ int fp_gru_a_wave(int hw)
+{
+  if (FP_SAMPLER_HW == 3) return hw < 3 ? hw : 9 - hw;
+  return hw == 3 ? 0 : (hw < 3 ? hw : 9 - hw);
+}
 constexpr int GB_RING = 8;           /* GRU_B column quads in flight (LDS) */
 
 struct FpLds {

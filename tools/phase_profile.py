@@ -44,10 +44,12 @@ def profile(B, variant=0, kernel=1):
             continue
         print(f"  wave {w}: " + " ".join(f"{NAMES[k][j]}={row[j]:7.0f}" for j in range(6)) + f"  loop={row[6]:7.0f}")
     if k == 5:
-        role = {0: "sampler", 3: "g0", 1: "g1", 2: "g2", 6: "g3", 5: "g4", 4: "g5"}  # fp_gru_a_wave
-        for w in (0, 3, 1, 2, 6, 5, 4):
+        sw = int(os.environ.get("FP_SAMPLER_HW", "3"))  # must match the build
+        role = ({3: "sampler", 0: "g0", 1: "g1", 2: "g2", 6: "g3", 5: "g4", 4: "g5"} if sw == 3 else
+                {0: "sampler", 3: "g0", 1: "g1", 2: "g2", 6: "g3", 5: "g4", 4: "g5"})  # fp_gru_a_wave
+        for w in sorted(role, key=lambda x: (role[x] != "sampler", role[x])):
             row = per[:, w, :].mean(0)
-            names = FP_S if w == 0 else FP_A
+            names = FP_S if role[w] == "sampler" else FP_A
             print(f"  {role[w]:>7}: " + " ".join(f"{v}={row[j]:6.0f}" for j, v in names.items()) + f"  loop={row[6]:7.0f}")
     fs = b.get_frame_stamps().astype(np.float64).mean(0)
     print("  frame kernel (cycles): prologue=%.0f conv1=%.0f conv2=%.0f dense1=%.0f dense2=%.0f proj=%.0f epilogue=%.0f total=%.0f" %
