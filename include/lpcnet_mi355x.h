@@ -140,6 +140,15 @@ LPCNET_EXPORT void lpcnet_mi355x_synthetic_features(unsigned stream, int nframes
 LPCNET_EXPORT float lpcnet_mi355x_lpc_from_cepstrum(float *lpc, const float *cepstrum);
 /* The rcpps table the device activations use (2048 entries). */
 LPCNET_EXPORT const uint32_t *lpcnet_mi355x_rcp_table(void);
+/* Device numerics self-test (diagnostics, not the synthesis path): runs one
+ * routine of the kernels' arithmetic (lpcnet_amd/csrc/device_math.h) on GPU
+ * `device` elementwise over n 32-bit inputs: op 0 tanh8_approx, 1
+ * sigmoid8_approx (vec_avx.h:393-440, emulated rcpps), 2 / 3 the batched
+ * forms of 0 / 1, 4 vector_ps_to_epi8 byte (vec_avx.h:321-336), 5 lin2ulaw
+ * (common.h:47-58), 6 floor(.5 + x) (lpcnet.c:266), 7 _mm256_cvtps_epi32;
+ * op 8: n kiss99 draws (kiss99.c:59-81) from the 4-word state in[0..3].
+ * Returns 0, or -1 on bad arguments / HIP failure. */
+LPCNET_EXPORT int lpcnet_mi355x_device_numerics(int device, int op, const void *in, void *out, int n);
 /* Number of visible HIP devices (0 on a machine without GPU). */
 LPCNET_EXPORT int lpcnet_mi355x_device_count(void);
 /* Last error string of this thread. */

@@ -81,6 +81,7 @@ def _load():
         "lpcnet_mi355x_lpc_from_cepstrum": (f, [vp, vp]),
         "lpcnet_mi355x_rcp_table": (C.POINTER(C.c_uint32), []),
         "lpcnet_mi355x_device_count": (i, []),
+        "lpcnet_mi355x_device_numerics": (i, [i, i, vp, vp, i]),
         "lpcnet_mi355x_last_error": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
@@ -119,6 +120,17 @@ class ModelInfo(C.Structure):
 
 def last_error() -> str:
     return (lib.lpcnet_mi355x_last_error() or b"").decode()
+
+
+def device_numerics(op: int, x: np.ndarray, n: int | None = None, device: int = 0) -> np.ndarray:
+    """Run one device-numerics routine (see lpcnet_mi355x_device_numerics)
+    on the GPU; x is reinterpreted as 32-bit words, the result is uint32."""
+    src = np.ascontiguousarray(x).view(np.uint32)
+    cnt = int(n if n is not None else src.size)
+    out = np.zeros(cnt, np.uint32)
+    if lib.lpcnet_mi355x_device_numerics(device, op, src.ctypes.data, out.ctypes.data, cnt) != 0:
+        raise LPCNetError("device numerics failed: " + last_error())
+    return out
 
 
 def device_count() -> int:

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include "device_math.h"
+#include "lds_flags.h"
 #include "lpcnet_engine.h"
 #include "sampler.h"
 
@@ -67,35 +68,6 @@ struct FpLds {
 };
 
 int fp_lds_bytes() { return IMG_VAR + FpLds::total; }
-
-/* LDS flags: the data they publish is in LDS, so ordering needs only the
- * writer's LDS queue drained before the flag store (lgkmcnt) and the
- * reader's dependent branch before its data reads. */
-__device__ __forceinline__ int flag_load(const int *p)
-{
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-/* Spin until *p >= v.  A wait that outlives FLAG_SPIN_LIMIT polls (a bug,
- * never a legal schedule) sets the workgroup's abort word, after which every
- * wait returns at once: the kernel then finishes with wrong output instead
- * of hanging the device. */
-constexpr int FLAG_SPIN_LIMIT = 1 << 20;
-__device__ __forceinline__ void flag_wait(const int *p, int v, int *abort_w)
-{
-  for (int it = 0; flag_load(p) < v; it++) {
-    if (flag_load(abort_w)) break;
-    if (it > FLAG_SPIN_LIMIT) {
-      __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      break;
-    }
-  }
-  asm volatile("" ::: "memory");
-}
-__device__ __forceinline__ void flag_publish(int *p, int v)
-{
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 /* Keep packed offsets packed: without this the compiler hoists every
  * unpacked offset out of the sample loop (one register per slot). */
@@ -302,7 +274,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
         xr[d] = fp_xv(xp, orr, d);
       }
       stamp(5);
-      flag_wait(ixseq, n + 1, abort_w);
+      flag_wait<1>(ixseq, n + 1, abort_w);
       stamp(0);
       /* GRU_A input (nnet.c:484-491): the 9 embedding gathers of this unit */
       float e[9];

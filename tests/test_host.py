@@ -91,3 +91,10 @@ def test_kernel_float_identities_exhaustive(tmp_path):
     r = subprocess.run([str(exe), os.path.join(ROOT, "tests", "golden", "rcp_x86.bin")], capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stdout
+
+
+def test_device_numerics_rejects_bad_arguments():
+    """Argument checks happen before any HIP call (no GPU needed)."""
+    assert L.lib.lpcnet_mi355x_device_numerics(0, 99, None, None, 1) == -1
+    assert L.lib.lpcnet_mi355x_device_numerics(0, 0, None, None, 4) == -1
+    assert L.lib.lpcnet_mi355x_device_numerics(0, 0, None, None, 0) == 0
