@@ -75,7 +75,10 @@ def dist_setup(args):
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # RCCL over xGMI carries only the barrier and the max-reduction of the
+        # timed interval (no data-path collective); LPCNET_DIST_BACKEND=gloo
+        # rehearses several ranks on one GPU
+        backend = os.environ.get("LPCNET_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
@@ -110,7 +113,8 @@ def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1)
     extra = min(steps, 8)
     feats = np.stack([L.synthetic_features(stream_base + s, F)[:, :20] for s in range(B)], 1)
     feats = np.ascontiguousarray(feats, np.float32)  # [F][B][20]
-    b = L.LPCNetBatch(B, int(os.environ.get("LOCAL_RANK", "0")), blob)
+    ndev = max(1, L.device_count())
+    b = L.LPCNetBatch(B, int(os.environ.get("LOCAL_RANK", "0")) % ndev, blob)
     d_feat = b.device_alloc(feats.nbytes)
     d_pcm = b.device_alloc((F + extra) * B * 160 * 2)
     b.h2d(d_feat, feats)

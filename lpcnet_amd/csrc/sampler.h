@@ -101,21 +101,32 @@ __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, floa
       val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
     }
   }
-  float sp_pcm = 0.f, sp_pred = 0.f;
-  int sp_idx = 0;
-  if (teach == nullptr) {
-    sp_pcm = pred + F.ulaw[(val << 4) | (F.hl & 15)];
-    float p2 = 0.f - sp_pcm * lpr[0];
-#pragma unroll
-    for (int j = 1; j < NLPC; j++) p2 = p2 - lsr[j - 1] * lpr[j];
-    sp_pred = p2;
-    sp_idx = lin2ulaw_x86(sp_pcm) | (lin2ulaw_x86(sp_pred) << 8);
-  }
+  /* level 4..7 node of this lane under the chosen prefix: its parameters
+   * are loaded first, so their LDS latency overlaps the speculation below
+   * (one basic block: the speculation is computed unconditionally and simply
+   * unused when teaching, a branch would serialise the two) */
+  const int lvl = 4 + F.lvl_in;
+  const int node = (1 << lvl) | (val << (lvl - 4)) | (F.qq + 1 - (1 << (lvl - 4)));
+  const float b47 = F.fcb[F.ch2 * 256 + node], f47 = F.fcf[F.ch2 * 256 + node];
+  float w47[NB];
   {
-    const int lvl = 4 + F.lvl_in;
-    const int off = F.qq + 1 - (1 << (lvl - 4));
-    const int node = (1 << lvl) | (val << (lvl - 4)) | off;
-    const float l = F.node_logit(F.fcb[F.ch2 * 256 + node], F.fcf[F.ch2 * 256 + node], F.fcw + node * 32 + F.ch2 * 16, xv);
+    const float4 *w4 = (const float4 *)(F.fcw + node * 32 + F.ch2 * 16);
+#pragma unroll
+    for (int j = 0; j < NB / 4; j++) {
+      const float4 v = w4[j];
+      w47[4 * j] = v.x; w47[4 * j + 1] = v.y; w47[4 * j + 2] = v.z; w47[4 * j + 3] = v.w;
+    }
+  }
+  /* candidate exc = 16*prefix + (hl & 15): output sample, pred(n+1), u-law
+   * indices (lpcnet.c:252-261), the reference's operations in order */
+  const float sp_pcm = pred + F.ulaw[(val << 4) | (F.hl & 15)];
+  float p2 = 0.f - sp_pcm * lpr[0];
+#pragma unroll
+  for (int j = 1; j < NLPC; j++) p2 = p2 - lsr[j - 1] * lpr[j];
+  const float sp_pred = p2;
+  const int sp_idx = lin2ulaw_x86(sp_pcm) | (lin2ulaw_x86(sp_pred) << 8);
+  {
+    const float l = F.node_logit(b47, f47, w47, xv);
     const unsigned long long m = __ballot(t47 < l) >> F.hb;
 #pragma unroll
     for (int b = 4; b < 8; b++) {
