@@ -21,7 +21,10 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblpcnet_mi355x.so")
+# LPCNET_LIB_VARIANT=<name> loads liblpcnet_mi355x_<name>.so from this
+# directory instead (in-tree A/B builds; still the native library, never a fallback)
+LIB_PATH = os.path.join(_HERE, "liblpcnet_mi355x%s.so" % (
+    "_" + os.environ["LPCNET_LIB_VARIANT"] if os.environ.get("LPCNET_LIB_VARIANT") else ""))
 
 NB_FEATURES = 20
 NB_TOTAL_FEATURES = 36
