@@ -28,111 +28,10 @@
 
 #include "device_math.h"
 #include "lpcnet_engine.h"
+#include "mf_common.h"
 #include "sampler.h"
 
 namespace lpcnet_mi355x {
-
-typedef int v4i __attribute__((ext_vector_type(4)));
-
-/* Keep packed offsets packed: without this the compiler hoists every
- * unpacked 16-bit offset out of the sample loop (one VGPR per slot). */
-template <int N>
-__device__ __forceinline__ void mf_opaque(uint32_t (&o)[N])
-{
-#pragma unroll
-  for (int k = 0; k < N; k++) asm volatile("" : "+v"(o[k]));
-}
-
-/* x word of slot t: the packed 16-bit LDS byte offsets o[t/2] */
-template <int NO>
-__device__ __forceinline__ uint32_t mf_x(const unsigned char *lds, const uint32_t (&o)[NO], int t)
-{
-  return *(const uint32_t *)(lds + ((o[t >> 1] >> (16 * (t & 1))) & 0xFFFF));
-}
-
-/* v_mfma_i32_4x4x4_16b_i8, 16 blocks: block b = lanes 4b..4b+3.
- * A (src0) lane 4b+m: 4 int8 of row m (= stream m's x quad of the block's
- * column block); B (src1) lane 4b+n: 4 int8 of column n (= weight row n);
- * D lane 4b+n, register m: sum over k of A[m][k] B[k][n] (exact int32).
- * Layout measured on gfx950 (tools/probes/mfma_i8_probe.hip). */
-__device__ __forceinline__ v4i mfma4(uint32_t x, uint32_t w, v4i acc)
-{
-  return __builtin_amdgcn_mfma_i32_4x4x4i8((int)x, (int)w, acc, 0, 0, 0);
-}
-
-/* GRU_A z and r products over ng 4-slot groups (wave-uniform ng): the two
- * gates interleave (independent accumulators), x words of group g+1 are
- * read from LDS while the MFMAs of group g run. */
-__device__ __forceinline__ void mf_zr(const unsigned char *lds, const uint32_t (&wz)[MF_ZMAX],
-                                      const uint32_t (&wr)[MF_ZMAX], const uint32_t (&oz)[MF_ZMAX / 2],
-                                      const uint32_t (&orr)[MF_ZMAX / 2], int ng, v4i &az, v4i &ar)
-{
-  uint32_t xz[4], xr[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    xz[k] = mf_x(lds, oz, k);
-    xr[k] = mf_x(lds, orr, k);
-  }
-#pragma unroll
-  for (int g = 0; g < MF_ZMAX / 4; g++) {
-    if (g < ng) {
-      uint32_t nz[4], nr[4];
-      if (g + 1 < MF_ZMAX / 4 && g + 1 < ng) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          nz[k] = mf_x(lds, oz, 4 * (g + 1) + k);
-          nr[k] = mf_x(lds, orr, 4 * (g + 1) + k);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        az = mfma4(xz[k], wz[4 * g + k], az);
-        ar = mfma4(xr[k], wr[4 * g + k], ar);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        xz[k] = nz[k];
-        xr[k] = nr[k];
-      }
-    }
-  }
-}
-
-/* NS-slot product over ng 4-slot groups, alternating two accumulators */
-template <int NS>
-__device__ __forceinline__ void mf_run(const unsigned char *lds, const uint32_t (&w)[NS], const uint32_t (&o)[NS / 2],
-                                       int ng, v4i &a0, v4i &a1)
-{
-  uint32_t x[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) x[k] = mf_x(lds, o, k);
-#pragma unroll
-  for (int g = 0; g < NS / 4; g++) {
-    if (g < ng) {
-      uint32_t n[4];
-      if (g + 1 < NS / 4 && g + 1 < ng) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) n[k] = mf_x(lds, o, 4 * (g + 1) + k);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        if (k & 1) a1 = mfma4(x[k], w[4 * g + k], a1);
-        else a0 = mfma4(x[k], w[4 * g + k], a0);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) x[k] = n[k];
-    }
-  }
-}
-
-/* v_mfma_i32_16x16x64_i8: A (src0) lane l = row l%16, B (src1) lane l =
- * column l%16, the 16 bytes of both = k 16(l/16) + 0..15 (any k permutation
- * common to A and B is the same product); D lane l register i = row
- * 4(l/16)+i, column l%16 (tools/probes/mfma16_probe.hip). */
-__device__ __forceinline__ v4i mfma16(const v4i &w, const v4i &x, v4i acc)
-{
-  return __builtin_amdgcn_mfma_i32_16x16x64_i8(w, x, acc, 0, 0, 0);
-}
 
 template <int S>
 struct MfLds {
@@ -268,16 +167,16 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     int az[S], ar[S], ah[S];
     float tz[S], tr[S], hpre[S];
     auto recurrent = [&]() {
-      v4i vz = {wsz, wsz, wsz, wsz}, vr = {wsr, wsr, wsr, wsr}, vh0 = {wsh, wsh, wsh, wsh}, vh1 = {0, 0, 0, 0};
+      v4i vz[1] = {{wsz, wsz, wsz, wsz}}, vr[1] = {{wsr, wsr, wsr, wsr}}, vh[2] = {{wsh, wsh, wsh, wsh}, {0, 0, 0, 0}};
       mf_opaque(oz);
       mf_opaque(orr);
       mf_opaque(oh);
-      mf_zr(lds, wz, wr, oz, orr, nzr, vz, vr);
-      mf_run<MF_HMAX>(lds, wh, oh, nh, vh0, vh1);
+      mf_zr<1>(lds, wz, wr, oz, orr, nzr, vz, vr);
+      mf_run<MF_HMAX, 2>(lds, wh, oh, nh, vh);
       for (int s = 0; s < S; s++) {
-        az[s] = vz[s];
-        ar[s] = vr[s];
-        ah[s] = vh0[s] + vh1[s];
+        az[s] = vz[0][s];
+        ar[s] = vr[0][s];
+        ah[s] = vh[0][s] + vh[1][s];
         tz[s] = bz + dz * st[s];
         tr[s] = br + dr * st[s];
         hpre[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
