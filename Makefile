@@ -14,7 +14,7 @@ LIB := lpcnet_amd/liblpcnet_mi355x.so
 CSRC := lpcnet_amd/csrc
 HDRS := include/lpcnet.h include/lpcnet_mi355x.h $(CSRC)/lpcnet_engine.h $(CSRC)/device_math.h $(CSRC)/sampler.h $(CSRC)/lds_flags.h $(CSRC)/mf_common.h $(CSRC)/rcp_table_x86.inc
 COMMON := -O3 -fPIC -ffp-contract=off -fno-fast-math -std=c++17 -Iinclude -I$(CSRC) -fvisibility=hidden -Wall -Wno-unused-function
-OBJS := $(BUILD)/kernels.o $(BUILD)/mf_kernel.o $(BUILD)/mfp_kernel.o $(BUILD)/fp_kernel.o $(BUILD)/selftest.o $(BUILD)/frame_kernel.o $(BUILD)/engine.o $(BUILD)/lpc_host.o $(BUILD)/model_gen.o
+OBJS := $(BUILD)/kernels.o $(BUILD)/mf_kernel.o $(BUILD)/fp_kernel.o $(BUILD)/selftest.o $(BUILD)/frame_kernel.o $(BUILD)/engine.o $(BUILD)/lpc_host.o $(BUILD)/model_gen.o
 
 all: lib oracle
 
@@ -30,9 +30,6 @@ $(BUILD)/frame_kernel.o: $(CSRC)/frame_kernel.hip $(HDRS) | $(BUILD)
 	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -c $< -o $@
 
 $(BUILD)/mf_kernel.o: $(CSRC)/mf_kernel.hip $(HDRS) | $(BUILD)
-	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -c $< -o $@
-
-$(BUILD)/mfp_kernel.o: $(CSRC)/mfp_kernel.hip $(HDRS) | $(BUILD)
 	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -c $< -o $@
 
 $(BUILD)/fp_kernel.o: $(CSRC)/fp_kernel.hip $(HDRS) | $(BUILD)

@@ -34,8 +34,7 @@ typedef struct {
   double ops_per_sample;          /* 2*MAC per stream per sample */
   int streams_per_workgroup;      /* streams per sample-kernel workgroup */
   int quad_path;                  /* 0 per-slot LDS, 1 quad LDS (lockstep), 2 wave-per-stream, 3 pipelined,
-                                     4 pipelined on the matrix cores, 5 fp32 latency kernel,
-                                     6 two-group matrix-core kernel */
+                                     4 pipelined on the matrix cores, 5 fp32 latency kernel */
   int lds_bytes;                  /* dynamic LDS of the sample kernel */
   double mfma_ops_per_group_sample; /* int8 matrix-core ops issued per workgroup per sample
                                        (mf_kernel; padding included), 0 otherwise */
@@ -56,11 +55,8 @@ LPCNET_EXPORT int lpcnet_batch_model_info(const LPCNetBatch *b, LPCNetModelInfo 
  * register tables; otherwise mode 3 rules apply), 5 the fp32 latency
  * kernel (fp32 models with a dense GRU_B whose blocks fit its register
  * tables; int8 models fall back to mode 4 rules, other fp32 models to the
- * lockstep kernel), 6 the matrix-core kernel with its 4 streams per
- * workgroup run as two groups half a sample apart (mode 4 rules, and
- * 4 streams per workgroup, i.e. >= 1024 streams; otherwise mode 4).
- * Automatic: 5 for fp32 models, 6 or 4 for int8 where they apply.  Results
- * are identical; only speed differs. */
+ * lockstep kernel).  Automatic: 5 for fp32 models, 4 for int8 where they
+ * apply.  Results are identical; only speed differs. */
 LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode);
 /* lpcnet_reset() on every stream / on one stream. */
 LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b);

@@ -117,8 +117,6 @@ class ModelInfo(C.Structure):
             return f"mf_kernel<{self.streams_per_workgroup}, false>"
         if self.quad_path == 5:
             return "fp_kernel<false>"
-        if self.quad_path == 6:
-            return "mfp_kernel<false>"
         quad = "true" if self.quad_path == 1 else "false"
         return f"sample_kernel<{self.streams_per_workgroup}, {self.variant}, {sat}, {quad}>"
 
@@ -223,7 +221,7 @@ class LPCNetBatch:
 
     def set_kernel(self, mode: int) -> None:
         """0 automatic, 1 lockstep sample kernel, 2 wave-per-stream kernel, 3 pipelined kernel,
-        4 matrix-core pipelined kernel, 5 fp32 latency kernel, 6 two-group matrix-core kernel
+        4 matrix-core pipelined kernel, 5 fp32 latency kernel
         (unavailable modes fall back)."""
         if lib.lpcnet_batch_set_kernel(self._b, mode) != 0:
             raise LPCNetError("bad kernel mode")

@@ -287,13 +287,12 @@ struct LPCNetBatch {
   bool sat = false;
   bool reg = false;
   int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 2 wave_kernel, 3 pipe_kernel, 4 matrix-core pipe_kernel,
-                            5 fp32 latency kernel, 6 two-group matrix-core kernel */
+                            5 fp32 latency kernel */
   int wave_nw = 0;       /* >0: wave_kernel with this many streams per workgroup */
   bool pipe = false;     /* pipe_kernel (mode 3) */
   bool mf_ok = false;    /* model fits the matrix-core register tables */
   bool mf = false;       /* mf_kernel (mode 4) */
-  bool mfp = false;      /* mfp_kernel (mode 6) */
-  double mf_ga_ops = 0;  /* int8 matrix-core ops per workgroup per sample: one GRU_A recurrent pass */
+  double mf_ga_ops = 0;  /* int8 matrix-core ops per workgroup per sample: the GRU_A recurrent pass */
   double mf_gb_ops = 0;  /* the GRU_B tiles of both sampler waves */
   bool fp_ok = false;    /* fp32 model fits the fp_kernel tables */
   bool fp = false;       /* fp_kernel (mode 5) */
@@ -384,7 +383,6 @@ void choose_kernel(LPCNetBatch *b)
   b->wave_nw = 0;
   b->pipe = false;
   b->mf = false;
-  b->mfp = false;
   b->info.mfma_ops_per_group_sample = b->mf_ga_ops + b->mf_gb_ops;
   b->fp = false;
   const bool quad_int8 = b->variant == LPCNET_VARIANT_INT8 && b->reg;
@@ -398,15 +396,6 @@ void choose_kernel(LPCNetBatch *b)
     return;
   }
   if (mode == 5) mode = b->mf_ok ? 4 : (quad_int8 ? 3 : 1);
-  if (mode == 6 && b->mf_ok && b->S == 4 && mfp_lds_bytes() <= 160 * 1024) {
-    b->mfp = true;
-    b->info.streams_per_workgroup = 4;
-    b->info.lds_bytes = mfp_lds_bytes();
-    b->info.quad_path = 6;
-    b->info.mfma_ops_per_group_sample = 2.0 * b->mf_ga_ops + b->mf_gb_ops;
-    return;
-  }
-  if (mode == 6) mode = 4;
   if (mode == 4 && b->mf_ok && mf_lds_bytes(b->S) <= 160 * 1024) {
     b->mf = true;
     b->info.streams_per_workgroup = b->S;
@@ -894,7 +883,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   in.bytes_per_stream_sample = 3.0 * GA_ROWS * 4 /* embedding rows */ + 8 * (32 + 2 * 4 + 2 * 4) /* dual_fc path */ + 2;
   /* mf_kernel matrix-core work: per GRU_A wave 8 nzr + 4 nh 4x4x4 MFMAs of
    * 16 x 4x4x4 MACs; per sampler wave 21 16x16x64 MFMAs (2 sampler waves).
-   * mfp_kernel runs the GRU_A pass once per group (choose_kernel). */
+   */
   b->mf_ga_ops = b->mf_gb_ops = 0;
   if (mf_ok) {
     double n4 = 0;
@@ -962,7 +951,6 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   const int lrc = N <= 0 ? 0
                 : b->fp    ? launch_fp(sa, b->stream)
-                : b->mfp   ? launch_mfp(sa, b->stream)
                 : b->mf    ? launch_mf(sa, b->S, b->info.lds_bytes, b->stream)
                 : b->pipe  ? launch_pipe(sa, b->S, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
                 : b->wave_nw ? launch_wave(sa, b->wave_nw, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
@@ -1082,7 +1070,7 @@ LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *d
 
 LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode)
 {
-  if (!b || mode < 0 || mode > 6) return -1;
+  if (!b || mode < 0 || mode > 5) return -1;
   b->kernel_mode = mode;
   if (b->have_model) choose_kernel(b);
   return 0;

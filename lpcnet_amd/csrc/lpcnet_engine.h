@@ -177,11 +177,6 @@ int launch_pipe(const SampleArgs &a, int S, int sat, int lds_bytes, void *stream
  * workgroup barriers per sample. */
 int mf_lds_bytes(int S);
 int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream);
-/* Two-group matrix-core kernel (mf_kernel's roles and arithmetic, 4 streams
- * per workgroup as two groups half a sample apart, LDS flags instead of
- * barriers). */
-int mfp_lds_bytes();
-int launch_mfp(const SampleArgs &a, void *stream);
 /* fp32 latency kernel: one stream per workgroup, LDS flags instead of
  * workgroup barriers (fp32 models within the FP_* limits, dense GRU_B). */
 int fp_lds_bytes();

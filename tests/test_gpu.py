@@ -90,8 +90,7 @@ def test_single_stream_api_matches_golden(require_gpu, blobs):
                                             (1101, (1100, 1024, 5), 0), (300, (299, 7), 2),
                                             (513, (512, 1, 300), 3), (1030, (1029, 1027, 2), 3),
                                             (513, (512, 1, 300), 4), (1030, (1029, 1027, 2), 4),
-                                            (1024, (0, 511, 1023), 4), (1030, (1029, 1027, 2), 6),
-                                            (2048, (0, 1029, 2047), 6)])
+                                            (1024, (0, 511, 1023), 4)])
 def test_large_batch_streams_match_oracle(require_gpu, blobs, B, check, kernel):
     """Lockstep kernel at 2 and 4 streams/workgroup, the wave-per-stream kernel
     (auto at >= 256 streams), ragged last workgroups, against the oracle."""
@@ -108,55 +107,43 @@ def test_large_batch_streams_match_oracle(require_gpu, blobs, B, check, kernel):
     assert np.abs(out[:, 2:]).mean() > 100
 
 
-def test_two_group_kernel_edge_cases(require_gpu, blobs):
-    """mfp_kernel (two stream groups half a sample apart) at 1026 streams
-    (ragged last workgroup): odd N, a per-stream reset, teacher forcing and
-    the per-sample trace, against the oracle on sampled streams and against
-    mf_kernel (itself pinned by the golden fixtures) on every stream."""
+def test_matrix_core_kernel_edge_cases_at_bench_size(require_gpu, blobs):
+    """mf_kernel at 4 streams per workgroup (1026 streams: ragged last
+    workgroup) through odd N, teacher forcing, a per-stream reset and the
+    per-sample trace (logits bit for bit, excitation), against the oracle on
+    streams of the first, a middle and the ragged workgroup; final GRU states."""
     B, F = 1026, 7
     blob = blobs["streams_int8"]
     allf = np.stack([feats(s, F) for s in range(B)], 1)
-    check = (0, 1, 2, 3, 517, 1025)
-    runs = {}
-    for kernel in (6, 4):
-        b = L.LPCNetBatch(B, 0, blob)
-        b.set_kernel(kernel)
-        assert b.info().quad_path == kernel
-        b.set_trace(True)
-        refs = {s: O.Oracle(blob, 0) for s in check} if kernel == 6 else None
-        t = np.arange(160)
-        outs, traces = [], []
-        for f in range(F):
-            if f == 5:
-                b.reset(2)
-                if refs:
-                    refs[2] = O.Oracle(blob, 0)
-            if f == 4:
-                teacher = np.stack([(2500 * np.sin(0.03 * (s % 7 + 1) * t)).astype(np.int16) for s in range(B)])
-                out = b.synthesize_impl(allf[f], teacher, 77)
-                if refs:
-                    for s in check:
-                        exp = refs[s].synthesize(allf[f, s], 160, preload=teacher[s][:77])
-                        assert np.array_equal(out[s, 77:], exp[77:]), (f, s)
-            else:
-                n = 81 if f == 3 else 160
-                out = b.synthesize(allf[f], n)
-                if refs:
-                    for s in check:
-                        assert np.array_equal(out[s], refs[s].synthesize(allf[f, s], n)), (f, s)
-            outs.append(out.copy())
-            if f >= 2:
-                lg, ex = b.get_trace(out.shape[1])
-                traces.append((bits(lg).copy(), ex.copy()))
-        runs[kernel] = (outs, traces, [b.get_state(s) for s in check])
+    check = (0, 1, 2, 3, 517, 1024, 1025)
+    b = L.LPCNetBatch(B, 0, blob)
+    b.set_kernel(4)
+    assert b.info().quad_path == 4 and b.info().streams_per_workgroup == 4
+    b.set_trace(True)
+    refs = {s: O.Oracle(blob, 0) for s in check}
+    t = np.arange(160)
     for f in range(F):
-        assert np.array_equal(runs[6][0][f], runs[4][0][f]), f
-    for (l6, e6), (l4, e4) in zip(runs[6][1], runs[4][1]):
-        assert np.array_equal(e6, e4)
-        assert np.array_equal(l6, l4)
-    for a, c in zip(runs[6][2], runs[4][2]):
-        for k in ("gru_a_state", "gru_b_state"):
-            assert np.array_equal(bits(a[k]), bits(c[k])), k
+        if f == 5:
+            b.reset(2)
+            refs[2] = O.Oracle(blob, 0)
+        pre, n = (77, 160) if f == 4 else (0, 81 if f == 3 else 160)
+        if pre:
+            teacher = np.stack([(2500 * np.sin(0.03 * (s % 7 + 1) * t)).astype(np.int16) for s in range(B)])
+            out = b.synthesize_impl(allf[f], teacher, pre)
+        else:
+            out = b.synthesize(allf[f], n)
+        lg, ex = b.get_trace(n)
+        for s in check:
+            exp, elg, eex, _ = refs[s].synthesize(allf[f, s], n, preload=teacher[s][:pre] if pre else None, trace=True)
+            assert np.array_equal(out[s], exp), (f, s)
+            if f >= 2:
+                assert np.array_equal(ex[s, pre:], eex[pre:]), (f, s)
+                assert np.array_equal(bits(lg[s, pre:]), bits(elg[pre:])), (f, s)
+    for s in check:
+        a, g = refs[s].state()
+        st = b.get_state(s)
+        assert np.array_equal(bits(st["gru_a_state"]), bits(a)), s
+        assert np.array_equal(bits(st["gru_b_state"]), bits(g)), s
 
 
 @pytest.mark.parametrize("B,check", [(1, (0,)), (70, (0, 37, 69))])

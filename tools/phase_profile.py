@@ -16,10 +16,6 @@ NAMES = {1: ["B(gru_a)", "wait1", "C(gru_b)", "wait2", "F(sample)", "wait3"],
 # fp_kernel stamps (index: name), GRU_A waves / sampler wave
 FP_A = {5: "top", 0: "wait_ix", 1: "gathers", 2: "zr_chain", 3: "elem+pub", 4: "wait_all", 8: "h_chain"}
 FP_S = {0: "pre", 1: "wait_w0", 2: "gru_b", 3: "elem+bcast", 4: "walk+pub", 8: "post"}
-# mfp_kernel stamps (summed over both groups on the GRU_A waves)
-MFP_A = {5: "wait_ix", 10: "gathers", 0: "elem+pub", 3: "wait_all", 2: "mv"}
-MFP_S = {13: "finish", 0: "draws+rec", 1: "wait_h", 10: "mfma", 14: "sig", 8: "tanh+", 9: "bcast", 11: "walk",
-         12: "post"}
 
 
 def profile(B, variant=0, kernel=1):
@@ -38,18 +34,11 @@ def profile(B, variant=0, kernel=1):
     n = max(st[:, :, 7].max(), 1)
     per = st / n  # cycles per sample
     info = b.info()
-    k = {3: 3, 4: 4, 5: 5, 6: 6}.get(info.quad_path, 1)
+    k = {3: 3, 4: 4, 5: 5}.get(info.quad_path, 1)
     print(f"B={B} variant={variant} kernel={info.kernel_name} groups={st.shape[0]}"
           f"  sample kernel {kms / max(kn, 1) * 1e3:.0f} us -> s_memtime rate "
           f"{st[:, :, 6].max() / max(kms / max(kn, 1), 1e-9) / 1e6:.2f} GHz (stamped run)")
-    if k == 6:
-        for w in range(8):
-            row = per[:, w, :].mean(0)
-            names = MFP_A if w < 6 else MFP_S
-            print(f"  wave {w}: " + " ".join(f"{v}={row[j]:6.0f}" for j, v in names.items()) + f"  loop={row[6]:7.0f}")
-        if st[:, :, 15].any():
-            print("  ABORT flag set in %d workgroups" % int((st[:, :, 15] > 0).any(1).sum()))
-    for w in range(8 if k not in (5, 6) else 0):
+    for w in range(8 if k != 5 else 0):
         row = per[:, w, :].mean(0)
         if row[6] == 0:
             continue
@@ -84,7 +73,7 @@ if __name__ == "__main__":
         if kern == 5:
             profile(1, 1, 5)
             continue
-        for B in ((1024,) if kern == 6 else (1, 1024)):
+        for B in (1, 1024):
             profile(B, 0, kern)
     if len(sys.argv) <= 2 or sys.argv[2] != "nofp32":
         profile(1, 1)
