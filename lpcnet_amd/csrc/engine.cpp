@@ -311,6 +311,13 @@ struct LPCNetBatch {
   float *h_lpc_dev[2] = {nullptr, nullptr}; /* device view of the pinned h_lpc */
   hipEvent_t ev_lpc[2] = {nullptr, nullptr};
   bool ev_lpc_used[2] = {false, false};
+  /* overlapped multi-frame path (few streams, free CUs): frame kernel f+1 on
+   * fstream beside sample kernel f on stream, outputs double-buffered in
+   * d_cond[f & 1] */
+  hipStream_t fstream = nullptr;
+  FrameCond *d_cond[2] = {nullptr, nullptr};
+  hipEvent_t ev_frame[2] = {nullptr, nullptr}, ev_samp[2] = {nullptr, nullptr}, ev_start = nullptr;
+  bool ev_samp_used[2] = {false, false};
   /* trace */
   bool trace = false;
   float *d_trace_logits = nullptr;
@@ -923,8 +930,17 @@ int ensure_trace(LPCNetBatch *b, int N)
   return 0;
 }
 
-int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lpc, short *d_pcm, int N, int preload = 0)
+/* ovl >= 0: overlapped form, frame f = ovl.  The frame kernel runs on
+ * fstream, followed by a copy of its outputs into d_cond[f & 1] (which
+ * sample kernel f-2 read: ev_samp); the sample kernel on stream waits only
+ * for that copy (ev_frame) and reads the frame's outputs there, so frame
+ * kernel f+1 runs beside sample kernel f.  The sample kernels read nothing
+ * else the frame kernel writes. */
+int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lpc, short *d_pcm, int N, int preload = 0,
+                      int ovl = -1)
 {
+  const int c = ovl & 1;
+  hipStream_t fs = ovl >= 0 ? b->fstream : b->stream;
   FrameArgs fa = b->fa;
   fa.st = b->d_state;
   fa.nstreams = b->B;
@@ -938,6 +954,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   sa.preload = std::max(0, std::min(preload, N));
   sa.stamps = b->d_stamps;
   fa.stamps = b->d_stamps ? b->d_stamps + (size_t)b->B * STAMP_WAVES * 16 : nullptr;
+  if (ovl >= 0) sa.cond = b->d_cond[c];
   /* timing 1: events around the sample kernel only; 2: the frame kernel too
    * (one event between the two kernels serves both pairs) */
   hipEvent_t e[3] = {nullptr, nullptr, nullptr};
@@ -946,8 +963,19 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
     e[1] = get_event(b);
     e[2] = get_event(b);
   }
-  if (e[0]) HIPCHK(hipEventRecord(e[0], b->stream));
-  if (launch_frame(fa, b->stream)) { set_err("frame kernel launch failed"); return -1; }
+  if (ovl >= 0 && b->ev_samp_used[c]) HIPCHK(hipStreamWaitEvent(fs, b->ev_samp[c], 0));
+  hipEvent_t ef = nullptr; /* end of the frame kernel, overlapped form with frame timing */
+  if (e[0]) HIPCHK(hipEventRecord(e[0], fs));
+  if (launch_frame(fa, fs)) { set_err("frame kernel launch failed"); return -1; }
+  if (ovl >= 0 && launch_cond_copy(b->d_state, b->d_cond[c], b->B, fs)) { set_err("copy launch failed"); return -1; }
+  if (ovl >= 0) {
+    if (e[0]) {
+      ef = get_event(b);
+      HIPCHK(hipEventRecord(ef, fs));
+    }
+    HIPCHK(hipEventRecord(b->ev_frame[c], fs));
+    HIPCHK(hipStreamWaitEvent(b->stream, b->ev_frame[c], 0));
+  }
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   const int lrc = N <= 0 ? 0
                 : b->fp    ? launch_fp(sa, b->stream)
@@ -960,10 +988,15 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
     return -1;
   }
   if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
+  if (ovl >= 0) {
+    HIPCHK(hipEventRecord(b->ev_samp[c], b->stream));
+    b->ev_samp_used[c] = true;
+  }
   if (e[0]) {
     b->ev_pairs[1].push_back(e[0]);
-    b->ev_pairs[1].push_back(e[1]);
+    b->ev_pairs[1].push_back(ef ? ef : e[1]);
   }
+  if (ef) b->ev_taken.push_back(ef);
   if (e[1]) {
     b->ev_pairs[0].push_back(e[1]);
     b->ev_pairs[0].push_back(e[2]);
@@ -1025,6 +1058,15 @@ LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
     ok = ok && hipHostGetDevicePointer((void **)&b->h_lpc_dev[i], b->h_lpc[i], 0) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&b->ev_lpc[i], hipEventDisableTiming) == hipSuccess;
   }
+  if (ok && nb_streams <= OVERLAP_MAX_STREAMS) {
+    ok = ok && hipStreamCreateWithFlags(&b->fstream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&b->ev_start, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < 2 && ok; i++) {
+      ok = ok && hipMalloc(&b->d_cond[i], sizeof(FrameCond) * (size_t)nb_streams) == hipSuccess;
+      ok = ok && hipEventCreateWithFlags(&b->ev_frame[i], hipEventDisableTiming) == hipSuccess;
+      ok = ok && hipEventCreateWithFlags(&b->ev_samp[i], hipEventDisableTiming) == hipSuccess;
+    }
+  }
   if (!ok) {
     set_err("device allocation failed");
     lpcnet_batch_destroy(b);
@@ -1041,6 +1083,7 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
   if (!b) return;
   b->set_device();
   if (b->stream) (void)hipStreamSynchronize(b->stream);
+  if (b->fstream) (void)hipStreamSynchronize(b->fstream);
   free_model(b);
   (void)hipFree(b->d_state);
   (void)hipFree(b->d_feat);
@@ -1053,6 +1096,13 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
     if (b->h_lpc[i]) (void)hipHostFree(b->h_lpc[i]);
     if (b->ev_lpc[i]) (void)hipEventDestroy(b->ev_lpc[i]);
   }
+  for (int i = 0; i < 2; i++) {
+    (void)hipFree(b->d_cond[i]);
+    if (b->ev_frame[i]) (void)hipEventDestroy(b->ev_frame[i]);
+    if (b->ev_samp[i]) (void)hipEventDestroy(b->ev_samp[i]);
+  }
+  if (b->ev_start) (void)hipEventDestroy(b->ev_start);
+  if (b->fstream) (void)hipStreamDestroy(b->fstream);
   for (hipEvent_t e : b->ev_taken) (void)hipEventDestroy(e);
   for (hipEvent_t e : b->ev_free) (void)hipEventDestroy(e);
   if (b->stream) (void)hipStreamDestroy(b->stream);
@@ -1156,6 +1206,14 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
   const size_t fstride = (size_t)b->B * NF;
   if (nframes == 0) return 0;
   int slot = 0;
+  /* overlapped frame kernels: matrix-core and fp32 latency kernels (the only
+   * ones reading the frame outputs through FrameCond), when CUs are free */
+  const bool ovl = b->fstream && (b->mf || b->fp) && nframes >= 2 && !b->d_stamps && !getenv("LPCNET_NO_OVERLAP");
+  if (ovl) {
+    /* the first frame kernel follows everything already on stream */
+    HIPCHK(hipEventRecord(b->ev_start, b->stream));
+    HIPCHK(hipStreamWaitEvent(b->fstream, b->ev_start, 0));
+  }
   auto wait_slot = [&](int sl) -> int {
     if (b->ev_lpc_used[sl]) HIPCHK(hipEventSynchronize(b->ev_lpc[sl]));
     return 0;
@@ -1166,8 +1224,10 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
     slot = f & 1;
     /* zero copy: the frame kernel reads the pinned host LPC directly (64 B
      * per stream); the slot is rewritten only after that kernel finished */
-    if (launch_frame_step(b, d_features + f * fstride, b->h_lpc_dev[slot], d_pcm + (size_t)f * b->B * N, N)) return -1;
-    HIPCHK(hipEventRecord(b->ev_lpc[slot], b->stream));
+    if (launch_frame_step(b, d_features + f * fstride, b->h_lpc_dev[slot], d_pcm + (size_t)f * b->B * N, N, 0,
+                          ovl ? f : -1))
+      return -1;
+    HIPCHK(hipEventRecord(b->ev_lpc[slot], ovl ? b->fstream : b->stream));
     b->ev_lpc_used[slot] = true;
     if (f + 1 < nframes) {
       /* host LPC of the next frame overlaps this frame's kernels */

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include "device_math.h"
+#include "l2_warm.h"
 #include "lds_flags.h"
 #include "lpcnet_engine.h"
 #include "sampler.h"
@@ -173,10 +174,11 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
   short *pcmbuf = (short *)((unsigned char *)sync + L::sync);
   unsigned char *img = lds + L::total;
 
+  if (l2_warm_role(A, A.nstreams)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int sid = blockIdx.x;
   const uint32_t *rcp = (const uint32_t *)(img + IMG_RCP);
-  const bool active = A.st[sid].frame_count > FEATURES_DELAY;
+  const bool active = frame_count_of(A, sid) > FEATURES_DELAY;
   if (!active) {
     for (int n = tid; n < A.N; n += FP_THREADS) A.pcm[(size_t)sid * A.N + n] = 0;
     return;
@@ -212,7 +214,8 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
     const int i = 64 * g + lane;
     const float bz = A.ga_par[i], br = A.ga_par[NA + i], bh = A.ga_par[2 * NA + i];
     const float dz = A.ga_par[3 * NA + i], dr = A.ga_par[4 * NA + i], dh = A.ga_par[5 * NA + i];
-    const float cz = ps->gru_a_cond[i], cr = ps->gru_a_cond[NA + i], ch = ps->gru_a_cond[2 * NA + i];
+    const float *ca = gru_a_cond_of(A, sid);
+    const float cz = ca[i], cr = ca[NA + i], ch = ca[2 * NA + i];
     float st = ps->gru_a_state[i];
     v4f wz[FP_ZF], wr[FP_ZF];
     uint32_t oz[FP_ZF / 4], orr[FP_ZF / 4], oh[FP_HF / 4];
@@ -349,7 +352,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
 #pragma unroll
     for (int j = 0; j < NLPC; j++) {
       lsr[j] = ps->last_sig[j];
-      lpr[j] = ps->lpc[j];
+      lpr[j] = lpc_of(A, sid)[j];
     }
     float deemph = ps->deemph_mem, pred = 0.f;
     int last_exc = ps->last_exc;
@@ -361,7 +364,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
 #pragma unroll
     for (int j = 1; j < NB; j++) sbv = u == j ? xv[j] : sbv;
     /* GRU_B row seeds (nnet.c:347-356): bias + condition, recurrent bias, weights */
-    const float gseed = A.gb_par[row] + ps->gru_b_cond[row];
+    const float gseed = A.gb_par[row] + gru_b_cond_of(A, sid)[row];
     const float rseed = A.gb_par[GB_ROWS + row];
     float rw16[NB];
 #pragma unroll
@@ -524,7 +527,7 @@ static int launch_fp_t(const SampleArgs &a, hipStream_t stream)
       return -1;
     attr_set = true;
   }
-  hipLaunchKernelGGL((fp_kernel<TRACE>), dim3(a.nstreams), dim3(FP_THREADS), fp_lds_bytes(), stream, a);
+  hipLaunchKernelGGL((fp_kernel<TRACE>), dim3(warm_grid(a.nstreams, a.nstreams)), dim3(FP_THREADS), fp_lds_bytes(), stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -128,8 +128,14 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
   float(*x2)[3 * COND] = (float(*)[3 * COND])x2_;
   float(*ya)[COND] = (float(*)[COND])ya_;
   float(*yb)[COND] = (float(*)[COND])yb_;
+  /* the single-stream launch has FK_B1_GRID workgroups of which only the
+   * last works: one-workgroup launches all land on XCD 0, and moving this
+   * kernel's 1 MB weight stream to another XCD's L2 leaves XCD 0's L2 to
+   * the sample kernel's embedding tables (placement affects speed only) */
+  if (NS == 1 && blockIdx.x != gridDim.x - 1) return;
+  const int grp = NS == 1 ? 0 : blockIdx.x;
   const int tid = threadIdx.x;
-  const int s0 = blockIdx.x * NS;
+  const int s0 = grp * NS;
   const uint32_t *rcp = A.rcp;
   unsigned long long t_prev = A.stamps ? __builtin_amdgcn_s_memtime() : 0, t_first = t_prev;
   unsigned long long stp[8] = {};
@@ -306,14 +312,38 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
   stamp(6);
   if (A.stamps && tid == 0) {
     stp[7] = t_prev - t_first;
-    for (int q = 0; q < 8; q++) A.stamps[(size_t)blockIdx.x * 16 + q] = stp[q];
+    for (int q = 0; q < 8; q++) A.stamps[(size_t)grp * 16 + q] = stp[q];
   }
 }
+
+/* FrameCond copy of the frame step's outputs (overlapped multi-frame path,
+ * engine.cpp launch_frame_step): a separate launch after the frame kernel,
+ * which stays untouched (a store of the copy inside its projection loop
+ * made it 2.4x slower at 1024 streams).  One workgroup per stream. */
+__global__ __launch_bounds__(256) void cond_copy_kernel(const StreamState *st, FrameCond *cond, int nstreams)
+{
+  const int sid = blockIdx.x;
+  if (sid >= nstreams) return;
+  const StreamState *p = &st[sid];
+  FrameCond *q = &cond[sid];
+  for (int e = threadIdx.x; e < GA_ROWS; e += blockDim.x) q->gru_a_cond[e] = p->gru_a_cond[e];
+  if (threadIdx.x < GB_ROWS) q->gru_b_cond[threadIdx.x] = p->gru_b_cond[threadIdx.x];
+  if (threadIdx.x < NLPC) q->lpc[threadIdx.x] = p->lpc[threadIdx.x];
+  if (threadIdx.x == 0) q->frame_count = p->frame_count;
+}
+
+int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, void *stream)
+{
+  hipLaunchKernelGGL(cond_copy_kernel, dim3(nstreams), dim3(256), 0, (hipStream_t)stream, st, cond, nstreams);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+constexpr int FK_B1_GRID = 2;
 
 int launch_frame(const FrameArgs &a, void *stream)
 {
   if (a.nstreams == 1) {
-    hipLaunchKernelGGL(frame_kernel<1>, dim3(1), dim3(FK_THREADS), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(frame_kernel<1>, dim3(FK_B1_GRID), dim3(FK_THREADS), 0, (hipStream_t)stream, a);
   } else {
     const int grid = (a.nstreams + FRAME_STREAMS - 1) / FRAME_STREAMS;
     hipLaunchKernelGGL(frame_kernel<FRAME_STREAMS>, dim3(grid), dim3(FK_THREADS), 0, (hipStream_t)stream, a);

@@ -99,6 +99,20 @@ constexpr int IMG_FCB = IMG_FCW + 256 * 32 * 4;  /* dual_fc bias [2][256] */
 constexpr int IMG_FCF = IMG_FCB + 512 * 4;       /* dual_fc factor [2][256] */
 constexpr int IMG_VAR = IMG_FCF + 512 * 4;       /* start of the variable sections */
 
+/* What one frame step hands from the frame kernel to the sample kernel,
+ * double-buffered by the overlapped multi-frame path (frame kernel f+1 runs
+ * beside sample kernel f): the conditioning vectors, the LPC of this frame
+ * and frame_count after this frame's update. */
+constexpr int OVERLAP_MAX_STREAMS = 64; /* batches up to this size get the overlapped multi-frame path */
+
+struct alignas(16) FrameCond {
+  float gru_a_cond[GA_ROWS];
+  float gru_b_cond[GB_ROWS];
+  float lpc[NLPC];
+  int frame_count;
+  int pad[3];
+};
+
 struct FrameArgs {
   StreamState *st;
   int nstreams;
@@ -115,6 +129,7 @@ struct FrameArgs {
 
 struct SampleArgs {
   StreamState *st;
+  const FrameCond *cond; /* optional [B]: read the frame's outputs here instead of st */
   int nstreams;
   int N;                 /* samples to produce (<= FRAME) */
   short *pcm;            /* [B][N] */
@@ -158,10 +173,33 @@ struct SampleArgs {
   int *trace_exc;        /* optional [B][N] */
 };
 
+/* The frame step's outputs as a sample kernel reads them: the FrameCond
+ * copy when the launch has one, else the stream state. */
+#if defined(__HIP__) || defined(__HIPCC__)
+__device__ __forceinline__ int frame_count_of(const SampleArgs &A, int sid)
+{
+  return A.cond ? A.cond[sid].frame_count : A.st[sid].frame_count;
+}
+__device__ __forceinline__ const float *gru_a_cond_of(const SampleArgs &A, int sid)
+{
+  return A.cond ? A.cond[sid].gru_a_cond : A.st[sid].gru_a_cond;
+}
+__device__ __forceinline__ const float *gru_b_cond_of(const SampleArgs &A, int sid)
+{
+  return A.cond ? A.cond[sid].gru_b_cond : A.st[sid].gru_b_cond;
+}
+__device__ __forceinline__ const float *lpc_of(const SampleArgs &A, int sid)
+{
+  return A.cond ? A.cond[sid].lpc : A.st[sid].lpc;
+}
+#endif
+
 /* Kernel launchers (kernels.hip).  variant: 0 int8, 1 fp32. sat: int8 pairs
  * may saturate. lds_bytes from sample_lds_bytes(). */
 int sample_lds_bytes(int S, int variant, int image_bytes);
 int launch_frame(const FrameArgs &a, void *stream);
+/* copy the frame step's outputs of every stream into cond[B] */
+int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, void *stream);
 int launch_sample(const SampleArgs &a, int S, int variant, int sat, int reg, int lds_bytes, void *stream);
 
 /* Wave-per-stream sample kernel (int8 quad layout): nw streams per workgroup. */

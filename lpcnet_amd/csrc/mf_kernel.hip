@@ -28,6 +28,7 @@
 
 #include "device_math.h"
 #include "lpcnet_engine.h"
+#include "l2_warm.h"
 #include "mf_common.h"
 #include "sampler.h"
 
@@ -67,6 +68,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   int *gbr = gbs + S * GB_ROWS;
   unsigned char *img = lds + L::total; /* fixed image sections: tables and dual_fc */
 
+  if (l2_warm_role(A, (A.nstreams + S - 1) / S)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = blockIdx.x * S;
   const uint32_t *rcp = (const uint32_t *)(img + IMG_RCP);
@@ -75,7 +77,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   bool any = false;
   for (int s = 0; s < S; s++) {
     const int sid = s0 + s;
-    active[s] = sid < A.nstreams && A.st[sid].frame_count > FEATURES_DELAY;
+    active[s] = sid < A.nstreams && frame_count_of(A, sid) > FEATURES_DELAY;
     any |= active[s];
   }
   if (!any) {
@@ -116,17 +118,18 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     const int wsz = A.ga_wsum[i], wsr = A.ga_wsum[NA + i], wsh = A.ga_wsum[2 * NA + i];
     float st[S];
     for (int s = 0; s < S; s++) {
-      const StreamState *p = &A.st[min(s0 + s, A.nstreams - 1)];
-      st[s] = p->gru_a_state[i];
-      cnd[i * S + s] = p->gru_a_cond[i];
-      cnd[(NA + i) * S + s] = p->gru_a_cond[NA + i];
-      cnd[(2 * NA + i) * S + s] = p->gru_a_cond[2 * NA + i];
+      const int sid = min(s0 + s, A.nstreams - 1);
+      st[s] = A.st[sid].gru_a_state[i];
+      const float *ca = gru_a_cond_of(A, sid);
+      cnd[i * S + s] = ca[i];
+      cnd[(NA + i) * S + s] = ca[NA + i];
+      cnd[(2 * NA + i) * S + s] = ca[2 * NA + i];
     }
     /* GRU_B accumulator seeds, frame constants (nnet.c:347-356 with the
      * offset-128 correction): cvt_rne((bias + cond) * SCALE) + 128 rowsum(w) */
     for (int e = tid; e < S * GB_ROWS; e += SAMPLE_THREADS) {
       const int s = e / GB_ROWS, r = e % GB_ROWS;
-      gbs[e] = cvt_rne((A.gb_par[r] + A.st[min(s0 + s, A.nstreams - 1)].gru_b_cond[r]) * kScale) + A.gb_wsum[r];
+      gbs[e] = cvt_rne((A.gb_par[r] + gru_b_cond_of(A, min(s0 + s, A.nstreams - 1))[r]) * kScale) + A.gb_wsum[r];
     }
     if (tid < GB_ROWS) gbr[tid] = cvt_rne(A.gb_par[GB_ROWS + tid] * kScale) + A.gb_wsum[GB_ROWS + tid];
     /* this lane's GRU_A weight rows and x offsets, for all N samples */
@@ -293,13 +296,13 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     const bool samp = my_s < S;                         /* wave-uniform */
     const bool samp_w = samp && (S == 4 || half == 0);  /* lanes owning the stream's outputs */
     const int ms = samp ? my_s : 0;
-    const bool my_active = samp && s0 + ms < A.nstreams && A.st[s0 + ms].frame_count > FEATURES_DELAY;
+    const bool my_active = samp && s0 + ms < A.nstreams && frame_count_of(A, s0 + ms) > FEATURES_DELAY;
     /* GRU_B: lane = (unit quad gq, stream gs, gi): unit gu = 4gq + gi of
      * stream gs; the MFMA columns are (gs, gi), so D register gi of this lane
      * holds row 4gq + gi.  gown: stream gs is one of this wave's. */
     const int gq = lane >> 4, gs = (lane & 15) >> 2, gi = lane & 3, gu = 4 * gq + gi, sl = min(gs, S - 1);
     const bool gown = gs < S && (S == 4 ? (gs >> 1) : gs) == sw;
-    const bool gact = gown && s0 + gs < A.nstreams && A.st[s0 + gs].frame_count > FEATURES_DELAY;
+    const bool gact = gown && s0 + gs < A.nstreams && frame_count_of(A, s0 + gs) > FEATURES_DELAY;
 
     float lsr[NLPC], lpr[NLPC];
     float pred = 0.f, deemph = 0.f;
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
 #pragma unroll
       for (int j = 0; j < NLPC; j++) {
         lsr[j] = p->last_sig[j];
-        lpr[j] = p->lpc[j];
+        lpr[j] = lpc_of(A, min(s0 + ms, A.nstreams - 1))[j];
       }
       deemph = p->deemph_mem;
       last_exc = p->last_exc;
@@ -480,7 +483,7 @@ static int launch_mf_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
       return -1;
     attr_set = true;
   }
-  const int grid = (a.nstreams + S - 1) / S;
+  const int grid = warm_grid((a.nstreams + S - 1) / S, a.nstreams);
   hipLaunchKernelGGL((mf_kernel<S, TRACE>), dim3(grid), dim3(MF_THREADS), lds_bytes, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -169,24 +169,45 @@ def test_fp32_latency_kernel_matches_oracle(require_gpu, blobs, B, check):
             assert np.abs(out.astype(np.float64)).mean() > 100
 
 
-def test_device_resident_frames_equal_host_path(require_gpu, blobs):
-    """lpcnet_batch_synthesize_frames (pipelined host LPC) == frame-by-frame host API."""
-    B, F = 64, 6
-    blob = blobs["streams_int8"]
-    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
-    a = L.LPCNetBatch(B, 0, blob)
-    ref = np.stack([a.synthesize(allf[f]) for f in range(F)], 0)
-    b = L.LPCNetBatch(B, 0, blob)
-    df = b.device_alloc(allf.nbytes)
+def _frames(b, allf, f0, f1):
+    """lpcnet_batch_synthesize_frames over frames f0..f1-1 -> [F][B][160]"""
+    part = np.ascontiguousarray(allf[f0:f1])
+    F, B = part.shape[:2]
+    df = b.device_alloc(part.nbytes)
     dp = b.device_alloc(F * B * 160 * 2)
-    b.h2d(df, allf)
-    b.synthesize_frames(allf, df, dp, F)
+    b.h2d(df, part)
+    b.synthesize_frames(part, df, dp, F)
     b.sync()
     got = np.zeros((F, B, 160), np.int16)
     b.d2h(got, dp)
     b.device_free(df)
     b.device_free(dp)
+    return got
+
+
+@pytest.mark.parametrize("B,name", [(64, "streams_int8"), (1, "streams_int8"), (1, "streams_fp32"),
+                                    (3, "streams_fp32"), (65, "streams_int8")])
+def test_device_resident_frames_equal_host_path(require_gpu, blobs, B, name):
+    """lpcnet_batch_synthesize_frames (pipelined host LPC; up to
+    OVERLAP_MAX_STREAMS = 64 streams the frame kernel of frame f+1 runs beside
+    the sample kernel of frame f, outputs double-buffered) == frame-by-frame
+    host API, including the frame conditioning left in the stream state, and
+    mixed with single-frame calls; B = 1 also against the oracle."""
+    F = 9
+    blob = blobs[name]
+    variant = 1 if name == "streams_fp32" else 0
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    a = L.LPCNetBatch(B, 0, blob)
+    ref = np.stack([a.synthesize(allf[f]) for f in range(F)], 0)
+    b = L.LPCNetBatch(B, 0, blob)
+    got = np.concatenate([_frames(b, allf, 0, 5), b.synthesize(allf[5])[None], _frames(b, allf, 6, F)], 0)
     assert np.array_equal(got, ref)
+    for s in (0, B - 1):
+        sa, sb = a.get_state(s), b.get_state(s)
+        for k in ("gru_a_state", "gru_b_state", "gru_a_cond", "gru_b_cond", "lpc"):
+            assert np.array_equal(bits(sa[k]), bits(sb[k])), (s, k)
+    if B == 1:
+        assert np.array_equal(got[:, 0], O.synth_stream(blob, allf[:, 0], variant))
 
 
 def test_partial_frame_and_reset_stream(require_gpu, blobs):
