@@ -319,22 +319,30 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
 /* FrameCond copy of the frame step's outputs (overlapped multi-frame path,
  * engine.cpp launch_frame_step): a separate launch after the frame kernel,
  * which stays untouched (a store of the copy inside its projection loop
- * made it 2.4x slower at 1024 streams).  One workgroup per stream. */
-__global__ __launch_bounds__(256) void cond_copy_kernel(const StreamState *st, FrameCond *cond, int nstreams)
+ * made it 2.4x slower at 1024 streams).  One workgroup for all (<= 64)
+ * streams, so one flag publishes the whole copy: every wave drains its
+ * stores (agent-scope fence), the barrier, then one release store. */
+__global__ __launch_bounds__(1024) void cond_copy_kernel(const StreamState *st, FrameCond *cond, int nstreams, int *ready,
+                                                         int tag)
 {
-  const int sid = blockIdx.x;
-  if (sid >= nstreams) return;
-  const StreamState *p = &st[sid];
-  FrameCond *q = &cond[sid];
-  for (int e = threadIdx.x; e < GA_ROWS; e += blockDim.x) q->gru_a_cond[e] = p->gru_a_cond[e];
-  if (threadIdx.x < GB_ROWS) q->gru_b_cond[threadIdx.x] = p->gru_b_cond[threadIdx.x];
-  if (threadIdx.x < NLPC) q->lpc[threadIdx.x] = p->lpc[threadIdx.x];
-  if (threadIdx.x == 0) q->frame_count = p->frame_count;
+  constexpr int W = GA_ROWS + GB_ROWS + NLPC + 1;
+  for (int e = threadIdx.x; e < nstreams * W; e += blockDim.x) {
+    const int sid = e / W, j = e % W;
+    const StreamState *p = &st[sid];
+    FrameCond *q = &cond[sid];
+    if (j < GA_ROWS) q->gru_a_cond[j] = p->gru_a_cond[j];
+    else if (j < GA_ROWS + GB_ROWS) q->gru_b_cond[j - GA_ROWS] = p->gru_b_cond[j - GA_ROWS];
+    else if (j < GA_ROWS + GB_ROWS + NLPC) q->lpc[j - GA_ROWS - GB_ROWS] = p->lpc[j - GA_ROWS - GB_ROWS];
+    else q->frame_count = p->frame_count;
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(ready, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, void *stream)
+int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, int *ready, int tag, void *stream)
 {
-  hipLaunchKernelGGL(cond_copy_kernel, dim3(nstreams), dim3(256), 0, (hipStream_t)stream, st, cond, nstreams);
+  hipLaunchKernelGGL(cond_copy_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, st, cond, nstreams, ready, tag);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
