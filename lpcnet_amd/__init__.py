@@ -325,7 +325,7 @@ class LPCNetBatch:
 
     def get_frame_stamps(self) -> np.ndarray:
         """[workgroups, 16] s_memtime phase durations of the last frame-kernel launch."""
-        out = np.zeros(((self.B + 3) // 4, 16), np.uint64)
+        out = np.zeros((self.B, 16), np.uint64)  # >= the frame kernel's workgroups for any batch
         g = lib.lpcnet_batch_get_frame_stamps(self._b, out.ctypes.data)
         if g < 0:
             raise LPCNetError("stamps not enabled")

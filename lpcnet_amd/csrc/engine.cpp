@@ -1345,7 +1345,7 @@ LPCNET_EXPORT int lpcnet_batch_set_stamps(LPCNetBatch *b, int enable)
   if (enable) {
     /* sample kernel [groups][STAMP_WAVES][16] (enough for any S), then the
      * frame kernel [B / FRAME_STREAMS][16] */
-    size_t n = (size_t)b->B * STAMP_WAVES * 16 + (size_t)(b->B / FRAME_STREAMS + 1) * 16;
+    size_t n = (size_t)b->B * STAMP_WAVES * 16 + (size_t)(frame_groups(b->B) + 1) * 16;
     HIPCHK(hipMalloc(&b->d_stamps, n * 8));
     HIPCHK(hipMemset(b->d_stamps, 0, n * 8));
   }
@@ -1365,7 +1365,7 @@ LPCNET_EXPORT int lpcnet_batch_get_frame_stamps(LPCNetBatch *b, unsigned long lo
 {
   if (!b || !b->d_stamps || !b->have_model || b->set_device()) return -1;
   HIPCHK(hipStreamSynchronize(b->stream));
-  const int g = (b->B + FRAME_STREAMS - 1) / FRAME_STREAMS;
+  const int g = frame_groups(b->B);
   HIPCHK(hipMemcpy(out, b->d_stamps + (size_t)b->B * STAMP_WAVES * 16, (size_t)g * 16 * 8, hipMemcpyDeviceToHost));
   return g;
 }

@@ -217,6 +217,8 @@ __device__ __forceinline__ const float *lpc_of(const SampleArgs &A, int sid)
  * may saturate. lds_bytes from sample_lds_bytes(). */
 int sample_lds_bytes(int S, int variant, int image_bytes);
 int launch_frame(const FrameArgs &a, void *stream);
+constexpr int FK_ONE_STREAM_MAX = 256; /* frame kernel: one stream per workgroup up to this batch */
+int frame_groups(int nstreams);        /* frame kernel workgroups (stamp rows) for a batch */
 /* copy the frame step's outputs of every stream into cond[B], then publish
  * *ready = tag (agent-scope release) */
 int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, int *ready, int tag, void *stream);
