@@ -319,8 +319,6 @@ struct LPCNetBatch {
   hipEvent_t ev_frame[2] = {nullptr, nullptr}, ev_samp[2] = {nullptr, nullptr}, ev_start = nullptr;
   bool ev_samp_used[2] = {false, false};
   hipEvent_t ev_samp_cur[2] = {nullptr, nullptr}; /* the event slot c's reuse waits on */
-  int *d_ready = nullptr; /* [2] tag of the frame whose FrameCond slot is complete */
-  int cond_seq = 0;
   /* trace */
   bool trace = false;
   float *d_trace_logits = nullptr;
@@ -938,7 +936,8 @@ int ensure_trace(LPCNetBatch *b, int N)
  * sample kernel f-2 read: ev_samp); the sample kernel on stream waits only
  * for that copy (ev_frame) and reads the frame's outputs there, so frame
  * kernel f+1 runs beside sample kernel f.  The sample kernels read nothing
- * else the frame kernel writes. */
+ * else the frame kernel writes.  Every fstream launch precedes a stream
+ * launch that waits for it, so a sync of stream covers both. */
 int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lpc, short *d_pcm, int N, int preload = 0,
                       int ovl = -1)
 {
@@ -957,13 +956,8 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   sa.preload = std::max(0, std::min(preload, N));
   sa.stamps = b->d_stamps;
   fa.stamps = b->d_stamps ? b->d_stamps + (size_t)b->B * STAMP_WAVES * 16 : nullptr;
-  int tag = 0;
   if (ovl >= 0) {
-    tag = ++b->cond_seq;
-    if (tag <= 0) tag = b->cond_seq = 1;
     sa.cond = b->d_cond[c];
-    sa.cond_ready = b->d_ready + c;
-    sa.cond_tag = tag;
   }
   /* timing 1: events around the sample kernel only; 2: the frame kernel too
    * (one event between the two kernels serves both pairs) */
@@ -977,7 +971,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   hipEvent_t ef = nullptr; /* end of the frame kernel, overlapped form with frame timing */
   if (e[0]) HIPCHK(hipEventRecord(e[0], fs));
   if (launch_frame(fa, fs)) { set_err("frame kernel launch failed"); return -1; }
-  if (ovl >= 0 && launch_cond_copy(b->d_state, b->d_cond[c], b->B, b->d_ready + c, tag, fs)) {
+  if (ovl >= 0 && launch_cond_copy(b->d_state, b->d_cond[c], b->B, fs)) {
     set_err("copy launch failed");
     return -1;
   }
@@ -986,10 +980,12 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
       ef = get_event(b);
       HIPCHK(hipEventRecord(ef, fs));
     }
-    /* the sample kernel waits for the copy's flag on the device (a
-     * cross-queue event wait here cost ~18 us per frame); ev_frame only
-     * joins the last frame back into stream (synthesize_frames) */
+    /* an event, not a device flag: a sample kernel polling a flag set by
+     * the other queue was faster by ~1 % but gave wrong output wherever the
+     * two queues do not run concurrently (rocprofv3 --pmc serialises
+     * dispatches: the poll timed out and read a stale slot) */
     HIPCHK(hipEventRecord(b->ev_frame[c], fs));
+    HIPCHK(hipStreamWaitEvent(b->stream, b->ev_frame[c], 0));
   }
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   const int lrc = N <= 0 ? 0
@@ -1083,7 +1079,6 @@ LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
   if (ok && nb_streams <= OVERLAP_MAX_STREAMS) {
     ok = ok && hipStreamCreateWithFlags(&b->fstream, hipStreamNonBlocking) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&b->ev_start, hipEventDisableTiming) == hipSuccess;
-    ok = ok && hipMalloc(&b->d_ready, 2 * sizeof(int)) == hipSuccess && hipMemset(b->d_ready, 0, 2 * sizeof(int)) == hipSuccess;
     for (int i = 0; i < 2 && ok; i++) {
       ok = ok && hipMalloc(&b->d_cond[i], sizeof(FrameCond) * (size_t)nb_streams) == hipSuccess;
       ok = ok && hipEventCreateWithFlags(&b->ev_frame[i], hipEventDisableTiming) == hipSuccess;
@@ -1125,7 +1120,6 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
     if (b->ev_samp[i]) (void)hipEventDestroy(b->ev_samp[i]);
   }
   if (b->ev_start) (void)hipEventDestroy(b->ev_start);
-  (void)hipFree(b->d_ready);
   if (b->fstream) (void)hipStreamDestroy(b->fstream);
   for (hipEvent_t e : b->ev_taken) (void)hipEventDestroy(e);
   for (hipEvent_t e : b->ev_free) (void)hipEventDestroy(e);
@@ -1253,8 +1247,6 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
       return -1;
     HIPCHK(hipEventRecord(b->ev_lpc[slot], ovl ? b->fstream : b->stream));
     b->ev_lpc_used[slot] = true;
-    /* every fstream launch ends before stream's last launch: sync(stream) covers both */
-    if (ovl && f + 1 == nframes) HIPCHK(hipStreamWaitEvent(b->stream, b->ev_frame[slot], 0));
     if (f + 1 < nframes) {
       /* host LPC of the next frame overlaps this frame's kernels */
       if (wait_slot(slot ^ 1)) return -1;

@@ -175,7 +175,6 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
   unsigned char *img = lds + L::total;
 
   if (l2_warm_role(A, A.nstreams)) return;
-  frame_cond_wait(A);
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int sid = blockIdx.x;
   const uint32_t *rcp = (const uint32_t *)(img + IMG_RCP);

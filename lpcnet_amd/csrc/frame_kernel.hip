@@ -320,10 +320,8 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
  * engine.cpp launch_frame_step): a separate launch after the frame kernel,
  * which stays untouched (a store of the copy inside its projection loop
  * made it 2.4x slower at 1024 streams).  One workgroup for all (<= 64)
- * streams, so one flag publishes the whole copy: every wave drains its
- * stores (agent-scope fence), the barrier, then one release store. */
-__global__ __launch_bounds__(1024) void cond_copy_kernel(const StreamState *st, FrameCond *cond, int nstreams, int *ready,
-                                                         int tag)
+ * streams. */
+__global__ __launch_bounds__(1024) void cond_copy_kernel(const StreamState *st, FrameCond *cond, int nstreams)
 {
   constexpr int W = GA_ROWS + GB_ROWS + NLPC + 1;
   for (int e = threadIdx.x; e < nstreams * W; e += blockDim.x) {
@@ -335,14 +333,11 @@ __global__ __launch_bounds__(1024) void cond_copy_kernel(const StreamState *st, 
     else if (j < GA_ROWS + GB_ROWS + NLPC) q->lpc[j - GA_ROWS - GB_ROWS] = p->lpc[j - GA_ROWS - GB_ROWS];
     else q->frame_count = p->frame_count;
   }
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(ready, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, int *ready, int tag, void *stream)
+int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, void *stream)
 {
-  hipLaunchKernelGGL(cond_copy_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, st, cond, nstreams, ready, tag);
+  hipLaunchKernelGGL(cond_copy_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, st, cond, nstreams);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -130,8 +130,6 @@ struct FrameArgs {
 struct SampleArgs {
   StreamState *st;
   const FrameCond *cond; /* optional [B]: read the frame's outputs here instead of st */
-  const int *cond_ready; /* with cond: the copy launch sets *cond_ready = cond_tag when cond is complete */
-  int cond_tag;
   int nstreams;
   int N;                 /* samples to produce (<= FRAME) */
   short *pcm;            /* [B][N] */
@@ -178,23 +176,6 @@ struct SampleArgs {
 /* The frame step's outputs as a sample kernel reads them: the FrameCond
  * copy when the launch has one, else the stream state. */
 #if defined(__HIP__) || defined(__HIPCC__)
-/* Overlapped path: wait until the copy launch of this frame has published
- * its FrameCond (agent-scope acquire by one lane, then the workgroup
- * barrier; MI355X_MICROARCH.md inter-workgroup visibility).  The producer
- * runs on another queue and never waits for this kernel; the wait is
- * bounded all the same (2^22 polls) so a lost flag cannot hang the device. */
-__device__ __forceinline__ void frame_cond_wait(const SampleArgs &A)
-{
-  if (!A.cond_ready) return;
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < (1 << 22); k++) {
-      if (__hip_atomic_load(A.cond_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == A.cond_tag) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-}
-
 __device__ __forceinline__ int frame_count_of(const SampleArgs &A, int sid)
 {
   return A.cond ? A.cond[sid].frame_count : A.st[sid].frame_count;
@@ -219,9 +200,8 @@ int sample_lds_bytes(int S, int variant, int image_bytes);
 int launch_frame(const FrameArgs &a, void *stream);
 constexpr int FK_ONE_STREAM_MAX = 256; /* frame kernel: one stream per workgroup up to this batch */
 int frame_groups(int nstreams);        /* frame kernel workgroups (stamp rows) for a batch */
-/* copy the frame step's outputs of every stream into cond[B], then publish
- * *ready = tag (agent-scope release) */
-int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, int *ready, int tag, void *stream);
+/* copy the frame step's outputs of every stream into cond[B] */
+int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, void *stream);
 int launch_sample(const SampleArgs &a, int S, int variant, int sat, int reg, int lds_bytes, void *stream);
 
 /* Wave-per-stream sample kernel (int8 quad layout): nw streams per workgroup. */

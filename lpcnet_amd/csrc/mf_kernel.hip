@@ -69,7 +69,6 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   unsigned char *img = lds + L::total; /* fixed image sections: tables and dual_fc */
 
   if (l2_warm_role(A, (A.nstreams + S - 1) / S)) return;
-  frame_cond_wait(A);
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = blockIdx.x * S;
   const uint32_t *rcp = (const uint32_t *)(img + IMG_RCP);
