@@ -319,7 +319,7 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
 /* FrameCond copy of the frame step's outputs (overlapped multi-frame path,
  * engine.cpp launch_frame_step): a separate launch after the frame kernel,
  * which stays untouched (a store of the copy inside its projection loop
- * made it 2.4x slower at 1024 streams).  One workgroup for all (<= 64)
+ * made it 2.4x slower at 1024 streams).  One workgroup for all (<= 128)
  * streams. */
 __global__ __launch_bounds__(1024) void cond_copy_kernel(const StreamState *st, FrameCond *cond, int nstreams)
 {

@@ -103,7 +103,7 @@ constexpr int IMG_VAR = IMG_FCF + 512 * 4;       /* start of the variable sectio
  * double-buffered by the overlapped multi-frame path (frame kernel f+1 runs
  * beside sample kernel f): the conditioning vectors, the LPC of this frame
  * and frame_count after this frame's update. */
-constexpr int OVERLAP_MAX_STREAMS = 64; /* batches up to this size get the overlapped multi-frame path */
+constexpr int OVERLAP_MAX_STREAMS = 128; /* batches up to this size get the overlapped multi-frame path (sample + frame workgroups fit the 256 CUs) */
 
 struct alignas(16) FrameCond {
   float gru_a_cond[GA_ROWS];

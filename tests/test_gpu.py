@@ -186,10 +186,10 @@ def _frames(b, allf, f0, f1):
 
 
 @pytest.mark.parametrize("B,name", [(64, "streams_int8"), (1, "streams_int8"), (1, "streams_fp32"),
-                                    (3, "streams_fp32"), (65, "streams_int8")])
+                                    (3, "streams_fp32"), (128, "streams_int8"), (129, "streams_int8")])
 def test_device_resident_frames_equal_host_path(require_gpu, blobs, B, name):
     """lpcnet_batch_synthesize_frames (pipelined host LPC; up to
-    OVERLAP_MAX_STREAMS = 64 streams the frame kernel of frame f+1 runs beside
+    OVERLAP_MAX_STREAMS = 128 streams the frame kernel of frame f+1 runs beside
     the sample kernel of frame f, outputs double-buffered) == frame-by-frame
     host API, including the frame conditioning left in the stream state, and
     mixed with single-frame calls; B = 1 also against the oracle."""
