@@ -25,6 +25,7 @@
 #include <functional>
 #include <mutex>
 #include <string>
+#include <sched.h>
 #include <thread>
 #include <vector>
 
@@ -269,7 +270,11 @@ int pool_threads()
 {
   const char *e = getenv("LPCNET_LPC_THREADS");
   if (e) return std::max(0, atoi(e));
+  /* the CPUs this process may run on (a launcher may pin each rank to its
+   * share of the node), not the whole machine */
   int hc = (int)std::thread::hardware_concurrency();
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) hc = std::max(1, CPU_COUNT(&set));
   return std::max(0, std::min(hc, 16) - 1);
 }
 
