@@ -186,7 +186,8 @@ def _frames(b, allf, f0, f1):
 
 
 @pytest.mark.parametrize("B,name", [(64, "streams_int8"), (1, "streams_int8"), (1, "streams_fp32"),
-                                    (3, "streams_fp32"), (128, "streams_int8"), (129, "streams_int8")])
+                                    (3, "streams_fp32"), (100, "streams_fp32"), (128, "streams_int8"),
+                                    (129, "streams_int8"), (64, "streams_int8_sat")])
 def test_device_resident_frames_equal_host_path(require_gpu, blobs, B, name):
     """lpcnet_batch_synthesize_frames (pipelined host LPC; up to
     OVERLAP_MAX_STREAMS = 128 streams the frame kernel of frame f+1 runs beside
