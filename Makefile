@@ -16,9 +16,18 @@ HDRS := include/lpcnet.h include/lpcnet_mi355x.h $(CSRC)/lpcnet_engine.h $(CSRC)
 COMMON := -O3 -fPIC -ffp-contract=off -fno-fast-math -std=c++17 -Iinclude -I$(CSRC) -fvisibility=hidden -Wall -Wno-unused-function
 OBJS := $(BUILD)/kernels.o $(BUILD)/mf_kernel.o $(BUILD)/fp_kernel.o $(BUILD)/selftest.o $(BUILD)/frame_kernel.o $(BUILD)/engine.o $(BUILD)/lpc_host.o $(BUILD)/model_gen.o
 
-all: lib oracle
+SYNTH := tools/lpcnet_synth
+
+all: lib synth oracle
 
 lib: $(LIB)
+
+# file-driven C caller of include/lpcnet.h (lpcnet_demo -synthesis equivalent):
+# plain C99 against the public header only, linked to the in-tree library
+synth: $(SYNTH)
+
+$(SYNTH): tools/lpcnet_synth.c include/lpcnet.h $(LIB)
+	$(CC) -std=c99 -O2 -Wall -Wextra -pedantic -Werror -Iinclude -o $@ $< -Llpcnet_amd -llpcnet_mi355x -Wl,-rpath,'$$ORIGIN/../lpcnet_amd'
 
 $(BUILD):
 	mkdir -p $(BUILD)
@@ -54,7 +63,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(BUILD) $(LIB)
+	rm -rf $(BUILD) $(LIB) $(SYNTH)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib oracle clean
+.PHONY: all lib synth oracle clean

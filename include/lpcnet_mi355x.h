@@ -11,6 +11,7 @@
 #define LPCNET_MI355X_H
 
 #include "lpcnet.h"
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -33,8 +34,8 @@ typedef struct {
   double bytes_per_stream_sample; /* per-stream bytes per sample (gathers, trace-free) */
   double ops_per_sample;          /* 2*MAC per stream per sample */
   int streams_per_workgroup;      /* streams per sample-kernel workgroup */
-  int quad_path;                  /* 0 per-slot LDS, 1 quad LDS (lockstep), 2 wave-per-stream, 3 pipelined,
-                                     4 pipelined on the matrix cores, 5 fp32 latency kernel */
+  int quad_path;                  /* sample kernel: 0 lockstep (per-slot LDS layout), 1 lockstep (quad
+                                     LDS layout), 4 mf_kernel (matrix cores), 5 fp_kernel (fp32) */
   int lds_bytes;                  /* dynamic LDS of the sample kernel */
   double mfma_ops_per_group_sample; /* int8 matrix-core ops issued per workgroup per sample
                                        (mf_kernel; padding included), 0 otherwise */
@@ -47,16 +48,14 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b);
 /* 0 on success, -1 on a missing / mis-sized array (lpcnet_load_model rules). */
 LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *data, int len);
 LPCNET_EXPORT int lpcnet_batch_model_info(const LPCNetBatch *b, LPCNetModelInfo *info);
-/* Sample-kernel selection: 0 automatic (default; env LPCNET_KERNEL), 1 the
- * lockstep kernel (6 waves per stream group), 2 the wave-per-stream kernel,
- * 3 the pipelined kernel (2 and 3: int8 quad-layout models only; otherwise
- * the lockstep kernel runs), 4 the pipelined kernel with both int8 products
- * on the matrix cores (non-saturating int8 models whose blocks fit its
- * register tables; otherwise mode 3 rules apply), 5 the fp32 latency
- * kernel (fp32 models with a dense GRU_B whose blocks fit its register
- * tables; int8 models fall back to mode 4 rules, other fp32 models to the
- * lockstep kernel).  Automatic: 5 for fp32 models, 4 for int8 where they
- * apply.  Results are identical; only speed differs. */
+/* Sample-kernel selection: 0 automatic (default; env LPCNET_KERNEL),
+ * 1 the lockstep kernel (every model: the fallback for saturating int8 models
+ * and fp32 models with a sparse GRU_B), 4 mf_kernel (both int8 products on
+ * the matrix cores; non-saturating int8 models whose blocks fit its register
+ * tables), 5 fp_kernel (fp32 models with a dense GRU_B whose blocks fit its
+ * tables).  Automatic: 5 where it applies, else 4 where it applies, else 1;
+ * a forced mode the model cannot run falls back to 1.  Results are
+ * identical; only speed differs.  Returns -1 for any other mode. */
 LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode);
 /* lpcnet_reset() on every stream / on one stream. */
 LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b);
@@ -90,7 +89,17 @@ LPCNET_EXPORT int lpcnet_batch_restore_state(LPCNetBatch *b, int stream, const v
  * frame has been enqueued (use lpcnet_batch_sync to wait). */
 LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_features, const float *d_features,
                                                  short *d_pcm, int nframes, int N);
+/* Wait for every enqueued frame.  Returns 0, or -1 (lpcnet_mi355x_last_error)
+ * on a HIP error or a device-side abort (see lpcnet_batch_set_spin_limit). */
 LPCNET_EXPORT int lpcnet_batch_sync(LPCNetBatch *b);
+
+/* Bound on the polls of one LDS flag wait inside the barrier-free sample
+ * kernel (fp_kernel).  A wait that exceeds it means a protocol fault: the
+ * kernel finishes early instead of hanging the device, and the next
+ * synchronising call (lpcnet_batch_synthesize / _impl / _sync) returns -1
+ * with lpcnet_mi355x_last_error() set -- never silent wrong PCM.  0 restores
+ * the default (2^20 polls); tiny values exist to test the reporting. */
+LPCNET_EXPORT int lpcnet_batch_set_spin_limit(LPCNetBatch *b, int polls);
 
 /* Device memory helpers (so callers need no HIP headers). */
 LPCNET_EXPORT void *lpcnet_batch_device_alloc(LPCNetBatch *b, size_t bytes);
@@ -149,6 +158,10 @@ LPCNET_EXPORT const uint32_t *lpcnet_mi355x_rcp_table(void);
  * op 8: n kiss99 draws (kiss99.c:59-81) from the 4-word state in[0..3].
  * Returns 0, or -1 on bad arguments / HIP failure. */
 LPCNET_EXPORT int lpcnet_mi355x_device_numerics(int device, int op, const void *in, void *out, int n);
+/* Validate a weight blob with every rule lpcnet_load_model applies
+ * (parse_lpcnet_weights.c:36-113 record/idx rules, array sizes, LDS budget)
+ * without a device.  Returns 0 or -1 (lpcnet_mi355x_last_error). */
+LPCNET_EXPORT int lpcnet_mi355x_validate_model(const unsigned char *data, int len);
 /* Number of visible HIP devices (0 on a machine without GPU). */
 LPCNET_EXPORT int lpcnet_mi355x_device_count(void);
 /* Last error string of this thread. */

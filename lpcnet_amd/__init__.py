@@ -67,6 +67,8 @@ def _load():
         "lpcnet_batch_restore_state": (i, [vp, i, vp]),
         "lpcnet_batch_synthesize_frames": (i, [vp, vp, vp, vp, i, i]),
         "lpcnet_batch_sync": (i, [vp]),
+        "lpcnet_batch_set_spin_limit": (i, [vp, i]),
+        "lpcnet_mi355x_validate_model": (i, [C.c_char_p, i]),
         "lpcnet_batch_device_alloc": (vp, [vp, C.c_size_t]),
         "lpcnet_batch_device_free": (i, [vp, vp]),
         "lpcnet_batch_memcpy_h2d": (i, [vp, vp, vp, C.c_size_t]),
@@ -109,10 +111,6 @@ class ModelInfo(C.Structure):
         """Demangled template instance of the sample kernel this model runs
         (as rocprofv3 names it)."""
         sat = "true" if self.may_saturate else "false"
-        if self.quad_path == 2:
-            return f"wave_kernel<{self.streams_per_workgroup}, {sat}>"
-        if self.quad_path == 3:
-            return f"pipe_kernel<{self.streams_per_workgroup}, {sat}, false>"
         if self.quad_path == 4:
             return f"mf_kernel<{self.streams_per_workgroup}, false>"
         if self.quad_path == 5:
@@ -134,6 +132,12 @@ def device_numerics(op: int, x: np.ndarray, n: int | None = None, device: int = 
     if lib.lpcnet_mi355x_device_numerics(device, op, src.ctypes.data, out.ctypes.data, cnt) != 0:
         raise LPCNetError("device numerics failed: " + last_error())
     return out
+
+
+def validate_model(blob: bytes) -> None:
+    """Host-only check of a weight blob with lpcnet_load_model's rules; raises LPCNetError."""
+    if lib.lpcnet_mi355x_validate_model(blob, len(blob)) != 0:
+        raise LPCNetError(last_error())
 
 
 def device_count() -> int:
@@ -220,11 +224,15 @@ class LPCNetBatch:
             raise LPCNetError(f"lpcnet_batch_load_model failed: {last_error()}")
 
     def set_kernel(self, mode: int) -> None:
-        """0 automatic, 1 lockstep sample kernel, 2 wave-per-stream kernel, 3 pipelined kernel,
-        4 matrix-core pipelined kernel, 5 fp32 latency kernel
-        (unavailable modes fall back)."""
+        """0 automatic, 1 lockstep sample kernel, 4 mf_kernel (matrix cores), 5 fp_kernel (fp32);
+        a mode the model cannot run falls back to 1."""
         if lib.lpcnet_batch_set_kernel(self._b, mode) != 0:
-            raise LPCNetError("bad kernel mode")
+            raise LPCNetError(last_error())
+
+    def set_spin_limit(self, polls: int) -> None:
+        """LDS flag-wait bound of the barrier-free kernel (0 = default); see lpcnet_mi355x.h."""
+        if lib.lpcnet_batch_set_spin_limit(self._b, polls) != 0:
+            raise LPCNetError("bad spin limit")
 
     def info(self) -> ModelInfo:
         mi = ModelInfo()

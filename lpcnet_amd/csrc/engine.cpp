@@ -291,10 +291,7 @@ struct LPCNetBatch {
   int variant = 0;
   bool sat = false;
   bool reg = false;
-  int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 2 wave_kernel, 3 pipe_kernel, 4 matrix-core pipe_kernel,
-                            5 fp32 latency kernel */
-  int wave_nw = 0;       /* >0: wave_kernel with this many streams per workgroup */
-  bool pipe = false;     /* pipe_kernel (mode 3) */
+  int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 4 matrix-core mf_kernel, 5 fp32 fp_kernel */
   bool mf_ok = false;    /* model fits the matrix-core register tables */
   bool mf = false;       /* mf_kernel (mode 4) */
   double mf_ga_ops = 0;  /* int8 matrix-core ops per workgroup per sample: the GRU_A recurrent pass */
@@ -329,6 +326,11 @@ struct LPCNetBatch {
   float *d_trace_logits = nullptr;
   int *d_trace_exc = nullptr;
   int trace_N = 0;
+  /* device -> host status word (pinned, mapped): a kernel that aborts sets
+   * STATUS_* bits; every synchronising entry point checks and clears it */
+  int *h_status = nullptr;
+  int *d_status = nullptr;
+  int spin_limit = FLAG_SPIN_LIMIT_DEFAULT;
   /* diagnostics */
   unsigned long long *d_stamps = nullptr;
   /* timing */
@@ -387,20 +389,19 @@ bool block_may_saturate(const int8_t *w)
   return false;
 }
 
-/* Sample-kernel choice: the wave-per-stream kernel for int8 quad-layout
- * models at >= 256 streams (one wave per stream, NW <= 4 streams per
- * workgroup so each wave has a whole SIMD's register file), otherwise the
- * lockstep kernel (6 waves per stream group; best single-stream latency). */
+/* Sample-kernel choice (mode 0 = automatic):
+ *   5  fp_kernel  -- fp32 models with a dense GRU_B within the FP_* limits
+ *   4  mf_kernel  -- non-saturating int8 models within the MF_* limits
+ *   1  sample_kernel (lockstep) -- every other model: saturating int8 models
+ *      (int16 maddubs saturation emulated) and fp32 models with a sparse GRU_B.
+ * A mode the model cannot run falls back to the lockstep kernel. */
 void choose_kernel(LPCNetBatch *b)
 {
-  b->wave_nw = 0;
-  b->pipe = false;
   b->mf = false;
-  b->info.mfma_ops_per_group_sample = b->mf_ga_ops + b->mf_gb_ops;
   b->fp = false;
-  const bool quad_int8 = b->variant == LPCNET_VARIANT_INT8 && b->reg;
+  b->info.mfma_ops_per_group_sample = 0;
   int mode = b->kernel_mode;
-  if (mode == 0) mode = b->fp_ok ? 5 : (b->mf_ok ? 4 : (quad_int8 ? 3 : 1));
+  if (mode == 0) mode = b->fp_ok ? 5 : (b->mf_ok ? 4 : 1);
   if (mode == 5 && b->fp_ok && fp_lds_bytes() <= 160 * 1024) {
     b->fp = true;
     b->info.streams_per_workgroup = 1;
@@ -408,31 +409,12 @@ void choose_kernel(LPCNetBatch *b)
     b->info.quad_path = 5;
     return;
   }
-  if (mode == 5) mode = b->mf_ok ? 4 : (quad_int8 ? 3 : 1);
   if (mode == 4 && b->mf_ok && mf_lds_bytes(b->S) <= 160 * 1024) {
     b->mf = true;
+    b->info.mfma_ops_per_group_sample = b->mf_ga_ops + b->mf_gb_ops;
     b->info.streams_per_workgroup = b->S;
     b->info.lds_bytes = mf_lds_bytes(b->S);
     b->info.quad_path = 4;
-    return;
-  }
-  if (mode == 4) mode = quad_int8 ? 3 : 1;
-  if (mode == 2 && quad_int8) {
-    int nw = std::min(4, std::max(1, (b->B + 255) / 256));
-    while (nw > 1 && wave_lds_bytes(nw, b->image_bytes) > 160 * 1024) nw /= 2;
-    if (wave_lds_bytes(nw, b->image_bytes) <= 160 * 1024) {
-      b->wave_nw = nw;
-      b->info.streams_per_workgroup = nw;
-      b->info.lds_bytes = wave_lds_bytes(nw, b->image_bytes);
-      b->info.quad_path = 2;
-      return;
-    }
-  }
-  if (mode == 3 && quad_int8 && pipe_lds_bytes(b->S, b->image_bytes) <= 160 * 1024) {
-    b->pipe = true;
-    b->info.streams_per_workgroup = b->S;
-    b->info.lds_bytes = pipe_lds_bytes(b->S, b->image_bytes);
-    b->info.quad_path = 3;
     return;
   }
   b->info.streams_per_workgroup = b->S;
@@ -440,7 +422,12 @@ void choose_kernel(LPCNetBatch *b)
   b->info.quad_path = b->reg ? 1 : 0;
 }
 
-int load_model(LPCNetBatch *b, const unsigned char *data, int len)
+/* Parse, validate and re-tile a weight blob; with upload, replace the
+ * batch's model on its device.  Nothing in *b changes unless every check
+ * passes (the SampleArgs are built locally and committed at the end), so a
+ * failed reload leaves either the previous model intact or, after the old
+ * buffers were freed, no model at all (have_model false). */
+int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload = true)
 {
   std::vector<Arr> L;
   if (!data || len <= 0 || !parse_blob(L, data, len)) {
@@ -559,7 +546,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
     memcpy(&img[off], p, n);
     return off;
   };
-  SampleArgs &sa = b->sa;
+  SampleArgs sa;
   memset(&sa, 0, sizeof(sa));
   std::vector<float4> ga_wf, gb_wf_unused;
   if (int8) sa.gb_rec_off = (int)put(gbrec, 3 * NB * NB);
@@ -806,10 +793,12 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
     set_err("model does not fit the 160 KiB LDS budget");
     return -1;
   }
+  if (!upload) return 0;
 
   if (b->set_device()) { set_err("hipSetDevice failed"); return -1; }
   free_model(b);
-  FrameArgs &fa = b->fa;
+  FrameArgs fa;
+  memset(&fa, 0, sizeof(fa));
 #define UP(dst, src, n) if (!(dst = dev_upload<std::remove_const<std::remove_pointer<decltype(dst)>::type>::type>(b, src, n))) { set_err("device upload failed"); free_model(b); return -1; }
   /* frame-network weights keep the blob's [in][out] layout, padded with
    * FRAME_PREFETCH zero input rows: frame_kernel reads that far ahead */
@@ -870,6 +859,8 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len)
   }
 #undef UP
   sa.image_bytes = (int)img.size();
+  b->sa = sa;
+  b->fa = fa;
   b->variant = variant;
   b->sat = sat;
   b->reg = reg;
@@ -960,6 +951,8 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   sa.pcm = d_pcm;
   sa.preload = std::max(0, std::min(preload, N));
   sa.stamps = b->d_stamps;
+  sa.status = b->d_status;
+  sa.spin_limit = b->spin_limit;
   fa.stamps = b->d_stamps ? b->d_stamps + (size_t)b->B * STAMP_WAVES * 16 : nullptr;
   if (ovl >= 0) {
     sa.cond = b->d_cond[c];
@@ -996,8 +989,6 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   const int lrc = N <= 0 ? 0
                 : b->fp    ? launch_fp(sa, b->stream)
                 : b->mf    ? launch_mf(sa, b->S, b->info.lds_bytes, b->stream)
-                : b->pipe  ? launch_pipe(sa, b->S, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
-                : b->wave_nw ? launch_wave(sa, b->wave_nw, b->sat ? 1 : 0, b->info.lds_bytes, b->stream)
                              : launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream);
   if (lrc) {
     set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -1039,6 +1030,19 @@ void compute_lpc(LPCNetBatch *b, const float *feat, int feat_stride, float *out)
   });
 }
 
+/* After a sync of b->stream: report (and clear) a device-side abort. */
+int check_status(LPCNetBatch *b)
+{
+  const int st = __atomic_load_n(b->h_status, __ATOMIC_ACQUIRE);
+  if (st == 0) return 0;
+  __atomic_store_n(b->h_status, 0, __ATOMIC_RELEASE);
+  if (st & STATUS_FLAG_TIMEOUT)
+    set_err("device abort: an LDS flag wait in the sample kernel exceeded its spin limit; the PCM of this call is invalid");
+  else
+    set_err("device abort: unknown status " + std::to_string(st));
+  return -1;
+}
+
 }  // namespace
 
 /* ======================================================================== */
@@ -1075,6 +1079,9 @@ LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
   ok = ok && hipMalloc(&b->d_state, sizeof(StreamState) * (size_t)nb_streams) == hipSuccess;
   ok = ok && hipMalloc(&b->d_feat, sizeof(float) * NF * (size_t)nb_streams) == hipSuccess;
   ok = ok && hipMalloc(&b->d_pcm, sizeof(short) * FRAME * (size_t)nb_streams) == hipSuccess;
+  ok = ok && hipHostMalloc(&b->h_status, 64, hipHostMallocMapped) == hipSuccess;
+  ok = ok && hipHostGetDevicePointer((void **)&b->d_status, b->h_status, 0) == hipSuccess;
+  if (ok) *b->h_status = 0;
   for (int i = 0; i < 2 && ok; i++) {
     ok = ok && hipMalloc(&b->d_lpc[i], sizeof(float) * NLPC * (size_t)nb_streams) == hipSuccess;
     ok = ok && hipHostMalloc(&b->h_lpc[i], sizeof(float) * NLPC * (size_t)nb_streams, hipHostMallocMapped) == hipSuccess;
@@ -1124,6 +1131,7 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
     if (b->ev_frame[i]) (void)hipEventDestroy(b->ev_frame[i]);
     if (b->ev_samp[i]) (void)hipEventDestroy(b->ev_samp[i]);
   }
+  if (b->h_status) (void)hipHostFree(b->h_status);
   if (b->ev_start) (void)hipEventDestroy(b->ev_start);
   if (b->fstream) (void)hipStreamDestroy(b->fstream);
   for (hipEvent_t e : b->ev_taken) (void)hipEventDestroy(e);
@@ -1143,7 +1151,10 @@ LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *d
 
 LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode)
 {
-  if (!b || mode < 0 || mode > 5) return -1;
+  if (!b || !(mode == 0 || mode == 1 || mode == 4 || mode == 5)) {
+    set_err("kernel mode must be 0 (auto), 1 (lockstep), 4 (mf_kernel) or 5 (fp_kernel)");
+    return -1;
+  }
   b->kernel_mode = mode;
   if (b->have_model) choose_kernel(b);
   return 0;
@@ -1185,6 +1196,13 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_impl(LPCNetBatch *b, const float *feat
   if (N < 0 || N > FRAME || !features || (N > 0 && !pcm) || preload < 0) { set_err("bad arguments"); return -1; }
   if (b->set_device()) return -1;
   if (ensure_trace(b, N)) return -1;
+  /* frames queued by lpcnet_batch_synthesize_frames may still read the pinned
+   * LPC slots: wait for them before h_lpc[0] is rewritten */
+  for (int sl = 0; sl < 2; sl++)
+    if (b->ev_lpc_used[sl]) {
+      HIPCHK(hipEventSynchronize(b->ev_lpc[sl]));
+      b->ev_lpc_used[sl] = false;
+    }
   compute_lpc(b, features, NF, b->h_lpc[0]);
   HIPCHK(hipMemcpyAsync(b->d_lpc[0], b->h_lpc[0], sizeof(float) * NLPC * b->B, hipMemcpyHostToDevice, b->stream));
   HIPCHK(hipMemcpyAsync(b->d_feat, features, sizeof(float) * NF * b->B, hipMemcpyHostToDevice, b->stream));
@@ -1193,7 +1211,7 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_impl(LPCNetBatch *b, const float *feat
   if (launch_frame_step(b, b->d_feat, b->d_lpc[0], b->d_pcm, N, preload)) return -1;
   if (N > 0) HIPCHK(hipMemcpyAsync(pcm, b->d_pcm, sizeof(short) * N * b->B, hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
-  return 0;
+  return check_status(b);
 }
 
 LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features, short *pcm, int N)
@@ -1265,6 +1283,13 @@ LPCNET_EXPORT int lpcnet_batch_sync(LPCNetBatch *b)
 {
   if (!b || b->set_device()) return -1;
   HIPCHK(hipStreamSynchronize(b->stream));
+  return check_status(b);
+}
+
+LPCNET_EXPORT int lpcnet_batch_set_spin_limit(LPCNetBatch *b, int polls)
+{
+  if (!b || polls < 0) return -1;
+  b->spin_limit = polls == 0 ? FLAG_SPIN_LIMIT_DEFAULT : polls;
   return 0;
 }
 
@@ -1414,6 +1439,13 @@ LPCNET_EXPORT int lpcnet_get_size(void) { return (int)sizeof(LPCNetState); }
 
 LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
 {
+  /* src/lpcnet.c:184-200 ends with lpcnet_reset(): re-initialising a live
+   * handle (from lpcnet_create / an earlier lpcnet_init) resets its streams
+   * and keeps its device binding and model; anything else is a fresh handle */
+  if (st->magic == kMagic && st->batch) {
+    lpcnet_batch_reset(st->batch);
+    return 0;
+  }
   st->magic = kMagic;
   const char *d = getenv("LPCNET_DEVICE");
   st->device = d ? atoi(d) : 0;
@@ -1452,9 +1484,31 @@ LPCNET_EXPORT int lpcnet_load_model(LPCNetState *st, const unsigned char *data, 
 
 LPCNET_EXPORT void lpcnet_synthesize(LPCNetState *st, const float *features, short *output, int N)
 {
-  if (!st || !st->batch || lpcnet_batch_synthesize(st->batch, features, output, N) != 0) {
-    if (output && N > 0) memset(output, 0, sizeof(short) * N);
+  /* void in the reference: a failed call (no model bound -- this library has
+   * no compiled-in model, so lpcnet_load_model is required -- or a device
+   * error) outputs silence, sets lpcnet_mi355x_last_error() and says so once
+   * on stderr */
+  static std::atomic<bool> warned{false};
+  int rc;
+  if (!st || !st->batch) {
+    set_err("lpcnet_synthesize: no model bound (call lpcnet_load_model first; liblpcnet_mi355x has no compiled-in model)");
+    rc = -1;
+  } else {
+    rc = lpcnet_batch_synthesize(st->batch, features, output, N);
   }
+  if (rc != 0) {
+    if (output && N > 0) memset(output, 0, sizeof(short) * N);
+    if (!warned.exchange(true)) fprintf(stderr, "liblpcnet_mi355x: %s\n", g_err.c_str());
+  }
+}
+
+/* Host-only check of a weight blob against every rule lpcnet_load_model
+ * applies (no device needed). */
+LPCNET_EXPORT int lpcnet_mi355x_validate_model(const unsigned char *data, int len)
+{
+  LPCNetBatch tmp;
+  tmp.B = 1;
+  return load_model(&tmp, data, len, false);
 }
 
 }  // extern "C"

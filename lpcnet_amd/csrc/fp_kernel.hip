@@ -277,7 +277,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
         xr[d] = fp_xv(xp, orr, d);
       }
       stamp(5);
-      flag_wait<1>(ixseq, n + 1, abort_w);
+      flag_wait<1>(ixseq, n + 1, abort_w, A.spin_limit);
       stamp(0);
       /* GRU_A input (nnet.c:484-491): the 9 embedding gathers of this unit */
       float e[9];
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
 #pragma unroll
           for (int w = 1; w < SAMPLE_WAVES; w++) m = min(m, flag_load(done + w));
           if (m < n + 1)
-            for (int w = 0; w < SAMPLE_WAVES; w++) flag_wait(done + w, n + 1, abort_w);
+            for (int w = 0; w < SAMPLE_WAVES; w++) flag_wait(done + w, n + 1, abort_w, A.spin_limit);
           asm volatile("" ::: "memory");
         }
         stamp(4);
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
       asm volatile("" : "+v"(wrow)); /* same weights every sample: do not hoist their loads */
       const float4 *wp = gbw + wrow;
       float y = gseed;
-      flag_wait(done, n + 1, abort_w);
+      flag_wait(done, n + 1, abort_w, A.spin_limit);
       stamp(1);
       {
         /* ring of GB_RING blocks in flight; wave w+1's flag is read 8 blocks
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
         for (int k = 0; k < NQ; k++) {
           const int d = k % GB_RING, seg = k / 16;
           if ((k & 15) == 16 - 2 * GB_RING && seg + 1 < SAMPLE_WAVES) fnext = flag_load(done + seg + 1);
-          if ((k & 15) == 16 - GB_RING && seg + 1 < SAMPLE_WAVES && fnext < n + 1) flag_wait(done + seg + 1, n + 1, abort_w);
+          if ((k & 15) == 16 - GB_RING && seg + 1 < SAMPLE_WAVES && fnext < n + 1) flag_wait(done + seg + 1, n + 1, abort_w, A.spin_limit);
           const float4 a = wq[d], b = xq[d];
           if (k + GB_RING < NQ) {
             wq[d] = wp[(k + GB_RING) * GB_ROWS];
@@ -515,6 +515,11 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
     for (int k = 0; k < 16; k++) A.stamps[((size_t)blockIdx.x * STAMP_WAVES + wv) * 16 + k] = k < 10 ? stp[k] : 0;
   }
   for (int n = tid; n < A.N; n += FP_THREADS) A.pcm[(size_t)sid * A.N + n] = pcmbuf[n];
+  /* every wave passed the final barrier: the abort word is settled */
+  if (tid == 0 && flag_load(abort_w) && A.status) {
+    A.status[0] = STATUS_FLAG_TIMEOUT; /* plain vector store to the pinned host word */
+    __threadfence_system();
+  }
 }
 
 template <bool TRACE>

@@ -637,712 +637,6 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
   }
 }
 
-/* ------------------------------------------------------------------------ */
-/* wave-per-stream sample network (large batches)                            */
-/*
- * One wavefront runs one stream through all N samples with no workgroup
- * barrier after the image load: the NW waves of a workgroup share the LDS
- * weight image (same quad layout as sample_kernel) and overlap each other's
- * latency.  Lane l owns GRU_A units l + 64j (j = 0..5): pass j is exactly
- * chunk j of the quad image.  GRU_B: pass rb = row block rb, lane (row l%8,
- * k-slice l/8) with three quad groups, reduced across k-slices by shuffles.
- */
-constexpr int WV_X = NA;              /* quantized GRU_A state, [96 column blocks] u32 */
-constexpr int WV_XB = NB;             /* quantized GRU_B state */
-constexpr int WV_ZR = 2 * GB_ROWS * 4;
-constexpr int WV_SB = NB * 4;
-constexpr int WV_PCM = FRAME * 2;
-constexpr int WV_STRIDE = ((WV_X + WV_XB + WV_ZR + WV_SB + WV_PCM) + 15) / 16 * 16;
-
-int wave_lds_bytes(int nw, int image_bytes) { return image_bytes + nw * WV_STRIDE; }
-
-template <int NW, bool SAT>
-__global__ __launch_bounds__(NW * 64) void wave_kernel(SampleArgs A)
-{
-  extern __shared__ uint4 lds4[];
-  unsigned char *lds = (unsigned char *)lds4;
-  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6); /* wave-uniform */
-  const int sid = blockIdx.x * NW + wv;
-  const bool valid = sid < A.nstreams;
-  const bool active = valid && A.st[sid].frame_count > FEATURES_DELAY;
-
-  for (int o = tid; o < A.image_bytes / 16; o += NW * 64) lds4[o] = A.image[o];
-  __syncthreads(); /* the only workgroup barrier */
-
-  unsigned char *wbase = lds + A.image_bytes + wv * WV_STRIDE;
-  unsigned char *xa = wbase;                 /* byte u = quantized unit u (XOR 0x80) */
-  unsigned char *xb = wbase + WV_X;
-  float *zr = (float *)(xb + WV_XB);
-  float *sbuf = zr + 2 * GB_ROWS;
-  short *pcmbuf = (short *)(sbuf + NB);
-  if (!active) {
-    if (valid)
-      for (int n = lane; n < A.N; n += 64) A.pcm[(size_t)sid * A.N + n] = 0;
-    return;
-  }
-  const uint32_t *rcp = (const uint32_t *)(lds + IMG_RCP);
-  const float *ulaw = (const float *)(lds + IMG_ULAW);
-  const float *logit_tab = (const float *)(lds + IMG_LOGIT);
-  const float *fcw = (const float *)(lds + IMG_FCW);
-  const float *fcb = (const float *)(lds + IMG_FCB);
-  const float *fcf = (const float *)(lds + IMG_FCF);
-  const uint4 *wq = (const uint4 *)lds;
-  const uint32_t *cq = (const uint32_t *)lds;
-  StreamState *P = &A.st[sid];
-
-  /* GRU_A units of this lane */
-  float st[6], cz[6], cr[6], ch[6];
-#pragma unroll
-  for (int j = 0; j < 6; j++) {
-    const int u = 64 * j + lane;
-    st[j] = P->gru_a_state[u];
-    cz[j] = P->gru_a_cond[u];
-    cr[j] = P->gru_a_cond[NA + u];
-    ch[j] = P->gru_a_cond[2 * NA + u];
-    xa[u] = (unsigned char)quant_s8(st[j]);
-  }
-  /* GRU_B: lane r = lane % 8 seeds rows 8*rb + r */
-  const int r8 = lane & 7, ks = lane >> 3;
-  float cbr[6];
-#pragma unroll
-  for (int rb = 0; rb < 6; rb++) cbr[rb] = P->gru_b_cond[rb * 8 + r8];
-  float sbv = P->gru_b_state[lane & (NB - 1)];
-  if (lane < NB) xb[lane] = (unsigned char)quant_s8(sbv);
-  float lsr[NLPC], lpr[NLPC];
-#pragma unroll
-  for (int j = 0; j < NLPC; j++) {
-    lsr[j] = P->last_sig[j];
-    lpr[j] = P->lpc[j];
-  }
-  float deemph = P->deemph_mem;
-  int last_exc = P->last_exc;
-  uint32_t rz = P->rng[0], rw = P->rng[1], rj = P->rng[2], rc = P->rng[3];
-  for (int e = lane; e < A.preload; e += 64) pcmbuf[e] = A.pcm[(size_t)sid * A.N + e];
-  const bool tracing = A.trace_logits != nullptr;
-
-  for (int n = 0; n < A.N; n++) {
-    /* ---- per-stream scalars: pred, u-law indices, kiss99 draws ---------- */
-    float pred = 0.f;
-#pragma unroll
-    for (int j = 0; j < NLPC; j++) pred = pred - lsr[j] * lpr[j];
-    const int sig = lin2ulaw_x86(lsr[0]) & 0xFF, prd = lin2ulaw_x86(pred) & 0xFF, exc_in = last_exc & 0xFF;
-    const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
-    const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
-
-    /* ---- GRU_A: gathers in flight during the integer matvec ------------- */
-    const float *e1 = A.emb_sig + sig * GA_ROWS, *e2 = A.emb_pred + prd * GA_ROWS, *e3 = A.emb_exc + exc_in * GA_ROWS;
-    float g1[18], g2[18], g3[18];
-#pragma unroll
-    for (int j = 0; j < 6; j++)
-#pragma unroll
-      for (int g = 0; g < 3; g++) {
-        const int row = g * NA + 64 * j + lane;
-        g1[3 * j + g] = e1[row];
-        g2[3 * j + g] = e2[row];
-        g3[3 * j + g] = e3[row];
-      }
-    int acc[18];
-#pragma unroll
-    for (int j = 0; j < 6; j++)
-#pragma unroll
-      for (int g = 0; g < 3; g++) {
-        int a = SAT ? 0 : A.ga_wsum[g * NA + 64 * j + lane];
-        const uint4 *wp = wq + A.ga_qoff[j][g] + lane;
-        const uint32_t *cp = cq + A.ga_coff[j][g] + (lane >> 3);
-        const int K4 = A.ga_K4[j][g];
-        for (int k = 0; k < K4; k++) {
-          const uint4 w = wp[k * 64];
-          const uint32_t c = cp[k * 8];
-          const uint32_t *x32 = (const uint32_t *)xa;
-          a = dot4<SAT>(w.x, x32[c & 0xFF], a);
-          a = dot4<SAT>(w.y, x32[(c >> 8) & 0xFF], a);
-          a = dot4<SAT>(w.z, x32[(c >> 16) & 0xFF], a);
-          a = dot4<SAT>(w.w, x32[c >> 24], a);
-        }
-        acc[3 * j + g] = a;
-      }
-#pragma unroll
-    for (int j = 0; j < 6; j++) {
-      const int u = 64 * j + lane;
-      const float bz = A.ga_par[u], br = A.ga_par[NA + u], bh = A.ga_par[2 * NA + u];
-      const float dz = A.ga_par[3 * NA + u], dr = A.ga_par[4 * NA + u], dh = A.ga_par[5 * NA + u];
-      const float inz = ((cz[j] + g1[3 * j]) + g2[3 * j]) + g3[3 * j];
-      const float inr = ((cr[j] + g1[3 * j + 1]) + g2[3 * j + 1]) + g3[3 * j + 1];
-      const float inh = ((ch[j] + g1[3 * j + 2]) + g2[3 * j + 2]) + g3[3 * j + 2];
-      const float gz = (float)(acc[3 * j] + cvt_rne(((bz + dz * st[j]) + inz) * kScale)) * kScale1;
-      const float gr = (float)(acc[3 * j + 1] + cvt_rne(((br + dr * st[j]) + inr) * kScale)) * kScale1;
-      const float gh = (float)(acc[3 * j + 2] + cvt_rne((bh + dh * st[j]) * kScale)) * kScale1;
-      const float z = sigmoid_x86(gz, rcp);
-      const float r = sigmoid_x86(gr, rcp);
-      float h = gh * r + inh;
-      h = tanh_x86(h, rcp);
-      st[j] = z * st[j] + (1.f - z) * h;
-    }
-    /* every read of the old x is done (program order, in-order LDS queue) */
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int j = 0; j < 6; j++) xa[64 * j + lane] = (unsigned char)quant_s8(st[j]);
-    __builtin_amdgcn_wave_barrier();
-
-    /* ---- GRU_B gate sums (nnet.c:345-361) -------------------------------- */
-#pragma unroll
-    for (int rb = 0; rb < 6; rb++) {
-      int a = 0, ar = 0;
-      const uint4 *wp = wq + A.gb_qoff[rb] + lane;
-      const uint32_t *cp = cq + A.gb_coff[rb] + ks;
-      const uint32_t *x32 = (const uint32_t *)xa;
-#pragma unroll
-      for (int k = 0; k < REG_GB / 4; k++) {
-        const uint4 w = wp[k * 64];
-        const uint32_t c = cp[k * 8];
-        a = dot4<SAT>(w.x, x32[c & 0xFF], a);
-        a = dot4<SAT>(w.y, x32[(c >> 8) & 0xFF], a);
-        a = dot4<SAT>(w.z, x32[(c >> 16) & 0xFF], a);
-        a = dot4<SAT>(w.w, x32[c >> 24], a);
-      }
-      if (ks < NB / 4)
-        ar = dot4<SAT>(((const uint32_t *)(lds + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r8], ((const uint32_t *)xb)[ks], ar);
-      a += __shfl_xor(a, 8);
-      a += __shfl_xor(a, 16);
-      a += __shfl_xor(a, 32);
-      ar += __shfl_xor(ar, 8);
-      ar += __shfl_xor(ar, 16);
-      ar += __shfl_xor(ar, 32);
-      if (ks == 0) {
-        const int row = rb * 8 + r8;
-        const int seed = cvt_rne((A.gb_par[row] + cbr[rb]) * kScale) + (SAT ? 0 : A.gb_wsum[row]);
-        const int seedr = cvt_rne(A.gb_par[GB_ROWS + row] * kScale) + (SAT ? 0 : A.gb_wsum[GB_ROWS + row]);
-        zr[row] = (float)(seed + a) * kScale1;
-        zr[GB_ROWS + row] = (float)(seedr + ar) * kScale1;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-
-    /* ---- GRU_B update, dual-FC tree sampling, output (as sample_kernel) -- */
-    {
-      const int u = lane & (NB - 1);
-      const float z = sigmoid_x86(zr[u] + zr[GB_ROWS + u], rcp);
-      const float r = sigmoid_x86(zr[NB + u] + zr[GB_ROWS + NB + u], rcp);
-      float h = zr[2 * NB + u] + zr[GB_ROWS + 2 * NB + u] * r;
-      h = tanh_x86(h, rcp);
-      sbv = z * sbv + (1.f - z) * h;
-      if (lane < NB) sbuf[lane] = sbv;
-    }
-    __builtin_amdgcn_wave_barrier();
-    float xv[NB];
-    {
-      const float4 *sb4 = (const float4 *)sbuf;
-#pragma unroll
-      for (int j = 0; j < NB / 4; j++) {
-        const float4 v = sb4[j];
-        xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
-      }
-    }
-    float thr[8];
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      thr[b] = logit_tab[(r0 >> (8 * b)) & 0xFF];
-      thr[b + 4] = logit_tab[(r1 >> (8 * b)) & 0xFF];
-    }
-    const int q = lane >> 1, ch2 = lane & 1;
-    const int qq = q < 15 ? q : 0;
-    const int lvl_in = qq == 0 ? 0 : (qq < 3 ? 1 : (qq < 7 ? 2 : 3));
-    auto node_logit = [&](int node) -> float {
-      float sum = fcb[ch2 * 256 + node];
-      const float *w = fcw + node * 32 + ch2 * 16;
-#pragma unroll
-      for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
-      const float v = fcf[ch2 * 256 + node] * tanh_x86(sum, rcp);
-      const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
-      return ch2 ? o + v : v + o;
-    };
-    float lg[8];
-    int val = 0;
-    {
-      const float l = node_logit(qq + 1);
-      const float t = lvl_in == 0 ? thr[0] : (lvl_in == 1 ? thr[1] : (lvl_in == 2 ? thr[2] : thr[3]));
-      const unsigned long long m = __ballot(t < l);
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const int nd = (1 << b) | val;
-        if (tracing) lg[b] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), 2 * (nd - 1)));
-        val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
-      }
-    }
-    {
-      const int lvl = 4 + lvl_in;
-      const int off = qq + 1 - (1 << (lvl - 4));
-      const float l = node_logit((1 << lvl) | (val << (lvl - 4)) | off);
-      const float t = lvl_in == 0 ? thr[4] : (lvl_in == 1 ? thr[5] : (lvl_in == 2 ? thr[6] : thr[7]));
-      const unsigned long long m = __ballot(t < l);
-#pragma unroll
-      for (int b = 4; b < 8; b++) {
-        const int qi = (1 << (b - 4)) - 1 + (val & ((1 << (b - 4)) - 1));
-        if (tracing) lg[b] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), 2 * qi));
-        val = (val << 1) | (int)((m >> (2 * qi)) & 1ull);
-      }
-    }
-    int exc = val;
-    float pcm;
-    if (n < A.preload) {
-      const float o_in = (float)pcmbuf[n];
-      const float pd = kPreemph * deemph;
-      exc = lin2ulaw_x86((o_in - pd) - pred);
-      pcm = o_in - pd;
-    } else {
-      pcm = pred + ulaw[exc];
-    }
-#pragma unroll
-    for (int j = NLPC - 1; j > 0; j--) lsr[j] = lsr[j - 1];
-    lsr[0] = pcm;
-    last_exc = exc;
-    float o = pcm + kPreemph * deemph;
-    deemph = o;
-    if (o < -32767) o = -32767;
-    if (o > 32767) o = 32767;
-    if (lane == 0 && n >= A.preload) pcmbuf[n] = (short)round_half_up(o);
-    if (tracing && lane < 8) {
-      float v = lg[0];
-#pragma unroll
-      for (int b = 1; b < 8; b++) v = lane == b ? lg[b] : v;
-      A.trace_logits[((size_t)sid * A.N + n) * 8 + lane] = v;
-    }
-    if (A.trace_exc && lane == 0) A.trace_exc[(size_t)sid * A.N + n] = exc;
-    if (lane < NB) xb[lane] = (unsigned char)quant_s8(sbv);
-    __builtin_amdgcn_wave_barrier();
-  }
-
-  /* ---- write back ---------------------------------------------------------- */
-#pragma unroll
-  for (int j = 0; j < 6; j++) P->gru_a_state[64 * j + lane] = st[j];
-  if (lane < NB) P->gru_b_state[lane] = sbv;
-  if (lane == 0) {
-#pragma unroll
-    for (int j = 0; j < NLPC; j++) P->last_sig[j] = lsr[j];
-    P->deemph_mem = deemph;
-    P->last_exc = last_exc;
-    P->rng[0] = rz; P->rng[1] = rw; P->rng[2] = rj; P->rng[3] = rc;
-  }
-  for (int e = lane; e < A.N; e += 64) A.pcm[(size_t)sid * A.N + e] = pcmbuf[e];
-}
-
-template <int NW, bool SAT>
-static int launch_wave_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
-{
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)wave_kernel<NW, SAT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-        hipSuccess)
-      return -1;
-    attr_set = true;
-  }
-  int grid = (a.nstreams + NW - 1) / NW;
-  hipLaunchKernelGGL((wave_kernel<NW, SAT>), dim3(grid), dim3(NW * 64), lds_bytes, stream, a);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-int launch_wave(const SampleArgs &a, int nw, int sat, int lds_bytes, void *stream)
-{
-  hipStream_t st = (hipStream_t)stream;
-#define W(n) if (nw == n) return sat ? launch_wave_t<n, true>(a, lds_bytes, st) : launch_wave_t<n, false>(a, lds_bytes, st);
-  W(1) W(2) W(4) W(8) W(16)
-#undef W
-  return -1;
-}
-
-/* ------------------------------------------------------------------------ */
-/* ------------------------------------------------------------------------ */
-/* pipe_kernel: fixed wave roles, the GRU_A recurrent product of sample n+1
- * overlapping the sampling of sample n.
- *
- * The recurrent part of GRU_A, W·q(h_A(n)) (sparse_sgemv_accum8x4 inside
- * compute_sparse_gru, nnet.c:441), depends on the GRU_A state only, not on
- * the excitation sampled at n (which enters sample n+1 through the embedding
- * gathers, nnet.c:484-491).  So while the sampler waves run GRU_B's update
- * and the dual-FC tree walk of sample n (nnet.c:362-371, 163-214), the six
- * GRU_A waves already accumulate W·q(h_A(n)) for sample n+1 in registers.
- * Per sample, three workgroup barriers:
- *   X  ix(n) (sig, pred, exc indices) published by the samplers
- *      GRU_A waves: embedding gathers + elementwise GRU_A(n) -> q(h_A(n))
- *      sampler waves: the two kiss99 draws and their logit thresholds
- *   Y  q(h_A(n)) complete
- *      GRU_A wave w: GRU_B gate sums of row block w (nnet.c:345-361)
- *   Z  GRU_B gate sums complete
- *      GRU_A waves: W·q(h_A(n)) for sample n+1
- *      sampler waves: GRU_B update, tree walk, output, pred(n+1) -> ix(n+1)
- * Same arithmetic as sample_kernel's quad path, term for term. */
-template <int S>
-struct PipeLds {
-  static constexpr int x = (NA / 4) * S * 4;   /* quantized GRU_A state (single buffer) */
-  static constexpr int xb = (NB / 4) * S * 4;  /* quantized GRU_B state */
-  static constexpr int sb = S * NB * 4;        /* float GRU_B state */
-  static constexpr int zr = S * 2 * GB_ROWS * 4;
-  static constexpr int ix = S * 4 * 4;
-  static constexpr int pcm = ((S * FRAME * 2 + 15) / 16) * 16;
-  static constexpr int total = x + xb + sb + zr + ix + pcm;
-};
-
-/* LDS: [image | regions] */
-int pipe_lds_bytes(int S, int image_bytes)
-{
-  return image_bytes + (S == 4 ? PipeLds<4>::total : (S == 2 ? PipeLds<2>::total : PipeLds<1>::total));
-}
-
-template <int S, bool SAT, bool TRACE>
-__global__ __launch_bounds__(PIPE_THREADS) void pipe_kernel(SampleArgs A)
-{
-  extern __shared__ uint4 lds4[];
-  unsigned char *lds = (unsigned char *)lds4;
-  using L = PipeLds<S>;
-  unsigned char *img = lds;
-  unsigned char *xa = lds + A.image_bytes;
-  unsigned char *xb = xa + L::x;
-  float *sbuf = (float *)(xb + L::xb);
-  float *zr = sbuf + S * NB;
-  int *ix = (int *)(zr + S * 2 * GB_ROWS);
-  short *pcmbuf = (short *)(ix + S * 4);
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int s0 = blockIdx.x * S;
-  const uint32_t *rcp = (const uint32_t *)(img + IMG_RCP);
-
-  bool active[S];
-  bool any = false;
-  for (int s = 0; s < S; s++) {
-    const int sid = s0 + s;
-    active[s] = sid < A.nstreams && A.st[sid].frame_count > FEATURES_DELAY;
-    any |= active[s];
-  }
-  if (!any) {
-    for (int e = tid; e < S * A.N; e += PIPE_THREADS) {
-      const int s = e / A.N, n = e % A.N;
-      if (s0 + s < A.nstreams) A.pcm[(size_t)(s0 + s) * A.N + n] = 0;
-    }
-    return;
-  }
-  {
-    uint4 *img4 = (uint4 *)img;
-    const int n16 = A.image_bytes / 16;
-    for (int o = tid; o < n16; o += PIPE_THREADS) img4[o] = A.image[o];
-  }
-  for (int e = tid; e < S * A.preload; e += PIPE_THREADS) {
-    const int s = e / A.preload, n = e % A.preload;
-    pcmbuf[s * FRAME + n] = A.pcm[(size_t)min(s0 + s, A.nstreams - 1) * A.N + n];
-  }
-
-  const bool stamping = A.stamps != nullptr;
-  unsigned long long stp[16] = {};
-  unsigned long long t_prev = 0, t_loop0 = 0;
-  auto stamp = [&](int k) {
-    if (stamping) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      stp[k] += t - t_prev;
-      t_prev = t;
-    }
-  };
-  auto stamp_start = [&]() {
-    if (stamping) t_prev = t_loop0 = __builtin_amdgcn_s_memtime();
-  };
-
-  /* Roles (wave-uniform): waves 0..5 GRU_A (thread = unit), waves 6..7
-   * samplers.  Each role runs its own sample loop with the same barrier
-   * sequence (prologue, then X, Y, Z per sample, then one final), so the
-   * registers of one role are not live in the other's code. */
-  if (wv < SAMPLE_WAVES) {
-    /* ======================= GRU_A role ================================== */
-    const uint4 *wq = (const uint4 *)img;
-    const uint32_t *cq = (const uint32_t *)img;
-    const int i = tid;
-    const int K4z = A.ga_K4[wv][0], K4r = A.ga_K4[wv][1], K4h = A.ga_K4[wv][2];
-    const int qoff = A.ga_qoff[wv][0], coff = A.ga_coff[wv][0];
-    const float bz = A.ga_par[i], br = A.ga_par[NA + i], bh = A.ga_par[2 * NA + i];
-    const float dz = A.ga_par[3 * NA + i], dr = A.ga_par[4 * NA + i], dh = A.ga_par[5 * NA + i];
-    const int wsz = A.ga_wsum[i], wsr = A.ga_wsum[NA + i], wsh = A.ga_wsum[2 * NA + i];
-    const int rb = wv, r8 = lane & 7, ks = lane >> 3, row = rb * 8 + r8;
-    float st[S], cz[S], cr[S], ch[S];
-    int gb_seed[S];
-    for (int s = 0; s < S; s++) {
-      const StreamState *p = &A.st[min(s0 + s, A.nstreams - 1)];
-      st[s] = p->gru_a_state[i];
-      cz[s] = p->gru_a_cond[i];
-      cr[s] = p->gru_a_cond[NA + i];
-      ch[s] = p->gru_a_cond[2 * NA + i];
-      gb_seed[s] = cvt_rne((A.gb_par[row] + p->gru_b_cond[row]) * kScale) + (SAT ? 0 : A.gb_wsum[row]);
-    }
-    const int gb_seedr = cvt_rne(A.gb_par[GB_ROWS + row] * kScale) + (SAT ? 0 : A.gb_wsum[GB_ROWS + row]);
-    __syncthreads(); /* image in LDS */
-    for (int s = 0; s < S; s++) xa[(i >> 2) * S * 4 + s * 4 + (i & 3)] = (unsigned char)quant_s8(st[s]);
-    __syncthreads(); /* initial q(h_A), q(h_B), ix */
-    stamp_start();
-
-    int az[S], ar[S], ah[S];
-    auto recurrent = [&]() {
-      for (int s = 0; s < S; s++) {
-        az[s] = SAT ? 0 : wsz;
-        ar[s] = SAT ? 0 : wsr;
-        ah[s] = SAT ? 0 : wsh;
-      }
-      gru_a_stream<S, SAT>(xa, wq, cq, qoff, coff, K4z, K4r, K4h, lane, az, ar, ah);
-    };
-    recurrent();
-    for (int n = 0; n < A.N; n++) {
-      stamp(4);
-      __syncthreads(); /* X */
-      stamp(5);
-      {
-        /* GRU_A input (nnet.c:484-491): all 9*S gathers in flight at once */
-        float e[S][9];
-        for (int s = 0; s < S; s++) {
-          /* the indices are the same in every lane: scalar row addresses */
-          const int4 v = *(const int4 *)(ix + s * 4);
-          const float *e1 = A.emb_sig + (__builtin_amdgcn_readfirstlane(v.x) & 0xFF) * GA_ROWS;
-          const float *e2 = A.emb_pred + (__builtin_amdgcn_readfirstlane(v.y) & 0xFF) * GA_ROWS;
-          const float *e3 = A.emb_exc + (__builtin_amdgcn_readfirstlane(v.z) & 0xFF) * GA_ROWS;
-#pragma unroll
-          for (int g = 0; g < 3; g++) {
-            e[s][g] = e1[g * NA + i];
-            e[s][3 + g] = e2[g * NA + i];
-            e[s][6 + g] = e3[g * NA + i];
-          }
-        }
-        /* compute_sparse_gru elementwise (nnet.c:431-447) */
-        float zrv[2 * S], hv[S], inh[S];
-        for (int s = 0; s < S; s++) {
-          const float inz = ((cz[s] + e[s][0]) + e[s][3]) + e[s][6];
-          const float inr = ((cr[s] + e[s][1]) + e[s][4]) + e[s][7];
-          inh[s] = ((ch[s] + e[s][2]) + e[s][5]) + e[s][8];
-          zrv[s] = (float)(az[s] + cvt_rne(((bz + dz * st[s]) + inz) * kScale)) * kScale1;
-          zrv[S + s] = (float)(ar[s] + cvt_rne(((br + dr * st[s]) + inr) * kScale)) * kScale1;
-          hv[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
-        }
-        sigmoid_x86_n<2 * S>(zrv, rcp);
-        for (int s = 0; s < S; s++) hv[s] = hv[s] * zrv[S + s] + inh[s];
-        tanh_x86_n<S>(hv, rcp);
-        for (int s = 0; s < S; s++) {
-          st[s] = zrv[s] * st[s] + (1.f - zrv[s]) * hv[s];
-          xa[(i >> 2) * S * 4 + s * 4 + (i & 3)] = (unsigned char)quant_s8(st[s]);
-        }
-      }
-      stamp(0);
-      __syncthreads(); /* Y */
-      stamp(1);
-      {
-        /* GRU_B gate sums of row block rb (nnet.c:345-361) */
-        int acc[S], accr[S];
-        for (int s = 0; s < S; s++) { acc[s] = 0; accr[s] = 0; }
-        gru_a_stream<S, SAT>(xa, wq, cq, A.gb_qoff[rb], A.gb_coff[rb], REG_GB / 4, 0, 0, lane, acc, acc, acc);
-        if (ks < NB / 4) {
-          const uint32_t w = ((const uint32_t *)(img + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r8];
-          dot_streams<S, SAT>(xb, ks * S * 4, w, accr);
-        }
-        for (int s = 0; s < S; s++) {
-          acc[s] = sum_lanes_xor8_16_32(acc[s]);
-          accr[s] = sum_lanes_xor8_16_32(accr[s]);
-        }
-        if (ks == 0) {
-          for (int s = 0; s < S; s++) {
-            zr[s * 2 * GB_ROWS + row] = (float)(gb_seed[s] + acc[s]) * kScale1;
-            zr[s * 2 * GB_ROWS + GB_ROWS + row] = (float)(gb_seedr + accr[s]) * kScale1;
-          }
-        }
-      }
-      stamp(2);
-      __syncthreads(); /* Z */
-      stamp(3);
-      if (n + 1 < A.N) recurrent(); /* W q(h_A(n)) for sample n+1, beside the sampling of n */
-    }
-    stamp(4);
-    __syncthreads(); /* final */
-    stamp(5);
-    for (int s = 0; s < S; s++)
-      if (active[s]) A.st[s0 + s].gru_a_state[i] = st[s];
-  } else {
-    /* ======================= sampler role ================================ */
-    const float *logit_tab = (const float *)(img + IMG_LOGIT);
-    /* with S=4 a sampler wave carries two streams, one per 32-lane half */
-    const int sw = wv - SAMPLE_WAVES;
-    const int half = lane >> 5, hl = lane & 31;
-    const int my_s = S == 4 ? 2 * sw + half : sw;
-    const bool samp = my_s < S;                         /* wave-uniform */
-    const bool samp_w = samp && (S == 4 || half == 0);  /* lanes owning the stream's outputs */
-    const int ms = samp ? my_s : 0;
-    const bool my_active = samp && s0 + ms < A.nstreams && A.st[s0 + ms].frame_count > FEATURES_DELAY;
-
-    float lsr[NLPC], lpr[NLPC];
-    float sbv = 0.f, pred = 0.f, deemph = 0.f;
-    uint32_t rz = 0, rw = 0, rj = 0, rc = 0;
-    int last_exc = 0;
-    {
-      const StreamState *p = &A.st[min(s0 + ms, A.nstreams - 1)];
-#pragma unroll
-      for (int j = 0; j < NLPC; j++) {
-        lsr[j] = p->last_sig[j];
-        lpr[j] = p->lpc[j];
-      }
-      sbv = p->gru_b_state[hl & (NB - 1)];
-      deemph = p->deemph_mem;
-      last_exc = p->last_exc;
-      rz = p->rng[0]; rw = p->rng[1]; rj = p->rng[2]; rc = p->rng[3];
-    }
-    __syncthreads(); /* image in LDS */
-    FcLane F;
-    F.init(img, lane);
-    if (samp_w && hl < NB) {
-      xb[(hl >> 2) * S * 4 + ms * 4 + (hl & 3)] = (unsigned char)quant_s8(sbv);
-      sbuf[ms * NB + hl] = sbv;
-    }
-    if (samp) {
-      /* pred and the u-law indices of the first sample (lpcnet.c:252-254) */
-      float p2 = 0.f;
-#pragma unroll
-      for (int j = 0; j < NLPC; j++) p2 = p2 - lsr[j] * lpr[j];
-      pred = p2;
-      if (samp_w && hl == 0) *(int4 *)(ix + ms * 4) = make_int4(lin2ulaw_x86(lsr[0]), lin2ulaw_x86(pred), last_exc, 0);
-    }
-    __syncthreads(); /* initial q(h_A), q(h_B), ix */
-    stamp_start();
-
-    float t03 = 0.f, t47 = 0.f;
-    constexpr bool tracing = TRACE;
-    /* Bookkeeping of sample n (lpcnet.c:260-270: LPC history shift,
-     * de-emphasis, output, q(h_B)) is deferred into the X->Y interval of
-     * sample n+1, where the sampler waves are otherwise idle; only the next
-     * indices ix(n+1) stay on the per-sample critical path. */
-    float pend_pcm = 0.f, pend_pred = 0.f;
-    int pend_exc = 0, pend_n = -1;
-    auto finish = [&]() {
-      if (pend_n < 0) return;
-#pragma unroll
-      for (int j = NLPC - 1; j > 0; j--) lsr[j] = lsr[j - 1];
-      lsr[0] = pend_pcm;
-      last_exc = pend_exc;
-      pred = pend_pred;
-      float o = pend_pcm + kPreemph * deemph;
-      deemph = o;
-      if (o < -32767) o = -32767;
-      if (o > 32767) o = 32767;
-      if (samp_w && hl == 0 && pend_n >= A.preload) pcmbuf[ms * FRAME + pend_n] = (short)round_half_up(o);
-      if (samp_w && hl < NB) xb[(hl >> 2) * S * 4 + ms * 4 + (hl & 3)] = (unsigned char)quant_s8(sbv);
-      pend_n = -1;
-    };
-    for (int n = 0; n < A.N; n++) {
-      stamp(4);
-      __syncthreads(); /* X */
-      stamp(5);
-      if (samp) {
-        finish();
-        stamp(13);
-        /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
-        const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
-        const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
-        lane_thresholds(F, logit_tab, r0, r1, t03, t47);
-      }
-      stamp(0);
-      __syncthreads(); /* Y */
-      stamp(1);
-      stamp(2);
-      __syncthreads(); /* Z */
-      stamp(3);
-      if (!samp) continue;
-      const int s = ms;
-      const float *zs = zr + s * 2 * GB_ROWS;
-      {
-        /* GRU_B elementwise (nnet.c:362-371); lanes >= 16 of a half duplicate */
-        const int u = hl & (NB - 1);
-        float zrb[2] = {zs[u] + zs[GB_ROWS + u], zs[NB + u] + zs[GB_ROWS + NB + u]};
-        sigmoid_x86_n<2>(zrb, rcp);
-        float h[1] = {zs[2 * NB + u] + zs[GB_ROWS + 2 * NB + u] * zrb[1]};
-        tanh_x86_n<1>(h, rcp);
-        sbv = zrb[0] * sbv + (1.f - zrb[0]) * h[0];
-        if (samp_w && hl < NB) sbuf[s * NB + hl] = sbv;
-      }
-      stamp(8);
-      /* same-wave LDS exchange (measured faster than 32 v_readlane: gfx9
-       * VALU ops read one SGPR each and SGPR hazards add wait states) */
-      __builtin_amdgcn_wave_barrier();
-      float xv[NB];
-      {
-        const float4 *sb4 = (const float4 *)(sbuf + s * NB);
-#pragma unroll
-        for (int j = 0; j < NB / 4; j++) {
-          const float4 v = sb4[j];
-          xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
-        }
-      }
-      stamp(9);
-      const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + s * FRAME + n : nullptr,
-                                            deemph);
-      stamp(11);
-      if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + s * 4) = make_int4(R.su, R.pu, R.exc, 0);
-      if (tracing && samp_w && hl < 8 && my_active) {
-        float v = R.lg[0];
-#pragma unroll
-        for (int b = 1; b < 8; b++) v = hl == b ? R.lg[b] : v;
-        A.trace_logits[((size_t)(s0 + s) * A.N + n) * 8 + hl] = v;
-      }
-      if (A.trace_exc && samp_w && hl == 0 && my_active) A.trace_exc[(size_t)(s0 + s) * A.N + n] = R.exc;
-      pend_pcm = R.pcm;
-      pend_pred = R.pn;
-      pend_exc = R.exc;
-      pend_n = n;
-      stamp(12);
-    }
-    if (samp) finish();
-    stamp(4);
-    __syncthreads(); /* final */
-    stamp(5);
-    if (samp_w && my_active) {
-      StreamState *p = &A.st[s0 + ms];
-      if (hl < NB) p->gru_b_state[hl] = sbv;
-      if (hl == 0) {
-#pragma unroll
-        for (int j = 0; j < NLPC; j++) p->last_sig[j] = lsr[j];
-        p->deemph_mem = deemph;
-        p->last_exc = last_exc;
-        p->rng[0] = rz; p->rng[1] = rw; p->rng[2] = rj; p->rng[3] = rc;
-      }
-    }
-  }
-  if (stamping && lane == 0) {
-    stp[6] = __builtin_amdgcn_s_memtime() - t_loop0;
-    stp[7] = (unsigned long long)A.N;
-    for (int k = 0; k < 16; k++) A.stamps[((size_t)blockIdx.x * STAMP_WAVES + wv) * 16 + k] = stp[k];
-  }
-  for (int e = tid; e < S * A.N; e += PIPE_THREADS) {
-    const int s = e / A.N, n = e % A.N;
-    if (s0 + s < A.nstreams) A.pcm[(size_t)(s0 + s) * A.N + n] = active[s] ? pcmbuf[s * FRAME + n] : (short)0;
-  }
-}
-
-template <int S, bool SAT, bool TRACE>
-static int launch_pipe_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
-{
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)pipe_kernel<S, SAT, TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return -1;
-    attr_set = true;
-  }
-  const int grid = (a.nstreams + S - 1) / S;
-  hipLaunchKernelGGL((pipe_kernel<S, SAT, TRACE>), dim3(grid), dim3(PIPE_THREADS), lds_bytes, stream, a);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-template <int S, bool SAT>
-static int launch_pipe_s(const SampleArgs &a, int lds_bytes, hipStream_t st)
-{
-  return a.trace_logits ? launch_pipe_t<S, SAT, true>(a, lds_bytes, st) : launch_pipe_t<S, SAT, false>(a, lds_bytes, st);
-}
-
-int launch_pipe(const SampleArgs &a, int S, int sat, int lds_bytes, void *stream)
-{
-  hipStream_t st = (hipStream_t)stream;
-  if (S == 4) return sat ? launch_pipe_s<4, true>(a, lds_bytes, st) : launch_pipe_s<4, false>(a, lds_bytes, st);
-  if (S == 2) return sat ? launch_pipe_s<2, true>(a, lds_bytes, st) : launch_pipe_s<2, false>(a, lds_bytes, st);
-  return sat ? launch_pipe_s<1, true>(a, lds_bytes, st) : launch_pipe_s<1, false>(a, lds_bytes, st);
-}
-
 template <int S, int V, bool SAT, bool REG>
 static int launch_sample_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
 {

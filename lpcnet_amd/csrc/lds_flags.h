@@ -17,19 +17,18 @@ __device__ __forceinline__ int flag_load(const int *p)
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-/* Spin until *p >= v.  A wait that outlives FLAG_SPIN_LIMIT polls (a bug,
- * never a legal schedule) sets the workgroup's abort word, after which every
- * wait returns at once: the kernel then finishes with wrong output instead
- * of hanging the device. */
-constexpr int FLAG_SPIN_LIMIT = 1 << 20;
+/* Spin until *p >= v.  A wait that outlives `limit` polls (a bug, never a
+ * legal schedule) sets the workgroup's abort word, after which every wait
+ * returns at once: the kernel finishes instead of hanging the device, and
+ * reports the abort through SampleArgs::status (the host call returns -1). */
 /* SLEEP > 0: s_sleep between polls (64 clocks per unit) -- for long waits,
  * so idle waves do not flood the LDS the working waves depend on. */
 template <int SLEEP = 0>
-__device__ __forceinline__ void flag_wait(const int *p, int v, int *abort_w)
+__device__ __forceinline__ void flag_wait(const int *p, int v, int *abort_w, int limit)
 {
   for (int it = 0; flag_load(p) < v; it++) {
     if (flag_load(abort_w)) break;
-    if (it > FLAG_SPIN_LIMIT) {
+    if (it > limit) {
       __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       break;
     }

@@ -25,9 +25,7 @@ constexpr int GB_ROWS = 3 * NB;
 constexpr int FEATURES_DELAY = 2;
 constexpr int SAMPLE_THREADS = 384; /* one thread per GRU_A unit */
 constexpr int SAMPLE_WAVES = SAMPLE_THREADS / 64;
-constexpr int PIPE_THREADS = 512;   /* pipe_kernel: 6 GRU_A waves + 2 sampler waves */
-constexpr int PIPE_WAVES = PIPE_THREADS / 64;
-constexpr int STAMP_WAVES = PIPE_WAVES; /* stamps are [workgroup][STAMP_WAVES][16] */
+constexpr int STAMP_WAVES = 8;      /* stamps are [workgroup][STAMP_WAVES][16] */
 constexpr int FRAME_STREAMS = 4;    /* streams per frame-network workgroup */
 constexpr int FRAME_PREFETCH = 64;  /* zero input rows padding each frame-network weight matrix */
 constexpr int REG_GB = 12;          /* GRU_B input slots per lane: block k = ks + 8*j, j < 12 */
@@ -171,7 +169,15 @@ struct SampleArgs {
   unsigned long long *stamps; /* optional diagnostics [grid][STAMP_WAVES][16] s_memtime sums */
   float *trace_logits;   /* optional [B][N][8] */
   int *trace_exc;        /* optional [B][N] */
+  int *status;           /* device view of the batch's pinned status word: a
+                            kernel that aborts sets bits (STATUS_*), the host
+                            checks after every sync */
+  int spin_limit;        /* polls before an LDS flag wait aborts (FLAG_SPIN_LIMIT_DEFAULT) */
 };
+
+constexpr int FLAG_SPIN_LIMIT_DEFAULT = 1 << 20; /* lpcnet_batch_set_spin_limit */
+/* Status bits a sample kernel reports to the host (SampleArgs::status). */
+constexpr int STATUS_FLAG_TIMEOUT = 1; /* an LDS flag wait exceeded spin_limit: output invalid */
 
 /* The frame step's outputs as a sample kernel reads them: the FrameCond
  * copy when the launch has one, else the stream state. */

@@ -536,10 +536,12 @@ static const int *find_idx(const warray *l, int n, const char *name, int nb_in, 
     *total = 0;
     while (remain > 0) {
       int nb = *idx++;
-      if (remain < nb + 1) return NULL;
+      /* nb < 0 and pos < 0: the reference's find_idx_check loops forever /
+       * accepts an out-of-bounds block here; rejected */
+      if (nb < 0 || remain < nb + 1) return NULL;
       for (int k = 0; k < nb; k++) {
         int pos = *idx++;
-        if (pos + 3 >= nb_in || (pos & 3)) return NULL;
+        if (pos + 3 >= nb_in || (pos & 3) || pos < 0) return NULL;
       }
       nb_out -= 8;
       remain -= nb + 1;

@@ -30,28 +30,25 @@ def blobs():
 
 
 @pytest.mark.parametrize("name,kernel", [("streams_int8", 1), ("streams_fp32", 1), ("streams_int8_sat", 1),
-                                         ("streams_int8", 2), ("streams_int8_sat", 2),
-                                         ("streams_int8", 3), ("streams_int8_sat", 3), ("streams_fp32", 3),
                                          ("streams_int8", 4), ("streams_int8_sat", 4), ("streams_fp32", 4),
                                          ("streams_fp32", 5), ("streams_int8", 5), ("streams_int8_sat", 5),
-                                         ("streams_int8", 0), ("streams_fp32", 0)])
+                                         ("streams_int8", 0), ("streams_fp32", 0), ("streams_int8_sat", 0)])
 def test_batch_matches_golden(require_gpu, blobs, name, kernel):
-    """kernel 1: lockstep sample_kernel, 2: wave-per-stream, 3: pipelined,
-    4: pipelined on the matrix cores (saturating models fall back to 3),
-    5: fp32 latency kernel (int8 models fall back to 4 / 3),
-    0: automatic (4 for non-saturating int8, 5 for fp32).  fp32 models run
-    the lockstep kernel for every mode but 5 and 0."""
+    """kernel 1: lockstep sample_kernel (quad_path 1 for int8 quad layouts,
+    0 for fp32), 4: mf_kernel on the matrix cores, 5: fp_kernel (fp32),
+    0: automatic (4 for non-saturating int8, 5 for fp32, 1 otherwise); a
+    mode the model cannot run falls back to the lockstep kernel."""
     G = np.load(os.path.join(GOLD, name + ".npz"))
     streams = list(G["streams"])
     F = G["pcm"].shape[1]
     b = L.LPCNetBatch(len(streams), 0, blobs[name])
     b.set_kernel(kernel)
     if name == "streams_fp32":
-        expect = {0: 5, 1: 0, 3: 0, 4: 0, 5: 5}[kernel]
+        expect = {0: 5, 1: 0, 4: 0, 5: 5}[kernel]
     elif name.endswith("_sat"):
-        expect = {0: 3, 1: 1, 2: 2, 3: 3, 4: 3, 5: 3}[kernel]
+        expect = {0: 1, 1: 1, 4: 1, 5: 1}[kernel]
     else:
-        expect = {0: 4, 1: 1, 2: 2, 3: 3, 4: 4, 5: 4}[kernel]
+        expect = {0: 4, 1: 1, 4: 4, 5: 1}[kernel]
     assert b.info().quad_path == expect
     info = b.info()
     assert info.variant == int(G["variant"])
@@ -87,13 +84,12 @@ def test_single_stream_api_matches_golden(require_gpu, blobs):
 
 @pytest.mark.parametrize("B,check,kernel", [(512, (0, 255, 511), 1), (1024, (0, 3, 517, 1023), 1),
                                             (1100, (1099, 1024, 5), 1), (1024, (0, 3, 517, 1023), 0),
-                                            (1101, (1100, 1024, 5), 0), (300, (299, 7), 2),
-                                            (513, (512, 1, 300), 3), (1030, (1029, 1027, 2), 3),
+                                            (1101, (1100, 1024, 5), 0), (300, (299, 7), 0),
                                             (513, (512, 1, 300), 4), (1030, (1029, 1027, 2), 4),
                                             (1024, (0, 511, 1023), 4)])
 def test_large_batch_streams_match_oracle(require_gpu, blobs, B, check, kernel):
-    """Lockstep kernel at 2 and 4 streams/workgroup, the wave-per-stream kernel
-    (auto at >= 256 streams), ragged last workgroups, against the oracle."""
+    """Lockstep kernel at 2 and 4 streams/workgroup, mf_kernel at 1, 2 and 4
+    streams/workgroup, ragged last workgroups, against the oracle."""
     F = 5
     blob = blobs["streams_int8"]
     b = L.LPCNetBatch(B, 0, blob)
@@ -254,7 +250,7 @@ def test_full_size_properties(require_gpu, blobs):
     assert np.abs(o1[:, 2:].astype(np.float64)).mean() > 100
 
 
-@pytest.mark.parametrize("kernel,variant", [(1, 0), (2, 0), (3, 0), (4, 0), (5, 1), (1, 1)])
+@pytest.mark.parametrize("kernel,variant", [(1, 0), (4, 0), (5, 1), (1, 1)])
 def test_preload_teacher_forcing_matches_oracle(require_gpu, blobs, kernel, variant):
     """lpcnet_synthesize_impl with preload (lpcnet.c:256-259, the PLC entry)."""
     blob = blobs["streams_fp32" if variant else "streams_int8"]
@@ -311,3 +307,120 @@ def test_state_save_restore_rollback(require_gpu, blobs):
     b.restore_state(1, snap)
     second = np.stack([b.synthesize(allf[f]) for f in range(4, 6)])
     assert np.array_equal(first[:, 1], second[:, 1])
+
+
+CHECK256 = (0, 1, 128, 254, 255)
+
+
+def test_batch256_auto_kernel_matches_oracle(require_gpu, blobs):
+    """BASELINE configs[2]: 256 streams on the automatic kernel (mf_kernel<1>,
+    256 workgroups; one-stream frame-kernel workgroups) through
+    lpcnet_batch_synthesize, against the oracle on streams 0, 1, 128, 254,
+    255: PCM, the 8 traced pre-sampling logits bit for bit, the excitation,
+    and the final GRU states; then lpcnet_batch_synthesize_frames over the
+    same frames gives the same PCM for every stream."""
+    B, F = 256, 6
+    blob = blobs["streams_int8"]
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    b = L.LPCNetBatch(B, 0, blob)
+    info = b.info()
+    assert info.quad_path == 4 and info.streams_per_workgroup == 1
+    b.set_trace(True)
+    refs = {s: O.Oracle(blob, 0) for s in CHECK256}
+    outs = []
+    for f in range(F):
+        out = b.synthesize(allf[f])
+        outs.append(out)
+        lg, ex = b.get_trace(160)
+        for s in CHECK256:
+            exp, elg, eex, _ = refs[s].synthesize(allf[f, s], 160, trace=True)
+            assert np.array_equal(out[s], exp), (f, s)
+            if f >= 2:
+                assert np.array_equal(ex[s], eex), (f, s)
+                assert np.array_equal(bits(lg[s]), bits(elg)), (f, s)
+    for s in CHECK256:
+        a, g = refs[s].state()
+        st = b.get_state(s)
+        assert np.array_equal(bits(st["gru_a_state"]), bits(a)), s
+        assert np.array_equal(bits(st["gru_b_state"]), bits(g)), s
+    assert np.abs(np.stack(outs)[2:].astype(np.float64)).mean() > 100
+    c = L.LPCNetBatch(B, 0, blob)
+    got = _frames(c, allf, 0, F)
+    assert np.array_equal(got, np.stack(outs))
+
+
+@pytest.mark.parametrize("B,name", [(1, "streams_int8"), (1, "streams_fp32"), (64, "streams_int8"),
+                                    (300, "streams_int8")])
+def test_unsynced_frames_then_single_frame(require_gpu, blobs, B, name):
+    """lpcnet_batch_synthesize_frames returns with frames still queued (an odd
+    count leaves the last one reading pinned LPC slot 0); a single-frame call
+    made right after, with no lpcnet_batch_sync, must not disturb them."""
+    F = 7
+    blob = blobs[name]
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    a = L.LPCNetBatch(B, 0, blob)
+    ref = np.stack([a.synthesize(allf[f]) for f in range(F)], 0)
+    b = L.LPCNetBatch(B, 0, blob)
+    part = np.ascontiguousarray(allf[:5])
+    df = b.device_alloc(part.nbytes)
+    dp = b.device_alloc(5 * B * 160 * 2)
+    b.h2d(df, part)
+    b.synthesize_frames(part, df, dp, 5)
+    out5 = b.synthesize(allf[5])            # no sync in between
+    out6 = b.synthesize(allf[6])
+    got = np.zeros((5, B, 160), np.int16)
+    b.d2h(got, dp)
+    b.device_free(df)
+    b.device_free(dp)
+    assert np.array_equal(got, ref[:5])
+    assert np.array_equal(out5, ref[5]) and np.array_equal(out6, ref[6])
+
+
+def test_device_abort_is_reported_not_silent(require_gpu, blobs):
+    """fp_kernel's LDS flag waits are bounded; with the bound forced to one
+    poll every launch aborts, and the call must fail (-1, last_error) instead
+    of returning PCM.  The default bound then synthesises correctly again."""
+    blob = blobs["streams_fp32"]
+    B, F = 2, 4
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    b = L.LPCNetBatch(B, 0, blob)
+    assert b.info().quad_path == 5
+    for f in range(3):
+        b.synthesize(allf[f])  # frames 0-2: frame 2 is the first non-silent one
+    b.set_spin_limit(1)
+    with pytest.raises(L.LPCNetError, match="spin limit"):
+        b.synthesize(allf[3])
+    # the queued path reports at the sync
+    df = b.device_alloc(allf.nbytes)
+    dp = b.device_alloc(F * B * 160 * 2)
+    b.h2d(df, allf)
+    b.synthesize_frames(allf, df, dp, F)
+    with pytest.raises(L.LPCNetError, match="spin limit"):
+        b.sync()
+    b.device_free(df)
+    b.device_free(dp)
+    b.set_spin_limit(0)
+    b.reset()
+    refs = [O.Oracle(blob, 1) for _ in range(B)]
+    for f in range(F):
+        out = b.synthesize(allf[f])
+        for s in range(B):
+            assert np.array_equal(out[s], refs[s].synthesize(allf[f, s])), (f, s)
+
+
+def test_drop_in_api_error_behaviour(require_gpu, blobs):
+    """lpcnet_synthesize without a model: silence plus last_error (the
+    reference would use its compiled-in model; this library has none);
+    lpcnet_init on a live handle resets it (lpcnet.c:184-200 ends in
+    lpcnet_reset) and keeps the model."""
+    import ctypes as C
+    G = np.load(os.path.join(GOLD, "streams_int8.npz"))
+    net = L.LPCNet()
+    out = net.synthesize(G["features"][0, 3])
+    assert np.all(out == 0) and "no model" in L.last_error()
+    net.load_model(blobs["streams_int8"])
+    for fr in range(4):
+        assert np.array_equal(net.synthesize(G["features"][0, fr]), G["pcm"][0, fr])
+    assert L.lib.lpcnet_init(C.c_void_p(net._st)) == 0
+    for fr in range(4):
+        assert np.array_equal(net.synthesize(G["features"][0, fr]), G["pcm"][0, fr]), fr

@@ -1,0 +1,209 @@
+"""Weight-blob ingest: every rejection rule of the reference's parser
+(src/parse_lpcnet_weights.c:36-113 parse_record / parse_weights /
+find_array_check / find_idx_check, record layout src/nnet.h:54-61) applied to
+a mutated synthetic blob must make the engine's loader and the CPU oracle
+both refuse it; blobs the reference accepts (records reordered, unknown or
+duplicate records) must still load.
+
+CPU tests go through lpcnet_mi355x_validate_model (the same parse and checks
+lpcnet_load_model runs, without a device); the -m gpu tests go through
+lpcnet_load_model / lpcnet_batch_load_model themselves.
+
+Two inputs the reference mishandles are rejected here on purpose
+(documented deviations): a negative block count in an idx
+array (find_idx_check loops forever or walks backwards) and a negative
+block position (accepted by find_idx_check, then read out of bounds)."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import lpcnet_amd as L
+import oracle_lib as O
+
+HEAD = 64  # WEIGHT_BLOCK_SIZE, nnet.h:42
+
+
+def records(blob: bytes):
+    """[(name, header bytes, payload bytes incl. padding)] of a blob."""
+    out, off = [], 0
+    while off < len(blob):
+        size, block = struct.unpack_from("<ii", blob, off + 12)
+        name = blob[off + 20:off + 64].split(b"\0")[0].decode()
+        out.append([name, bytearray(blob[off:off + HEAD]), bytearray(blob[off + HEAD:off + HEAD + block])])
+        off += HEAD + block
+    return out
+
+
+def join(recs) -> bytes:
+    return b"".join(bytes(h) + bytes(p) for _, h, p in recs)
+
+
+def set_size(rec, size=None, block=None):
+    s, b = struct.unpack_from("<ii", rec[1], 12)
+    struct.pack_into("<ii", rec[1], 12, s if size is None else size, b if block is None else block)
+
+
+def make_record(name: str, payload: bytes, type_=0) -> list:
+    block = (len(payload) + 63) // 64 * 64
+    h = bytearray(HEAD)
+    h[0:4] = b"DNNw"
+    struct.pack_into("<iiii", h, 4, 0, type_, len(payload), block)
+    h[20:20 + len(name)] = name.encode()
+    return [name, h, bytearray(payload) + bytearray(block - len(payload))]
+
+
+def find(recs, name):
+    return next(r for r in recs if r[0] == name)
+
+
+def idx_words(rec):
+    size = struct.unpack_from("<i", rec[1], 12)[0]
+    return np.frombuffer(bytes(rec[2][:size]), np.int32).copy()
+
+
+def put_idx(rec, words):
+    data = np.asarray(words, np.int32).tobytes()
+    block = (len(data) + 63) // 64 * 64
+    rec[2] = bytearray(data) + bytearray(block - len(data))
+    set_size(rec, len(data), block)
+
+
+def _mut_idx(name, fn):
+    def m(recs):
+        r = find(recs, name)
+        put_idx(r, fn(idx_words(r)))
+    return m
+
+
+def _first_pos(w):
+    """index of the first block position of the first non-empty row block"""
+    p = 0
+    while w[p] == 0:
+        p += 1
+    return p + 1
+
+
+def _set(w, i, v):
+    w = w.copy()
+    w[i] = v
+    return w
+
+
+MUTATIONS = {
+    # parse_record (parse_lpcnet_weights.c:36-51)
+    "truncated_last_record": lambda r: r[-1].__setitem__(2, r[-1][2][:-8]),
+    "trailing_bytes_shorter_than_a_header": lambda r: r.append(["", bytearray(10), bytearray()]),
+    "block_size_below_size": lambda r: set_size(find(r, "dual_fc_bias"), size=4096),
+    "name_not_nul_terminated": lambda r: find(r, "dual_fc_bias")[1].__setitem__(63, ord("x")),
+    "negative_size": lambda r: set_size(find(r, "feature_conv1_bias"), size=-4),
+    # parse_weights treats a zero-size record as an error (ret > 0 required, :63)
+    "zero_size_record": lambda r: r.append(make_record("empty", b"")),
+    # find_array_check (:83-87)
+    "missing_array": lambda r: r.remove(find(r, "dual_fc_factor")),
+    "mis_sized_array": lambda r: set_size(find(r, "gru_b_dense_feature_bias"), size=47 * 4),
+    "gru_a_weights_not_32_per_block": lambda r: set_size(find(r, "sparse_gru_a_recurrent_weights"),
+                                                         size=struct.unpack_from("<i", find(r, "sparse_gru_a_recurrent_weights")[1], 12)[0] - 32),
+    # find_idx_check (:89-113)
+    "idx_pos_misaligned": _mut_idx("sparse_gru_a_recurrent_weights_idx", lambda w: _set(w, _first_pos(w), w[_first_pos(w)] + 1)),
+    "idx_pos_past_input": _mut_idx("gru_b_weights_idx", lambda w: _set(w, _first_pos(w), 384)),
+    "idx_block_count_past_end": _mut_idx("sparse_gru_a_recurrent_weights_idx", lambda w: _set(w, 0, len(w))),
+    "idx_extra_row_block": _mut_idx("gru_b_weights_idx", lambda w: np.concatenate([w, [0]])),
+    "idx_missing_row_block": _mut_idx("gru_b_weights_idx", lambda w: w[w[0] + 1:]),
+    # deviations: the reference hangs / reads out of bounds on these
+    "idx_negative_block_count": _mut_idx("gru_b_weights_idx", lambda w: _set(w, 0, -1)),
+    "idx_negative_position": _mut_idx("sparse_gru_a_recurrent_weights_idx", lambda w: _set(w, _first_pos(w), -4)),
+}
+
+ACCEPTED = {
+    "reversed_record_order": lambda r: r.reverse(),
+    "unknown_record_appended": lambda r: r.append(make_record("not_a_layer_weights", b"\1" * 100)),
+    # find_array_entry returns the first record of a name (:77-80)
+    "duplicate_record_after_original": lambda r: r.append(
+        make_record("dual_fc_bias", b"\0" * (512 * 4))),
+}
+
+
+@pytest.fixture(scope="module")
+def blob():
+    return L.synthetic_model(1, L.VARIANT_INT8)
+
+
+def mutated(blob, fn):
+    recs = records(blob)
+    fn(recs)
+    return join(recs)
+
+
+def test_records_roundtrip(blob):
+    assert join(records(blob)) == blob
+    assert L.validate_model(blob) is None
+    O.Oracle(blob)
+
+
+@pytest.mark.parametrize("name", sorted(MUTATIONS))
+def test_rejected_by_engine_and_oracle(blob, name):
+    bad = mutated(blob, MUTATIONS[name])
+    assert bad != blob
+    with pytest.raises(L.LPCNetError):
+        L.validate_model(bad)
+    assert L.last_error()
+    with pytest.raises(ValueError):
+        O.Oracle(bad)
+
+
+@pytest.mark.parametrize("name", sorted(ACCEPTED))
+def test_accepted_by_engine_and_oracle(blob, name):
+    good = mutated(blob, ACCEPTED[name])
+    L.validate_model(good)
+    O.Oracle(good)
+
+
+def test_fp32_blob_validates():
+    L.validate_model(L.synthetic_model(1, L.VARIANT_FP32))
+    L.validate_model(L.synthetic_model(1, L.VARIANT_INT8, True))
+
+
+def test_empty_and_tiny_blobs_rejected(blob):
+    for b in (b"", blob[:63], blob[:64]):
+        with pytest.raises(L.LPCNetError):
+            L.validate_model(b)
+
+
+def test_reordered_blob_same_oracle_pcm(blob):
+    good = mutated(blob, ACCEPTED["reversed_record_order"])
+    f = L.synthetic_features(5, 4)[:, :20]
+    assert np.array_equal(O.synth_stream(blob, f, 0), O.synth_stream(good, f, 0))
+
+
+# ---- through the device entry points -------------------------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["truncated_last_record", "name_not_nul_terminated", "missing_array",
+                                  "idx_pos_misaligned", "idx_extra_row_block", "idx_negative_block_count"])
+def test_load_model_rejects_and_keeps_previous_model(require_gpu, blob, name):
+    """A rejected reload leaves the bound model untouched: synthesis still
+    matches the golden fixture (the ADVICE r01 failure mode was a half-rewritten
+    kernel argument block after a failed reload)."""
+    G = np.load(os.path.join(O.GOLDEN, "streams_int8.npz"))
+    b = L.LPCNetBatch(len(G["streams"]), 0, blob)
+    for fr in range(3):
+        assert np.array_equal(b.synthesize(G["features"][:, fr, :20]), G["pcm"][:, fr])
+    with pytest.raises(L.LPCNetError):
+        b.load_model(mutated(blob, MUTATIONS[name]))
+    for fr in range(3, 6):
+        assert np.array_equal(b.synthesize(G["features"][:, fr, :20]), G["pcm"][:, fr]), fr
+    net = L.LPCNet()
+    with pytest.raises(L.LPCNetError):
+        net.load_model(mutated(blob, MUTATIONS[name]))
+
+
+@pytest.mark.gpu
+def test_reordered_blob_loads_on_device_same_pcm(require_gpu, blob):
+    G = np.load(os.path.join(O.GOLDEN, "streams_int8.npz"))
+    good = mutated(blob, ACCEPTED["reversed_record_order"])
+    good = mutated(good, ACCEPTED["duplicate_record_after_original"])
+    b = L.LPCNetBatch(len(G["streams"]), 0, good)
+    for fr in range(6):
+        assert np.array_equal(b.synthesize(G["features"][:, fr, :20]), G["pcm"][:, fr]), fr
