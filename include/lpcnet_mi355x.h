@@ -82,11 +82,10 @@ LPCNET_EXPORT int lpcnet_batch_restore_state(LPCNetBatch *b, int stream, const v
 
 /* nframes consecutive frames for every stream with device-resident I/O:
  * d_features [nframes][B][NB_FEATURES] and d_pcm [nframes][B][N] are device
- * pointers on the batch's device.  h_features holds the same features on the
- * host: lpc_from_cepstrum (freq.c:310-320) runs on host threads, pipelined
- * two frames ahead of its use (FEATURES_DELAY), and uploads 64 B/stream/frame.
- * Work is enqueued on the batch's HIP stream; the call returns once every
- * frame has been enqueued (use lpcnet_batch_sync to wait). */
+ * pointers on the batch's device.  h_features is ignored (it may be NULL;
+ * lpc_from_cepstrum runs on the device since round 2 -- kept for ABI
+ * compatibility).  Work is enqueued on the batch's HIP stream; the call
+ * returns once every frame has been enqueued (use lpcnet_batch_sync to wait). */
 LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_features, const float *d_features,
                                                  short *d_pcm, int nframes, int N);
 /* Wait for every enqueued frame.  Returns 0, or -1 (lpcnet_mi355x_last_error)
@@ -145,8 +144,10 @@ LPCNET_EXPORT int lpcnet_batch_get_state(LPCNetBatch *b, int stream, float *gru_
 LPCNET_EXPORT int lpcnet_mi355x_synthetic_model(unsigned seed, int variant, int flags, unsigned char *buf, int cap);
 /* Synthetic feature frames (NB_TOTAL_FEATURES floats each) for stream `stream`. */
 LPCNET_EXPORT void lpcnet_mi355x_synthetic_features(unsigned stream, int nframes, float *out);
-/* Host restatement of freq.c:310-320 lpc_from_cepstrum used by the engine. */
-LPCNET_EXPORT float lpcnet_mi355x_lpc_from_cepstrum(float *lpc, const float *cepstrum);
+/* lpc_from_cepstrum (freq.c:310-320) of n cepstra [n][18] -> lpc [n][16] on
+ * GPU `device`, through the engine's lpc_kernel (diagnostics / parity: the
+ * synthesis entry points run the same kernel per frame).  Returns 0 or -1. */
+LPCNET_EXPORT int lpcnet_mi355x_device_lpc(int device, const float *cepstra, float *lpc, int n);
 /* The rcpps table the device activations use (2048 entries). */
 LPCNET_EXPORT const uint32_t *lpcnet_mi355x_rcp_table(void);
 /* Device numerics self-test (diagnostics, not the synthesis path): runs one
@@ -155,7 +156,9 @@ LPCNET_EXPORT const uint32_t *lpcnet_mi355x_rcp_table(void);
  * sigmoid8_approx (vec_avx.h:393-440, emulated rcpps), 2 / 3 the batched
  * forms of 0 / 1, 4 vector_ps_to_epi8 byte (vec_avx.h:321-336), 5 lin2ulaw
  * (common.h:47-58), 6 floor(.5 + x) (lpcnet.c:266), 7 _mm256_cvtps_epi32;
- * op 8: n kiss99 draws (kiss99.c:59-81) from the 4-word state in[0..3].
+ * op 8: n kiss99 draws (kiss99.c:59-81) from the 4-word state in[0..3];
+ * op 9: the band power of lpc_from_cepstrum, (float)(pow(10, x) *
+ * compensation[i % 18]) (freq.c:318, pow10_dd.h).
  * Returns 0, or -1 on bad arguments / HIP failure. */
 LPCNET_EXPORT int lpcnet_mi355x_device_numerics(int device, int op, const void *in, void *out, int n);
 /* Validate a weight blob with every rule lpcnet_load_model applies

@@ -83,7 +83,7 @@ def _load():
         "lpcnet_batch_get_state": (i, [vp, i, vp, vp, vp, vp, vp, vp]),
         "lpcnet_mi355x_synthetic_model": (i, [u, i, i, vp, i]),
         "lpcnet_mi355x_synthetic_features": (None, [u, i, vp]),
-        "lpcnet_mi355x_lpc_from_cepstrum": (f, [vp, vp]),
+        "lpcnet_mi355x_device_lpc": (i, [i, vp, vp, i]),
         "lpcnet_mi355x_rcp_table": (C.POINTER(C.c_uint32), []),
         "lpcnet_mi355x_device_count": (i, []),
         "lpcnet_mi355x_device_numerics": (i, [i, i, vp, vp, i]),
@@ -160,11 +160,12 @@ def synthetic_features(stream: int, nframes: int) -> np.ndarray:
     return out
 
 
-def lpc_from_cepstrum(cepstrum: np.ndarray) -> np.ndarray:
-    """Host restatement of freq.c:310-320 used by the engine."""
-    c = np.ascontiguousarray(cepstrum, np.float32)
-    out = np.zeros(16, np.float32)
-    lib.lpcnet_mi355x_lpc_from_cepstrum(out.ctypes.data, c.ctypes.data)
+def device_lpc(cepstra: np.ndarray, device: int = 0) -> np.ndarray:
+    """lpc_from_cepstrum (freq.c:310-320) of cepstra [n, 18] on the GPU (lpc_kernel) -> [n, 16]."""
+    c = np.ascontiguousarray(np.asarray(cepstra, np.float32).reshape(-1, 18))
+    out = np.zeros((c.shape[0], 16), np.float32)
+    if lib.lpcnet_mi355x_device_lpc(device, c.ctypes.data, out.ctypes.data, c.shape[0]) != 0:
+        raise LPCNetError("device LPC failed: " + last_error())
     return out
 
 
@@ -301,9 +302,9 @@ class LPCNetBatch:
 
     def synthesize_frames(self, h_features: np.ndarray, d_features: int, d_pcm: int, nframes: int,
                           n: int = FRAME_SIZE) -> None:
-        """Enqueue ``nframes`` frames; h_features [nframes, B, 20] (host copy for LPC)."""
-        assert h_features.dtype == np.float32 and h_features.flags.c_contiguous
-        if lib.lpcnet_batch_synthesize_frames(self._b, h_features.ctypes.data, d_features, d_pcm, nframes, n) != 0:
+        """Enqueue ``nframes`` frames from device features [nframes, B, 20] into device pcm
+        [nframes, B, n].  ``h_features`` is unused (LPC runs on the device); kept for callers."""
+        if lib.lpcnet_batch_synthesize_frames(self._b, None, d_features, d_pcm, nframes, n) != 0:
             raise LPCNetError(last_error())
 
     def sync(self) -> None:

@@ -8,8 +8,9 @@
  *    block-sparse GRU weights into the sample kernel's LDS image;
  *  - per-stream device state (lpcnet_private.h:28-48) and reset semantics
  *    (lpcnet.c:174-182);
- *  - per-frame scheduling: lpc_from_cepstrum on a host thread pool, pipelined
- *    one frame ahead, then frame_kernel + sample_kernel on one HIP stream.
+ *  - per-frame scheduling: lpc_kernel (lpc_from_cepstrum), frame_kernel and
+ *    the sample kernel on the batch's HIP stream (the first two on a second
+ *    stream, one frame ahead, for small batches).
  * Compile with -ffp-contract=off (the u-law / logit tables are computed here
  * with the reference's exact expressions).
  */
@@ -21,12 +22,9 @@
 
 #include <algorithm>
 #include <atomic>
-#include <condition_variable>
 #include <functional>
 #include <mutex>
 #include <string>
-#include <sched.h>
-#include <thread>
 #include <vector>
 
 #include "lpcnet_engine.h"
@@ -191,91 +189,56 @@ int total_blocks(const std::vector<std::vector<int>> &b)
   return t;
 }
 
-/* ---- small persistent thread pool for lpc_from_cepstrum ---------------- */
-class Pool {
- public:
-  explicit Pool(int n)
-  {
-    for (int i = 0; i < n; i++) th_.emplace_back([this] { worker(); });
-  }
-  ~Pool()
-  {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto &t : th_) t.join();
-  }
-  /* run f(chunk) for chunk in [0, n) on the workers and the calling thread */
-  void parallel_for(int n, const std::function<void(int)> &f)
-  {
-    if (n <= 0) return;
-    if (th_.empty() || n == 1) {
-      for (int i = 0; i < n; i++) f(i);
-      return;
-    }
-    {
-      std::lock_guard<std::mutex> g(m_);
-      job_ = &f;
-      n_ = n;
-      next_.store(0);
-      left_.store(n);
-      gen_++;
-    }
-    cv_.notify_all();
-    drain();
-    std::unique_lock<std::mutex> g(m_);
-    done_.wait(g, [this] { return left_.load() == 0; });
-    job_ = nullptr;
-  }
-
- private:
-  void drain()
-  {
-    for (;;) {
-      int i = next_.fetch_add(1);
-      if (i >= n_) break;
-      (*job_)(i);
-      if (left_.fetch_sub(1) == 1) {
-        std::lock_guard<std::mutex> g(m_);
-        done_.notify_all();
-      }
-    }
-  }
-  void worker()
-  {
-    uint64_t seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return stop_ || (gen_ != seen && job_ != nullptr); });
-        if (stop_) return;
-        seen = gen_;
-      }
-      drain();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex m_;
-  std::condition_variable cv_, done_;
-  const std::function<void(int)> *job_ = nullptr;
-  int n_ = 0;
-  std::atomic<int> next_{0}, left_{0};
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-};
-
-int pool_threads()
+/* ---- lpc_from_cepstrum tables (lpc_kernel.hip) ------------------------- */
+/* The reference's constants, built as the reference builds them: the idct
+ * matrix (freq.c:56-59 dct_table), the 320-point kiss FFT twiddles
+ * (lpcnet_tables.c kfft, generated by dump_lpcnet_tables.c:88-95 as
+ * (float)cos/sin of -2*pi*i/320 in double), kiss_fft's input permutation for
+ * factors (4,4,4,5) applied outermost-5-first, and per spectrum bin the band
+ * and (float)j/band_size interpolation fraction (freq.c:202-216). */
+void build_lpc_tables(LpcTables &T)
 {
-  const char *e = getenv("LPCNET_LPC_THREADS");
-  if (e) return std::max(0, atoi(e));
-  /* the CPUs this process may run on (a launcher may pin each rank to its
-   * share of the node), not the whole machine */
-  int hc = (int)std::thread::hardware_concurrency();
-  cpu_set_t set;
-  if (sched_getaffinity(0, sizeof(set), &set) == 0) hc = std::max(1, CPU_COUNT(&set));
-  return std::max(0, std::min(hc, 16) - 1);
+  static const short eband[LPC_NBANDS] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 28, 34, 40};
+  static const float comp[LPC_NBANDS] = {0.8f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 0.666667f, 0.5f, 0.5f, 0.5f,
+                                         0.333333f, 0.25f, 0.25f, 0.2f, 0.166667f, 0.173913f};
+  memset(&T, 0, sizeof(T));
+  const double pi = 3.14159265358979323846264338327;
+  for (int i = 0; i < LPC_WIN; i++) {
+    const double ph = (-2 * pi / LPC_WIN) * i;
+    T.twr[i] = (float)cos(ph);
+    T.twi[i] = (float)sin(ph);
+  }
+  /* per spectrum bin k < 160: band and (float)j/band_size (freq.c:206-213) */
+  unsigned char band[160];
+  float frac[160];
+  for (int b = 0; b < LPC_NBANDS - 1; b++) {
+    const int n = (eband[b + 1] - eband[b]) * 4;
+    for (int j = 0; j < n; j++) {
+      band[eband[b] * 4 + j] = (unsigned char)b;
+      frac[eband[b] * 4 + j] = (float)j / n;
+    }
+  }
+  /* input sample d0 + 5*d1 + 20*d2 + 80*d3 feeds FFT slot d0*64 + d1*16 + d2*4 + d3 */
+  for (int d0 = 0; d0 < 5; d0++)
+    for (int d1 = 0; d1 < 4; d1++)
+      for (int d2 = 0; d2 < 4; d2++)
+        for (int d3 = 0; d3 < 4; d3++) {
+          const int i = d0 * 64 + d1 * 16 + d2 * 4 + d3, bin = d0 + 5 * d1 + 20 * d2 + 80 * d3;
+          const int k = bin <= 160 ? bin : LPC_WIN - bin;
+          LpcSlot &sl = T.slot[i];
+          sl.band = k < 160 ? band[k] : (unsigned char)(LPC_NBANDS - 1);
+          sl.frac = k < 160 ? frac[k] : 0.f;
+          sl.conj = bin > 160 ? 1 : 0;
+        }
+  for (int i = 0; i < LPC_NBANDS; i++)
+    for (int j = 0; j < LPC_NBANDS; j++) {
+      float v = (float)cos((i + .5) * j * M_PI / LPC_NBANDS);
+      if (j == 0) v = (float)(v * sqrt(.5));
+      T.dct[i * LPC_NBANDS + j] = v;
+    }
+  for (int i = 0; i < LPC_NBANDS; i++) T.comp[i] = comp[i];
+  T.sqrt_2_18 = sqrt(2. / LPC_NBANDS);
+  T.scale = 1.f / 320.f;
 }
 
 }  // namespace
@@ -308,11 +271,8 @@ struct LPCNetBatch {
   StreamState *d_state = nullptr;
   float *d_feat = nullptr;
   short *d_pcm = nullptr;
-  float *d_lpc[2] = {nullptr, nullptr};
-  float *h_lpc[2] = {nullptr, nullptr};
-  float *h_lpc_dev[2] = {nullptr, nullptr}; /* device view of the pinned h_lpc */
-  hipEvent_t ev_lpc[2] = {nullptr, nullptr};
-  bool ev_lpc_used[2] = {false, false};
+  float *d_lpc = nullptr;          /* [LPC_CHUNK][B][NLPC] lpc_from_cepstrum of queued frames */
+  LpcTables *d_lpc_tab = nullptr;
   /* overlapped multi-frame path (few streams, free CUs): frame kernel f+1 on
    * fstream beside sample kernel f on stream, outputs double-buffered in
    * d_cond[f & 1] */
@@ -338,8 +298,6 @@ struct LPCNetBatch {
   std::vector<hipEvent_t> ev_taken; /* events handed out since the last reset */
   std::vector<hipEvent_t> ev_pairs[2];
   std::vector<hipEvent_t> ev_free;
-  Pool *pool = nullptr;
-
   int set_device() { return hipSetDevice(device) == hipSuccess ? 0 : -1; }
 };
 
@@ -934,8 +892,12 @@ int ensure_trace(LPCNetBatch *b, int N)
  * kernel f+1 runs beside sample kernel f.  The sample kernels read nothing
  * else the frame kernel writes.  Every fstream launch precedes a stream
  * launch that waits for it, so a sync of stream covers both. */
-int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lpc, short *d_pcm, int N, int preload = 0,
-                      int ovl = -1)
+/* d_lpc_frame: this frame's lpc_from_cepstrum output ([B][NLPC]); with
+ * run_lpc the LPC kernel computing it is launched first, otherwise it was
+ * computed earlier on the same queue (lpcnet_batch_synthesize_frames
+ * batches it over many frames). */
+int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_frame, bool run_lpc, short *d_pcm, int N,
+                      int preload = 0, int ovl = -1)
 {
   const int c = ovl & 1;
   hipStream_t fs = ovl >= 0 ? b->fstream : b->stream;
@@ -943,7 +905,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   fa.st = b->d_state;
   fa.nstreams = b->B;
   fa.features = d_features;
-  fa.lpc_new = d_lpc;
+  fa.lpc_new = d_lpc_frame;
   SampleArgs sa = b->sa;
   sa.st = b->d_state;
   sa.nstreams = b->B;
@@ -968,6 +930,12 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   if (ovl >= 0 && b->ev_samp_used[c]) HIPCHK(hipStreamWaitEvent(fs, b->ev_samp_cur[c], 0));
   hipEvent_t ef = nullptr; /* end of the frame kernel, overlapped form with frame timing */
   if (e[0]) HIPCHK(hipEventRecord(e[0], fs));
+  /* lpc_from_cepstrum of this frame's features: the frame kernel pushes it
+   * into the two-frame LPC ring (lpcnet.c:110-112) */
+  if (run_lpc && launch_lpc(d_features, d_lpc_frame, b->B, b->d_lpc_tab, fs)) {
+    set_err("lpc kernel launch failed");
+    return -1;
+  }
   if (launch_frame(fa, fs)) { set_err("frame kernel launch failed"); return -1; }
   if (ovl >= 0 && launch_cond_copy(b->d_state, b->d_cond[c], b->B, fs)) {
     set_err("copy launch failed");
@@ -1020,16 +988,6 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, const float *d_lp
   return 0;
 }
 
-void compute_lpc(LPCNetBatch *b, const float *feat, int feat_stride, float *out)
-{
-  const int chunk = 32;
-  int nchunks = (b->B + chunk - 1) / chunk;
-  b->pool->parallel_for(nchunks, [&](int c) {
-    int e = std::min(b->B, (c + 1) * chunk);
-    for (int s = c * chunk; s < e; s++) lpc_from_cepstrum_host(out + (size_t)s * NLPC, feat + (size_t)s * feat_stride);
-  });
-}
-
 /* After a sync of b->stream: report (and clear) a device-side abort. */
 int check_status(LPCNetBatch *b)
 {
@@ -1061,9 +1019,30 @@ LPCNET_EXPORT int lpcnet_mi355x_device_count(void)
 
 LPCNET_EXPORT const uint32_t *lpcnet_mi355x_rcp_table(void) { return kRcpTable; }
 
-LPCNET_EXPORT float lpcnet_mi355x_lpc_from_cepstrum(float *lpc, const float *cepstrum)
+LPCNET_EXPORT int lpcnet_mi355x_device_lpc(int device, const float *cepstra, float *lpc, int n)
 {
-  return lpc_from_cepstrum_host(lpc, cepstrum);
+  if (n < 0 || (n > 0 && (!cepstra || !lpc))) { set_err("bad arguments"); return -1; }
+  if (n == 0) return 0;
+  if (hipSetDevice(device) != hipSuccess) { set_err("hipSetDevice failed"); return -1; }
+  LpcTables T;
+  build_lpc_tables(T);
+  float *dc = nullptr, *dl = nullptr;
+  LpcTables *dt = nullptr;
+  int rc = -1;
+  if (hipMalloc(&dc, sizeof(float) * NF * (size_t)n) == hipSuccess && hipMalloc(&dl, sizeof(float) * NLPC * (size_t)n) == hipSuccess &&
+      hipMalloc(&dt, sizeof(T)) == hipSuccess && hipMemcpy(dt, &T, sizeof(T), hipMemcpyHostToDevice) == hipSuccess) {
+    /* cepstra arrive as [n][NLPC+2] (18 bands); the kernel reads [n][NF] */
+    std::vector<float> f((size_t)NF * n, 0.f);
+    for (int i = 0; i < n; i++) memcpy(&f[(size_t)i * NF], cepstra + (size_t)i * LPC_NBANDS, sizeof(float) * LPC_NBANDS);
+    if (hipMemcpy(dc, f.data(), f.size() * 4, hipMemcpyHostToDevice) == hipSuccess && launch_lpc(dc, dl, n, dt, nullptr) == 0 &&
+        hipMemcpy(lpc, dl, sizeof(float) * NLPC * (size_t)n, hipMemcpyDeviceToHost) == hipSuccess)
+      rc = 0;
+  }
+  if (rc) set_err("device LPC failed");
+  (void)hipFree(dc);
+  (void)hipFree(dl);
+  (void)hipFree(dt);
+  return rc;
 }
 
 LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
@@ -1082,11 +1061,12 @@ LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
   ok = ok && hipHostMalloc(&b->h_status, 64, hipHostMallocMapped) == hipSuccess;
   ok = ok && hipHostGetDevicePointer((void **)&b->d_status, b->h_status, 0) == hipSuccess;
   if (ok) *b->h_status = 0;
-  for (int i = 0; i < 2 && ok; i++) {
-    ok = ok && hipMalloc(&b->d_lpc[i], sizeof(float) * NLPC * (size_t)nb_streams) == hipSuccess;
-    ok = ok && hipHostMalloc(&b->h_lpc[i], sizeof(float) * NLPC * (size_t)nb_streams, hipHostMallocMapped) == hipSuccess;
-    ok = ok && hipHostGetDevicePointer((void **)&b->h_lpc_dev[i], b->h_lpc[i], 0) == hipSuccess;
-    ok = ok && hipEventCreateWithFlags(&b->ev_lpc[i], hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipMalloc(&b->d_lpc, sizeof(float) * NLPC * (size_t)nb_streams * LPC_CHUNK) == hipSuccess;
+  ok = ok && hipMalloc(&b->d_lpc_tab, sizeof(LpcTables)) == hipSuccess;
+  if (ok) {
+    LpcTables T;
+    build_lpc_tables(T);
+    ok = hipMemcpy(b->d_lpc_tab, &T, sizeof(T), hipMemcpyHostToDevice) == hipSuccess;
   }
   if (ok && nb_streams <= OVERLAP_MAX_STREAMS) {
     ok = ok && hipStreamCreateWithFlags(&b->fstream, hipStreamNonBlocking) == hipSuccess;
@@ -1102,7 +1082,6 @@ LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
     lpcnet_batch_destroy(b);
     return nullptr;
   }
-  b->pool = new Pool(std::min(pool_threads(), std::max(0, nb_streams / 32)));
   if (const char *km = getenv("LPCNET_KERNEL")) b->kernel_mode = atoi(km);
   lpcnet_batch_reset(b);
   return b;
@@ -1121,11 +1100,8 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
   (void)hipFree(b->d_trace_logits);
   (void)hipFree(b->d_trace_exc);
   (void)hipFree(b->d_stamps);
-  for (int i = 0; i < 2; i++) {
-    (void)hipFree(b->d_lpc[i]);
-    if (b->h_lpc[i]) (void)hipHostFree(b->h_lpc[i]);
-    if (b->ev_lpc[i]) (void)hipEventDestroy(b->ev_lpc[i]);
-  }
+  (void)hipFree(b->d_lpc);
+  (void)hipFree(b->d_lpc_tab);
   for (int i = 0; i < 2; i++) {
     (void)hipFree(b->d_cond[i]);
     if (b->ev_frame[i]) (void)hipEventDestroy(b->ev_frame[i]);
@@ -1137,7 +1113,6 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
   for (hipEvent_t e : b->ev_taken) (void)hipEventDestroy(e);
   for (hipEvent_t e : b->ev_free) (void)hipEventDestroy(e);
   if (b->stream) (void)hipStreamDestroy(b->stream);
-  delete b->pool;
   delete b;
 }
 
@@ -1196,19 +1171,11 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_impl(LPCNetBatch *b, const float *feat
   if (N < 0 || N > FRAME || !features || (N > 0 && !pcm) || preload < 0) { set_err("bad arguments"); return -1; }
   if (b->set_device()) return -1;
   if (ensure_trace(b, N)) return -1;
-  /* frames queued by lpcnet_batch_synthesize_frames may still read the pinned
-   * LPC slots: wait for them before h_lpc[0] is rewritten */
-  for (int sl = 0; sl < 2; sl++)
-    if (b->ev_lpc_used[sl]) {
-      HIPCHK(hipEventSynchronize(b->ev_lpc[sl]));
-      b->ev_lpc_used[sl] = false;
-    }
-  compute_lpc(b, features, NF, b->h_lpc[0]);
-  HIPCHK(hipMemcpyAsync(b->d_lpc[0], b->h_lpc[0], sizeof(float) * NLPC * b->B, hipMemcpyHostToDevice, b->stream));
+  /* everything below is ordered after work already queued on b->stream */
   HIPCHK(hipMemcpyAsync(b->d_feat, features, sizeof(float) * NF * b->B, hipMemcpyHostToDevice, b->stream));
   if (preload > 0 && N > 0)
     HIPCHK(hipMemcpyAsync(b->d_pcm, pcm, sizeof(short) * N * b->B, hipMemcpyHostToDevice, b->stream));
-  if (launch_frame_step(b, b->d_feat, b->d_lpc[0], b->d_pcm, N, preload)) return -1;
+  if (launch_frame_step(b, b->d_feat, b->d_lpc, true, b->d_pcm, N, preload)) return -1;
   if (N > 0) HIPCHK(hipMemcpyAsync(pcm, b->d_pcm, sizeof(short) * N * b->B, hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
   return check_status(b);
@@ -1240,13 +1207,13 @@ LPCNET_EXPORT int lpcnet_batch_restore_state(LPCNetBatch *b, int stream, const v
 LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_features, const float *d_features,
                                                  short *d_pcm, int nframes, int N)
 {
+  (void)h_features; /* kept for ABI compatibility: lpc_from_cepstrum now runs on the device */
   if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
-  if (N < 0 || N > FRAME || nframes < 0 || !h_features || !d_features || !d_pcm) { set_err("bad arguments"); return -1; }
+  if (N < 0 || N > FRAME || nframes < 0 || !d_features || !d_pcm) { set_err("bad arguments"); return -1; }
   if (b->set_device()) return -1;
   if (ensure_trace(b, N)) return -1;
   const size_t fstride = (size_t)b->B * NF;
   if (nframes == 0) return 0;
-  int slot = 0;
   /* overlapped frame kernels: matrix-core and fp32 latency kernels (the only
    * ones reading the frame outputs through FrameCond), when CUs are free */
   const bool ovl = b->fstream && (b->mf || b->fp) && nframes >= 2 && !b->d_stamps && !getenv("LPCNET_NO_OVERLAP");
@@ -1255,26 +1222,21 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
     HIPCHK(hipEventRecord(b->ev_start, b->stream));
     HIPCHK(hipStreamWaitEvent(b->fstream, b->ev_start, 0));
   }
-  auto wait_slot = [&](int sl) -> int {
-    if (b->ev_lpc_used[sl]) HIPCHK(hipEventSynchronize(b->ev_lpc[sl]));
-    return 0;
-  };
-  if (wait_slot(0)) return -1;
-  compute_lpc(b, h_features, NF, b->h_lpc[0]);
-  for (int f = 0; f < nframes; f++) {
-    slot = f & 1;
-    /* zero copy: the frame kernel reads the pinned host LPC directly (64 B
-     * per stream); the slot is rewritten only after that kernel finished */
-    if (launch_frame_step(b, d_features + f * fstride, b->h_lpc_dev[slot], d_pcm + (size_t)f * b->B * N, N, 0,
-                          ovl ? f : -1))
+  hipStream_t fs = ovl ? b->fstream : b->stream;
+  for (int c0 = 0; c0 < nframes; c0 += LPC_CHUNK) {
+    /* lpc_from_cepstrum depends only on the features: one launch for up to
+     * LPC_CHUNK frames x B streams fills the GPU (a per-frame launch of B
+     * one-wave streams is latency-bound); queued on the frame kernels' queue,
+     * after the frame kernels of the previous chunk that read d_lpc */
+    const int n = std::min(LPC_CHUNK, nframes - c0);
+    if (launch_lpc(d_features + c0 * fstride, b->d_lpc, n * b->B, b->d_lpc_tab, fs)) {
+      set_err("lpc kernel launch failed");
       return -1;
-    HIPCHK(hipEventRecord(b->ev_lpc[slot], ovl ? b->fstream : b->stream));
-    b->ev_lpc_used[slot] = true;
-    if (f + 1 < nframes) {
-      /* host LPC of the next frame overlaps this frame's kernels */
-      if (wait_slot(slot ^ 1)) return -1;
-      compute_lpc(b, h_features + (f + 1) * fstride, NF, b->h_lpc[slot ^ 1]);
     }
+    for (int f = c0; f < c0 + n; f++)
+      if (launch_frame_step(b, d_features + f * fstride, b->d_lpc + (size_t)(f - c0) * b->B * NLPC, false,
+                            d_pcm + (size_t)f * b->B * N, N, 0, ovl ? f : -1))
+        return -1;
   }
   return 0;
 }

@@ -115,7 +115,7 @@ struct FrameArgs {
   StreamState *st;
   int nstreams;
   const float *features; /* [B][NF] for this frame */
-  const float *lpc_new;  /* [B][NLPC] lpc_from_cepstrum(features) (host) */
+  const float *lpc_new;  /* [B][NLPC] lpc_from_cepstrum(features) (lpc_kernel) */
   const float *conv1_w, *conv1_b, *conv2_w, *conv2_b;
   const float *dense1_w, *dense1_b, *dense2_w, *dense2_b;
   const float *gadf_w, *gadf_b, *gbdf_w, *gbdf_b;
@@ -228,8 +228,33 @@ int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream);
 int fp_lds_bytes();
 int launch_fp(const SampleArgs &a, void *stream);
 
-/* Host LPC (lpc_host.cpp). */
-float lpc_from_cepstrum_host(float *lpc, const float *ceps);
+/* lpc_from_cepstrum on the device (lpc_kernel.hip).  Constant tables built
+ * once per batch on the host (engine.cpp build_lpc_tables): the idct matrix
+ * (freq.c dct_table), the 320-point kiss FFT twiddles and input permutation
+ * (kiss_fft.c, lpcnet_tables.c), the band index and interpolation fraction of
+ * every spectrum bin (freq.c:202-216), the compensation factors (freq.c:50). */
+constexpr int LPC_NBANDS = 18;
+constexpr int LPC_WIN = 320;
+constexpr int LPC_ORDER1 = NLPC + 1;
+constexpr int LPC_CHUNK = 32;     /* frames per batched lpc_kernel launch (lpcnet_batch_synthesize_frames) */
+/* FFT input slot i (after kiss_fft's digit reversal): spectrum bin
+ * k = perm[i] (mirrored to 320 - k above 160), interpolated between band
+ * energies `band` and band + 1 with fraction `frac` (band = NB_BANDS - 1 for
+ * the zero bin 160), imaginary part -0.f for the mirrored (conjugate) bins. */
+struct LpcSlot {
+  float frac;
+  unsigned char band, conj, pad[2];
+};
+struct LpcTables {
+  double sqrt_2_18;               /* sqrt(2./NB_BANDS) (freq.c:238) */
+  float scale;                    /* 1/320, kiss_fft's inverse scaling */
+  float dct[LPC_NBANDS * LPC_NBANDS];
+  float comp[LPC_NBANDS];
+  float twr[LPC_WIN], twi[LPC_WIN];
+  LpcSlot slot[LPC_WIN];
+};
+/* features [nstreams][NF] -> lpc_out [nstreams][NLPC] */
+int launch_lpc(const float *features, float *lpc_out, int nstreams, const LpcTables *tables, void *stream);
 
 }  // namespace lpcnet_mi355x
 

@@ -13,6 +13,7 @@
 #include "lpcnet.h"
 #include "lpcnet_engine.h"
 #include "lpcnet_mi355x.h"
+#include "pow10_dd.h"
 
 namespace lpcnet_mi355x {
 
@@ -53,6 +54,13 @@ __global__ void numerics_kernel(int op, const uint32_t *__restrict__ in, uint32_
     case 5: out[e] = (uint32_t)lin2ulaw_x86(x); break;
     case 6: out[e] = (uint32_t)round_half_up(x); break;
     case 7: out[e] = (uint32_t)cvt_rne(x); break;
+    case 9: {
+      /* band power of lpc_from_cepstrum (freq.c:318) with compensation[e % 18] */
+      const float comp[18] = {0.8f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 0.666667f, 0.5f, 0.5f, 0.5f,
+                              0.333333f, 0.25f, 0.25f, 0.2f, 0.166667f, 0.173913f};
+      out[e] = __float_as_uint((float)(pow10_dd((double)x) * (double)comp[e % 18]));
+      break;
+    }
     default: out[e] = 0; break;
   }
 }
@@ -63,7 +71,7 @@ using namespace lpcnet_mi355x;
 
 extern "C" LPCNET_EXPORT int lpcnet_mi355x_device_numerics(int device, int op, const void *in, void *out, int n)
 {
-  if (op < 0 || op > 8 || n < 0 || (n > 0 && (!in || !out))) return -1;
+  if (op < 0 || op > 9 || n < 0 || (n > 0 && (!in || !out))) return -1;
   if (n == 0) return 0;
   if (hipSetDevice(device) != hipSuccess) return -1;
   const size_t nin = op == 8 ? 4 : (size_t)n;
