@@ -2,18 +2,31 @@
 """bench.py -- LPCNet synthesis throughput on MI355X (BASELINE.json metric).
 
 One "step" = one 10 ms frame (160 samples) for every stream of the batch:
-frame network + 160 recurrent samples, device-resident features and PCM,
-lpc_from_cepstrum on host threads pipelined ahead (its 64 B/stream H2D upload
-is inside the timed region).  Workload: BASELINE.json configs[3] -- int8 path,
+lpc_from_cepstrum + frame network + 160 recurrent samples, device-resident
+features and PCM (lpcnet_batch_synthesize_frames; everything inside the timed
+region runs on the GPU).  Workload: BASELINE.json configs[3] -- int8 path,
 1024 streams per GPU (configs[4] shards 1024 streams per GPU, weak scaling).
-The batch=1 line (configs[1]) is reported alongside.
+configs[1] (batch=1, fp32 and int8) and configs[2] (batch=256) are reported
+alongside in `batch1`, `batch1_fp32`, `batch256`.
 
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Rank 0 prints one JSON line.
+
+Roofline: algorithmic bytes per stream-sample = the shared
+weight bytes of one sample step (GRU_A/GRU_B weights + idx + biases, plus the
+frame network's 1.08 MB / 160) / B + 15,009 per-stream bytes (3 embedding rows,
+the dual_fc path, conditioning share, PCM), recomputed from the loaded index;
+per launch x 160 x B, over the sample kernel's HIP-event launch time.  `bound`
+stays "hbm" as the contract prescribes, and the line says what actually
+binds: `hbm_actual_GBs` / `l2_hit` from the PMC passes of this same source
+tree (tools/gpu_evidence.sh -> pmc_traffic.json, used only when its
+source_sha256 matches), and `latency` from an untimed s_memtime-stamped run
+(critical-path cycles per sample x 160 / clock vs the measured launch).
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -25,19 +38,20 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: int8 MFMA dense = 2x the ~2.5 PF bf16 rate
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2 aggregate, measured
 
 
-def measured_pmc(kernel_prefix):
-    """PMC record of the sample kernel from the committed rocprofv3 passes of
-    this same command (tools/gpu_profile.sh -> tools/pmc_summary.py ->
-    profiles/<round>/pmc_traffic.json: HBM bytes per launch from
-    FETCH_SIZE/WRITE_SIZE, MFMA busy fraction); PMC counters cannot be read
-    in-process.  ({}, None) when no profile matches the kernel."""
-    import glob
-    # a pass just made on this box (tools/gpu_evidence.sh) first, then the committed ones
+def measured_pmc(config, kernel_name):
+    """PMC record (tools/pmc_summary.py) of `kernel_name` in bench configuration
+    `config` from the passes of THIS source tree: gpurun_out/ first (a pass
+    just made on this box), then the committed profiles/r*/ (newest round
+    first).  ({}, None) when no record matches the source hash."""
+    from pmc_summary import source_sha256
+    want = source_sha256(ROOT)
     cands = [os.path.join(ROOT, "gpurun_out", "pmc_traffic.json")]
     cands += sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True)
     for f in cands:
@@ -45,8 +59,10 @@ def measured_pmc(kernel_prefix):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        for k, v in d.items():
-            if kernel_prefix in k:
+        if d.get("source_sha256") != want:
+            continue
+        for k, v in d.get("configs", {}).get(config, {}).items():
+            if kernel_name in k:
                 return v, os.path.relpath(f, ROOT)
     return {}, None
 
@@ -58,8 +74,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3, help="untimed frames")
     p.add_argument("--streams", type=int, default=1024, help="streams per GPU")
     p.add_argument("--variant", choices=["int8", "fp32"], default="int8")
-    p.add_argument("--no-batch1", action="store_true")
+    p.add_argument("--no-batch1", action="store_true", help="skip the batch1 / batch1_fp32 / batch256 lines")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-latency", action="store_true", help="skip the stamped latency run")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--timers", type=int, default=1,
                    help="HIP events in the timed region: 0 none, 1 around the sample kernel, 2 both kernels")
@@ -105,7 +122,7 @@ def max_over_ranks(dist, x):
 
 
 def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1):
-    """Returns (seconds for `steps` frames, kernel ms / launches, info).
+    """Returns (seconds for `steps` frames, kernel ms / launches, info, pcm).
     The timed region carries HIP events around each sample-kernel launch
     (timers=1; 2 adds the frame kernel); the frame kernel's own time comes
     from a short untimed pass with both kernels timed."""
@@ -119,20 +136,18 @@ def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1)
     d_pcm = b.device_alloc((F + extra) * B * 160 * 2)
     b.h2d(d_feat, feats)
     if warmup:
-        b.synthesize_frames(feats[:warmup], d_feat, d_pcm, warmup)
+        b.synthesize_frames(None, d_feat, d_pcm, warmup)
     barrier_sync(timed_dist, b)
     b.reset_timers(timers)
     t0 = time.perf_counter()
-    b.synthesize_frames(np.ascontiguousarray(feats[warmup:]), d_feat + warmup * B * 20 * 4, d_pcm + warmup * B * 160 * 2,
-                        steps)
+    b.synthesize_frames(None, d_feat + warmup * B * 20 * 4, d_pcm + warmup * B * 160 * 2, steps)
     barrier_sync(timed_dist, b)
     dt = time.perf_counter() - t0
     ks, kn = b.kernel_ms(0)
     pcm = np.zeros((F, B, 160), np.int16)
     b.d2h(pcm, d_pcm)
     b.reset_timers(2)
-    b.synthesize_frames(np.ascontiguousarray(feats[warmup:warmup + extra]), d_feat + warmup * B * 20 * 4,
-                        d_pcm + F * B * 160 * 2, extra)
+    b.synthesize_frames(None, d_feat + warmup * B * 20 * 4, d_pcm + F * B * 160 * 2, extra)
     b.sync()
     fs, fn = b.kernel_ms(1)
     info = b.info()
@@ -142,21 +157,111 @@ def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1)
     return dt, (ks, kn, fs, fn), info, pcm
 
 
+def algorithmic_bytes_per_launch(info, B):
+    """SURVEY 8d per stream-sample figure x 160 x B (one frame)"""
+    per = (info.bytes_shared_per_sample + info.bytes_shared_per_frame / 160.0) / B + info.bytes_per_stream_sample
+    return per * 160 * B, per
+
+
+def roofline(info, B, launch_ms, config):
+    bytes_launch, per = algorithmic_bytes_per_launch(info, B)
+    achieved = bytes_launch / (launch_ms * 1e-3) / 1e9
+    pmc, src = measured_pmc(config, info.kernel_name)
+    traffic = pmc.get("hbm_bytes_per_launch")
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+         "traffic": traffic, "kernel": info.kernel_name, "avg_launch_ms": launch_ms,
+         "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_stream_sample": per,
+         "pmc_source": src,
+         # what the counters say actually moves: HBM bytes / launch time, and the
+         # L2 hit rate of the gathers (the algorithmic bytes are served by L2)
+         "hbm_actual_GBs": traffic / (launch_ms * 1e-3) / 1e9 if traffic else None,
+         "l2_hit": pmc.get("l2_hit"),
+         "l2_frac": achieved / L2_PEAK_GBS}
+    mf = None
+    if info.mfma_ops_per_group_sample > 0:
+        groups = (B + info.streams_per_workgroup - 1) // info.streams_per_workgroup
+        ops = info.mfma_ops_per_group_sample * groups * 160
+        mf = {"achieved_tops": ops / (launch_ms * 1e-3) / 1e12, "peak_tops": I8_PEAK_TOPS,
+              "ops_per_launch": ops, "busy_frac_pmc": pmc.get("mfma_util")}
+    return r, mf
+
+
+def latency(L, blob, B, measured_ms):
+    """Critical path of the sample kernel from s_memtime phase stamps (one
+    untimed stamped frame): cycles per sample x 160 / clock, against the
+    measured (unstamped) launch.  The stamped launch itself runs ~5-10 %
+    slower (instrumentation)."""
+    F = 4
+    b = L.LPCNetBatch(B, int(os.environ.get("LOCAL_RANK", "0")) % max(1, L.device_count()), blob)
+    allf = np.stack([L.synthetic_features(s, F)[:, :20] for s in range(B)], 1)
+    for f in range(F - 1):
+        b.synthesize(allf[f])
+    b.set_stamps(True)
+    b.reset_timers(1)
+    b.synthesize(allf[F - 1])
+    kms, kn = b.kernel_ms(0)
+    st = b.get_stamps().astype(np.float64)  # [groups][8 waves][16]
+    info = b.info()
+    b.close()
+    n = max(st[:, :, 7].max(), 1)
+    per = st / n
+    loop = per[:, :, 6].max(axis=1).mean()
+    stamped_ms = kms / max(kn, 1)
+    clock = st[:, :, 6].max() / (stamped_ms * 1e-3) / 1e9
+    out = {"kernel": info.kernel_name, "cycles_per_sample": loop, "clock_ghz_stamped": clock,
+           "stamped_launch_ms": stamped_ms, "predicted_launch_ms": loop * 160 / (clock * 1e9) * 1e3,
+           "measured_launch_ms": measured_ms,
+           "cycles_per_sample_at_measured": loop * measured_ms / stamped_ms}
+    if info.quad_path == 4:
+        ga = per[:, :6, :].mean(axis=0)   # GRU_A waves [6][16]
+        sm = per[:, 6, :].mean(axis=0)    # sampler wave 6
+        out["critical_path_cycles"] = {
+            "gru_a_gathers": float(ga[:, 10].max()),
+            "gru_a_elementwise_slowest_wave": float(ga[:, 0].max()),
+            "gru_a_elementwise_fastest_wave": float(ga[:, 0].min()),
+            "sampler_gru_b": float(sm[8] + sm[10] + sm[14]),
+            "sampler_walk": float(sm[11]),
+            "sampler_post": float(sm[12]),
+            "sampler_wait_at_Y": float(sm[1]),
+        }
+    return out
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds):
-    """The reference's own AVX2 kernels (oracle/_ref) driven by the oracle's
-    lpcnet.c/nnet.c restatement, one stream per thread on the host cores."""
+    """The reference's own AVX2 kernels (oracle/_ref, compiled from the
+    reference sources) driven by the oracle's lpcnet.c/nnet.c restatement,
+    one stream per worker thread, one worker pinned per host core this
+    process may use.  On the GPU box that is the harness's CPU share for one
+    GPU (OMP_NUM_THREADS = 16 there; the affinity mask shows the whole
+    machine), so `per_core` is the number to scale to a node."""
     import lpcnet_amd as L
     import oracle_lib as O
     kind = "reference" if O.have_ref() else "port"
     kernels = O.ref_kernels() if O.have_ref() else None
     blob = L.synthetic_model(1, 0)
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    cpus = sorted(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(len(cpus), share) if share > 0 else len(cpus))
     # warm the lazily built tables on one thread first
     O.Oracle(blob, 0, kernels).synthesize(L.synthetic_features(0, 1)[0])
     frames_done = [0] * threads
     stop = [False]
 
     def work(t):
+        try:
+            os.sched_setaffinity(threading.get_native_id(), {cpus[t % len(cpus)]})
+        except OSError:
+            pass
         o = O.Oracle(blob, 0, kernels)
         f = L.synthetic_features(1000 + t, 64)
         k = 0
@@ -175,10 +280,27 @@ def cpu_baseline(seconds):
         t.join()
     dt = time.perf_counter() - t0
     frames = sum(frames_done)
-    return {"value": frames * 160 / dt, "unit": "samples/s", "cores": threads, "kind": kind,
-            "sample": f"{threads} threads x 1 stream each, int8 synthetic model, {frames} frames in {dt:.1f}s "
+    value = frames * 160 / dt
+    return {"value": value, "unit": "samples/s", "cores": threads, "kind": kind,
+            "per_core": value / threads, "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "affinity_cpus": len(cpus),
+            "sample": f"{threads} pinned threads x 1 stream each (one per core of this process's CPU share), int8 "
+                      f"synthetic model, {frames} frames in {dt:.1f}s "
                       f"({'reference vec_avx.h/kiss99/freq.c kernels compiled from /root/reference/src' if kind == 'reference' else 'portable oracle'}"
-                      f" + oracle restatement of lpcnet.c/nnet.c)"}
+                      f" + oracle restatement of lpcnet.c/nnet.c; restatement/reference speed ratio: BASELINE.md section 3)"}
+
+
+def side_line(L, blob, B, args, config, variant_name):
+    nf = max(args.steps, 20)
+    dt, (k, n, _, _), info, _ = run_batch(L, blob, B, 0, args.warmup, nf, None, args.timers)
+    launch = k / max(n, 1)
+    rf, mf = roofline(info, B, launch, config)
+    out = {"samples_per_s": B * nf * 160 / dt, "rt_streams": B * nf * 160 / dt / 16000.0, "x_realtime_per_stream":
+           nf * 160 / dt / 16000.0, "ms_per_frame": dt / nf * 1e3, "sample_kernel_avg_ms": launch,
+           "kernel": info.kernel_name, "path": variant_name, "roofline": rf}
+    if mf:
+        out["mfma"] = mf
+    return out
 
 
 def main():
@@ -189,17 +311,14 @@ def main():
     blob = L.synthetic_model(1, variant)
     B = args.streams
     from lpcnet_amd.shard import weak_shard
-    dt, (ks, kn, fs, fn), info, pcm = run_batch(L, blob, B, weak_shard(rank, B).start, args.warmup, args.steps, dist, args.timers)
+    dt, (ks, kn, fs, fn), info, pcm = run_batch(L, blob, B, weak_shard(rank, B).start, args.warmup, args.steps, dist,
+                                                args.timers)
     dt = max_over_ranks(dist, dt)
     samples = world * B * 160 * args.steps
     value = samples / dt
-    # roofline of the dominant kernel (sample network), algorithmic bytes per launch
     sample_ms = ks / kn if kn else dt / args.steps * 1e3  # timers off: the frame step bounds the launch
-    bytes_launch = 160 * info.bytes_shared_per_sample + B * 160 * info.bytes_per_stream_sample
-    achieved = bytes_launch / (sample_ms * 1e-3) / 1e9
-    kname = info.kernel_name
-    pmc, tsrc = measured_pmc(kname) if B == 1024 else ({}, None)
-    traffic = pmc.get("hbm_bytes_per_launch_corrected")
+    config = {1024: "b1024", 256: "b256", 1: "b1"}.get(B, f"b{B}") + ("_fp32" if variant else "")
+    rf, mf = roofline(info, B, sample_ms, config)
     out = {
         "metric": "real-time 16 kHz streams/GPU; samples/s at batch=1 and batch=1024",
         "value": value,
@@ -218,40 +337,23 @@ def main():
                    "parallelism": f"stream shards x{world}, no collective"},
         "rt_streams_per_gpu": value / world / 16000.0,
         "frame_step_ms": dt / args.steps * 1e3,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-                     "kernel": kname, "avg_launch_ms": sample_ms, "launches": kn,
-                     "algorithmic_bytes_per_launch": bytes_launch},
+        "roofline": rf,
         "frame_kernel_avg_ms": fs / max(fn, 1),
         # matrix-core work of the sample kernel (north_star: MFMA at batch >= 256):
         # int8 ops issued per launch / launch time, and the PMC busy fraction
-        "mfma": ({"achieved_tops": info.mfma_ops_per_group_sample * ((B + info.streams_per_workgroup - 1)
-                                                                    // info.streams_per_workgroup) * 160
-                                   / (sample_ms * 1e-3) / 1e12,
-                  "peak_tops": I8_PEAK_TOPS, "busy_frac_pmc": pmc.get("mfma_util"),
-                  "ops_per_launch": info.mfma_ops_per_group_sample * ((B + info.streams_per_workgroup - 1)
-                                                                     // info.streams_per_workgroup) * 160}
-                 if info.mfma_ops_per_group_sample > 0 else None),
+        "mfma": mf,
         "kernel_config": {"streams_per_workgroup": info.streams_per_workgroup, "quad_path": info.quad_path,
                           "lds_bytes": info.lds_bytes, "gru_a_blocks": info.gru_a_blocks},
         "pcm_checksum": int(np.abs(pcm[-1].astype(np.int64)).sum()),
     }
+    if rank == 0 and world == 1 and not args.no_latency:
+        out["latency"] = latency(L, blob, B, sample_ms)
     if rank == 0 and world == 1 and not args.no_batch1:
-        dt1, (k1, n1, _, _), _, _ = run_batch(L, blob, 1, 0, args.warmup, max(args.steps, 20), None, args.timers)
-        s1 = max(args.steps, 20) * 160 / dt1
-        out["batch1"] = {"samples_per_s": s1, "x_realtime": s1 / 16000.0, "ms_per_frame": dt1 / max(args.steps, 20) * 1e3,
-                         "sample_kernel_avg_ms": k1 / max(n1, 1), "path": "int8"}
+        out["batch1"] = side_line(L, blob, 1, args, "b1", "int8")
         # BASELINE configs[1]: batch=1 with the fp32 (--disable-dot-product) GRU_A weights
-        blob32 = L.synthetic_model(1, L.VARIANT_FP32)
-        nf = max(args.steps, 20)
-        dt2, (k2, n2, _, _), _, _ = run_batch(L, blob32, 1, 0, args.warmup, nf, None, args.timers)
-        out["batch1_fp32"] = {"samples_per_s": nf * 160 / dt2, "x_realtime": nf * 160 / dt2 / 16000.0,
-                              "ms_per_frame": dt2 / nf * 1e3, "sample_kernel_avg_ms": k2 / max(n2, 1)}
+        out["batch1_fp32"] = side_line(L, L.synthetic_model(1, L.VARIANT_FP32), 1, args, "b1_fp32", "fp32")
         # BASELINE configs[2]: 256 streams on one GPU (int8 products on the matrix cores)
-        dt3, (k3, n3, _, _), info3, _ = run_batch(L, blob, 256, 0, args.warmup, nf, None, args.timers)
-        out["batch256"] = {"samples_per_s": 256 * nf * 160 / dt3, "rt_streams": 256 * nf * 160 / dt3 / 16000.0,
-                           "ms_per_frame": dt3 / nf * 1e3, "sample_kernel_avg_ms": k3 / max(n3, 1),
-                           "kernel": info3.kernel_name}
+        out["batch256"] = side_line(L, blob, 256, args, "b256", "int8")
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

@@ -30,8 +30,10 @@ typedef struct {
   int gru_b_blocks;     /* 8x4 blocks in gru_b_weights */
   int may_saturate;     /* 1 if an int8 pair can saturate the int16 maddubs sum */
   double bytes_shared_per_frame;  /* algorithmic weight bytes read once per frame step */
-  double bytes_shared_per_sample; /* algorithmic weight bytes read once per sample step */
-  double bytes_per_stream_sample; /* per-stream bytes per sample (gathers, trace-free) */
+  double bytes_shared_per_sample; /* algorithmic weight bytes read once per sample step (SURVEY 8d;
+                                     add bytes_shared_per_frame / 160 for the whole step) */
+  double bytes_per_stream_sample; /* per-stream bytes per sample (3 embedding rows, dual_fc path,
+                                     conditioning/features/PCM share; SURVEY 8d: 15,009) */
   double ops_per_sample;          /* 2*MAC per stream per sample */
   int streams_per_workgroup;      /* streams per sample-kernel workgroup */
   int quad_path;                  /* sample kernel: 0 lockstep (per-slot LDS layout), 1 lockstep (quad

@@ -842,7 +842,10 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   in.bytes_shared_per_frame = frame_w;
   in.bytes_shared_per_sample = 32.0 * nba * wbytes + 4.0 * (nba + GA_ROWS / 8) /* idx */ + 6.0 * NA * 4 /* bias+diag */ +
                                32.0 * nbb * wbytes + 4.0 * (nbb + GB_ROWS / 8) + 3.0 * NB * NB * wbytes + 2.0 * GB_ROWS * 4;
-  in.bytes_per_stream_sample = 3.0 * GA_ROWS * 4 /* embedding rows */ + 8 * (32 + 2 * 4 + 2 * 4) /* dual_fc path */ + 2;
+  /* 3 gathered embedding rows, the 8 dual_fc nodes on the path (2
+   * channels x (16 weights + bias + factor)), and the frame's conditioning +
+   * features per sample, the output sample */
+  in.bytes_per_stream_sample = 3.0 * GA_ROWS * 4 + 8 * 2 * (NB + 2) * 4 + (GA_ROWS + GB_ROWS + NF) * 4.0 / FRAME + 2;
   /* mf_kernel matrix-core work: per GRU_A wave 8 nzr + 4 nh 4x4x4 MFMAs of
    * 16 x 4x4x4 MACs; per sampler wave 21 16x16x64 MFMAs (2 sampler waves).
    */

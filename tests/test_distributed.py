@@ -1,7 +1,15 @@
-"""World-size-2 gloo run of the sharded path on CPU: each rank synthesises its
-own shard of streams (CPU oracle standing in for the per-rank engine), the
-ranks exchange only checksums, and the result is identical to the same global
-stream ids synthesised in one process (shard invariance)."""
+"""Sharded multi-rank path (streams shard, no data-path
+collective), world size 2 over gloo.
+
+* CPU (no GPU needed): the rank/shard plumbing with the CPU ORACLE standing
+  in for the per-rank engine -- each rank synthesises its own shard of
+  streams, the ranks exchange only checksums, and the result equals the same
+  global stream ids synthesised in one process.
+* -m gpu: the same with the ENGINE, through bench.py's own run_batch (the
+  timed path of `bench.py --gpus N`): each rank runs its weak shard on device
+  LOCAL_RANK % device_count() (both ranks share the card on a one-GPU box),
+  the PCM of every stream is gathered, and it must equal the single-process
+  run of the same global stream ids."""
 import os
 import socket
 
@@ -72,3 +80,44 @@ def test_two_rank_gloo_shard_invariance():
     single = [int(np.abs(_stream_pcm(blob, sid).astype(np.int64)).sum()) for sid in range(TOTAL)]
     assert sums == single
     assert maxlen == 3.0
+
+
+def _engine_worker(rank, world, port, out, per_rank, frames):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["LOCAL_RANK"] = str(rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import lpcnet_amd as L
+    blob = L.synthetic_model(1, 0)
+    _, _, _, pcm = bench.run_batch(L, blob, per_rank, weak_shard(rank, per_rank).start, 2, frames - 2, dist, 1)
+    t = torch.from_numpy(np.ascontiguousarray(pcm.astype(np.int32)))
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    if rank == 0:
+        out.put(np.concatenate([p.numpy() for p in parts], axis=1))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_engine_shard_invariance(require_gpu):
+    import bench
+    import lpcnet_amd as L
+    per_rank, frames, world = 96, 6, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engine_worker, args=(r, world, port, q, per_rank, frames)) for r in range(world)]
+    for p in procs:
+        p.start()
+    sharded = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    blob = L.synthetic_model(1, 0)
+    _, _, _, single = bench.run_batch(L, blob, world * per_rank, 0, 2, frames - 2, None, 1)
+    assert sharded.shape == single.shape == (frames, world * per_rank, 160)
+    assert np.array_equal(sharded, single.astype(np.int32))
+    assert np.abs(single[2:].astype(np.float64)).mean() > 100

@@ -1,62 +1,80 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 outputs into profiles/<round>/: kernel stats and the
-per-launch HBM traffic of the sample kernel from FETCH_SIZE / WRITE_SIZE.
-gfx950 correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE reads half the bytes
-of wide coalesced streaming reads -> doubled; both counters are in KB."""
+"""Summarise the rocprofv3 PMC passes of tools/gpu_evidence.sh into one JSON
+record per bench configuration:
+
+  {"source_sha256": <hash of lpcnet_amd/csrc + Makefile>,
+   "configs": {"b1024": {"<kernel>": {...}}, "b256": ..., "b1": ..., "b1_fp32": ...}}
+
+per kernel: median over its non-silent launches of
+  hbm_bytes_per_launch   2 x FETCH_SIZE + WRITE_SIZE (KB counters; gfx950:
+                         FETCH_SIZE reads half the bytes of wide reads,
+                         MI355X_MICROARCH.md "HBM")
+  l2_hit                 TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
+  mfma_util              SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
+bench.py reads it back only when source_sha256 matches the tree it runs from.
+Usage: pmc_summary.py <gpurun_out dir> <out.json>"""
 import csv
 import glob
+import hashlib
 import json
 import os
+import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def rows(pattern):
-    out = []
-    for f in glob.glob(pattern, recursive=True):
-        with open(f) as fh:
-            out += list(csv.DictReader(fh))
-    return out
+def source_sha256(root=ROOT):
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(root, "lpcnet_amd", "csrc", "*"))) + [os.path.join(root, "Makefile")]
+    for f in files:
+        if os.path.isfile(f):
+            h.update(os.path.basename(f).encode())
+            h.update(open(f, "rb").read())
+    return h.hexdigest()
 
 
-def per_kernel(counter_rows, counter):
-    agg = {}
-    for r in counter_rows:
-        if r.get("Counter_Name") != counter:
+def counters(d):
+    """{kernel: {counter: [per-dispatch values]}} of one pass directory"""
+    per = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"]
+            per.setdefault(k, {}).setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"], 0.0)
+            per[k][r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: {c: list(v.values()) for c, v in cs.items()} for k, cs in per.items()}
+
+
+def med_nonsilent(vals):
+    """median over launches above 20 % of the largest (drops the silent first frames)"""
+    if not vals:
+        return None
+    top = max(vals)
+    keep = [v for v in vals if v >= 0.2 * top] or vals
+    return statistics.median(keep)
+
+
+def main(outdir, out):
+    res = {"source_sha256": source_sha256(), "configs": {}}
+    for d in sorted(glob.glob(os.path.join(outdir, "pmc_*_*"))):
+        if not os.path.isdir(d):
             continue
-        k = r["Kernel_Name"]
-        agg.setdefault(k, []).append(float(r["Counter_Value"]))
-    return agg
-
-
-def main(outdir):
-    os.makedirs(outdir, exist_ok=True)
-    fetch = per_kernel(rows(os.path.join(ROOT, "gpurun_out/pmc_fetch/**/*counter_collection.csv")), "FETCH_SIZE")
-    write = per_kernel(rows(os.path.join(ROOT, "gpurun_out/pmc_write/**/*counter_collection.csv")), "WRITE_SIZE")
-    res = {}
-    for k in set(fetch) | set(write):
-        f = fetch.get(k, [])
-        w = write.get(k, [])
-        # drop the near-empty launches of the silent first frames (FEATURES_DELAY)
-        fm = sorted(f)[len(f) // 2] if f else None
-        wm = sorted(w)[len(w) // 2] if w else None
-        res[k] = {"launches": len(f), "fetch_kb_median": fm, "write_kb_median": wm,
-                  "hbm_bytes_per_launch_corrected": (2 * fm * 1024 if fm is not None else 0) + (wm * 1024 if wm is not None else 0)}
-    # MFMA utilisation: busy cycles of all SIMDs over (elapsed cycles x 1024
-    # SIMDs); elapsed = GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs)
-    mf = rows(os.path.join(ROOT, "gpurun_out/pmc_mfma/**/*counter_collection.csv"))
-    busy, gui, sqb = per_kernel(mf, "SQ_VALU_MFMA_BUSY_CYCLES"), per_kernel(mf, "GRBM_GUI_ACTIVE"), per_kernel(mf, "SQ_BUSY_CYCLES")
-    for k in set(busy) & set(gui):
-        b, g = sorted(busy[k]), sorted(gui[k])
-        bm, gm = b[len(b) // 2], g[len(g) // 2]
-        res.setdefault(k, {})
-        res[k].update({"mfma_busy_cycles_median": bm, "grbm_gui_active_median": gm,
-                       "sq_busy_cycles_median": sorted(sqb.get(k, [0]))[len(sqb.get(k, [0])) // 2],
-                       "mfma_util": bm / max(1.0, gm / 8 * 1024)})
-    json.dump(res, open(os.path.join(outdir, "pmc_traffic.json"), "w"), indent=1)
+        cfg = os.path.basename(d).split("_", 2)[2]  # pmc_<pass>_<config>
+        for k, cs in counters(d).items():
+            rec = res["configs"].setdefault(cfg, {}).setdefault(k, {})
+            for c, vals in cs.items():
+                rec[c] = med_nonsilent(vals)
+    for cfg, ks in res["configs"].items():
+        for k, r in ks.items():
+            if "FETCH_SIZE" in r and "WRITE_SIZE" in r:
+                r["hbm_bytes_per_launch"] = 2 * r["FETCH_SIZE"] * 1024 + r["WRITE_SIZE"] * 1024
+            if "TCC_HIT_sum" in r and "TCC_MISS_sum" in r:
+                r["l2_hit"] = r["TCC_HIT_sum"] / max(1.0, r["TCC_HIT_sum"] + r["TCC_MISS_sum"])
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in r and "GRBM_GUI_ACTIVE" in r:
+                r["mfma_util"] = r["SQ_VALU_MFMA_BUSY_CYCLES"] / max(1.0, r["GRBM_GUI_ACTIVE"] / 8 * 1024)
+    json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r01"))
+    main(sys.argv[1], sys.argv[2])
