@@ -224,6 +224,11 @@ def latency(L, blob, B, measured_ms):
             "sampler_post": float(sm[12]),
             "sampler_wait_at_Y": float(sm[1]),
         }
+        if os.environ.get("LPCNET_FINE_STAMPS"):
+            out["gru_a_waves"] = {f"w{w}": {"gathers": float(ga[w, 10]), "inputs": float(ga[w, 11]), "sigmoid": float(ga[w, 12]),
+                                            "tanh_update": float(ga[w, 13]), "quant_store": float(ga[w, 0]),
+                                            "waitY": float(ga[w, 1]), "recurrent": float(ga[w, 2]), "waitX": float(ga[w, 5])}
+                                  for w in range(6)}
     return out
 
 

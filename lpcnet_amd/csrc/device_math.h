@@ -110,6 +110,35 @@ __device__ __forceinline__ void sigmoid_x86_n(float (&X)[N], const uint32_t *tab
   for (int k = 0; k < N; k++) X[k] = clamp_x86(__builtin_fmaf(num[k], den[k], 0.5f), 0.f, 1.f);
 }
 
+/* sigmoid8_approx for inputs of the form (float)(int32) * kScale1 (+ another
+ * such term): |X| < 2^18, so X2 < 2^36, the Pade denominator lies in
+ * [952.72, 2^73) and the numerator is finite.  rcpps of such a denominator
+ * never reaches the flush-to-zero range (exponent field <= 200 < 253, see
+ * rcp_x86_fix) and no NaN can arise, so the result is rcp_x86 / clamp_x86
+ * without the flush select and the NaN select: identical to sigmoid_x86_n
+ * for every such input.  Used for the int8 products' z / r gates. */
+template <int N>
+__device__ __forceinline__ void sigmoid_x86_fin_n(float (&X)[N], const uint32_t *tab)
+{
+  float num[N], den[N];
+  uint32_t t[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const float X2 = X[k] * X[k];
+    num[k] = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
+    den[k] = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
+    num[k] = num[k] * X[k];
+    t[k] = tab[(__float_as_uint(den[k]) >> 12) & 0x7ff];
+  }
+#pragma unroll
+  for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const float r = __int_as_float((int)(t[k] - (__float_as_uint(den[k]) & 0x7f800000u)));
+    X[k] = __builtin_amdgcn_fmed3f(__builtin_fmaf(num[k], r, 0.5f), 0.f, 1.f);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void tanh_x86_n(float (&X)[N], const uint32_t *tab)
 {

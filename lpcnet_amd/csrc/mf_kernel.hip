@@ -162,6 +162,11 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8(st[s]);
     __syncthreads(); /* initial q(h_A), q(h_B), ix, seeds */
     stamp_start();
+#ifdef MF_PRIO45
+    /* waves 4/5 share SIMDs with the older waves 0/1 and lose every VALU
+     * arbitration at equal priority */
+    if (wv >= 4) __builtin_amdgcn_s_setprio(MF_PRIO45);
+#endif
 
     /* per-sample terms that depend only on the state and the recurrent sums,
      * computed right after the recurrent product (off the X->Y critical path):
@@ -215,64 +220,33 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
           asm volatile("" ::"v"(g));
           stamp(10);
         }
-        /* compute_sparse_gru elementwise (nnet.c:431-447) */
+        /* compute_sparse_gru elementwise (nnet.c:431-447).  Scalar float ops
+         * only: packed v_pk_add/mul_f32 (explicit or SLP-formed -- this file
+         * is built with -fno-slp-vectorize) cost more SIMD issue cycles than
+         * the scalar pairs, and waves 0/4 and 1/5 share one SIMD's VALU here
+         * (measured: 7,450 -> 7,240 cycles per sample at 1024 streams) */
         float zrv[2 * S], hv[S], inh[S];
-        if constexpr (S % 2 == 0) {
-          /* stream pairs on packed v_pk_add/mul_f32: each lane of a packed
-           * op is the scalar IEEE op, so the sums keep their order and bits */
-          typedef float v2f __attribute__((ext_vector_type(2)));
-          for (int s = 0; s < S; s += 2) {
-            const v2f inz = ((*(const v2f *)(cnd + i * S + s) + v2f{e[s][0], e[s + 1][0]}) + v2f{e[s][3], e[s + 1][3]}) +
-                            v2f{e[s][6], e[s + 1][6]};
-            const v2f inr = ((*(const v2f *)(cnd + (NA + i) * S + s) + v2f{e[s][1], e[s + 1][1]}) +
-                             v2f{e[s][4], e[s + 1][4]}) +
-                            v2f{e[s][7], e[s + 1][7]};
-            const v2f ih = ((*(const v2f *)(cnd + (2 * NA + i) * S + s) + v2f{e[s][2], e[s + 1][2]}) +
-                            v2f{e[s][5], e[s + 1][5]}) +
-                           v2f{e[s][8], e[s + 1][8]};
-            const v2f qz = (v2f{tz[s], tz[s + 1]} + inz) * kScale;
-            const v2f qr = (v2f{tr[s], tr[s + 1]} + inr) * kScale;
-            const v2f fz = v2f{(float)(az[s] + cvt_rne(qz.x)), (float)(az[s + 1] + cvt_rne(qz.y))} * kScale1;
-            const v2f fr = v2f{(float)(ar[s] + cvt_rne(qr.x)), (float)(ar[s + 1] + cvt_rne(qr.y))} * kScale1;
-            zrv[s] = fz.x;
-            zrv[s + 1] = fz.y;
-            zrv[S + s] = fr.x;
-            zrv[S + s + 1] = fr.y;
-            inh[s] = ih.x;
-            inh[s + 1] = ih.y;
-            hv[s] = hpre[s];
-            hv[s + 1] = hpre[s + 1];
-          }
-        } else {
-          for (int s = 0; s < S; s++) {
-            const float inz = ((cnd[i * S + s] + e[s][0]) + e[s][3]) + e[s][6];
-            const float inr = ((cnd[(NA + i) * S + s] + e[s][1]) + e[s][4]) + e[s][7];
-            inh[s] = ((cnd[(2 * NA + i) * S + s] + e[s][2]) + e[s][5]) + e[s][8];
-            zrv[s] = (float)(az[s] + cvt_rne((tz[s] + inz) * kScale)) * kScale1;
-            zrv[S + s] = (float)(ar[s] + cvt_rne((tr[s] + inr) * kScale)) * kScale1;
-            hv[s] = hpre[s];
-          }
+        for (int s = 0; s < S; s++) {
+          const float inz = ((cnd[i * S + s] + e[s][0]) + e[s][3]) + e[s][6];
+          const float inr = ((cnd[(NA + i) * S + s] + e[s][1]) + e[s][4]) + e[s][7];
+          inh[s] = ((cnd[(2 * NA + i) * S + s] + e[s][2]) + e[s][5]) + e[s][8];
+          zrv[s] = (float)(az[s] + cvt_rne((tz[s] + inz) * kScale)) * kScale1;
+          zrv[S + s] = (float)(ar[s] + cvt_rne((tr[s] + inr) * kScale)) * kScale1;
+          hv[s] = hpre[s];
         }
-        sigmoid_x86_n<2 * S>(zrv, rcp);
-        if constexpr (S % 2 == 0) {
-          typedef float v2f __attribute__((ext_vector_type(2)));
-          for (int s = 0; s < S; s += 2) {
-            const v2f h2 = v2f{hv[s], hv[s + 1]} * v2f{zrv[S + s], zrv[S + s + 1]} + v2f{inh[s], inh[s + 1]};
-            hv[s] = h2.x;
-            hv[s + 1] = h2.y;
-          }
-          tanh_x86_n<S>(hv, rcp);
-          for (int s = 0; s < S; s += 2) {
-            const v2f z = v2f{zrv[s], zrv[s + 1]};
-            const v2f n2 = z * v2f{st[s], st[s + 1]} + (1.f - z) * v2f{hv[s], hv[s + 1]};
-            st[s] = n2.x;
-            st[s + 1] = n2.y;
-          }
-        } else {
-          for (int s = 0; s < S; s++) hv[s] = hv[s] * zrv[S + s] + inh[s];
-          tanh_x86_n<S>(hv, rcp);
-          for (int s = 0; s < S; s++) st[s] = zrv[s] * st[s] + (1.f - zrv[s]) * hv[s];
-        }
+#ifdef MF_FINE
+        if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(11); }
+#endif
+        sigmoid_x86_fin_n<2 * S>(zrv, rcp);
+#ifdef MF_FINE
+        if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(12); }
+#endif
+        for (int s = 0; s < S; s++) hv[s] = hv[s] * zrv[S + s] + inh[s];
+        tanh_x86_n<S>(hv, rcp);
+        for (int s = 0; s < S; s++) st[s] = zrv[s] * st[s] + (1.f - zrv[s]) * hv[s];
+#ifdef MF_FINE
+        if (stamping) { float g = 0.f; for (int k = 0; k < S; k++) g += st[k]; asm volatile("" ::"v"(g)); stamp(13); }
+#endif
         for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8(st[s]);
       }
       stamp(0);
@@ -411,7 +385,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         /* GRU_B elementwise (nnet.c:362-371), unit gu of stream sl */
         float zrb[2] = {(float)pick(acc[0]) * kScale1 + (float)pick(accr[0]) * kScale1,
                         (float)pick(acc[1]) * kScale1 + (float)pick(accr[1]) * kScale1};
-        sigmoid_x86_n<2>(zrb, rcp);
+        sigmoid_x86_fin_n<2>(zrb, rcp);
         float hh[1] = {(float)pick(acc[2]) * kScale1 + ((float)pick(accr[2]) * kScale1) * zrb[1]};
         stamp(14);
         tanh_x86_n<1>(hh, rcp);
