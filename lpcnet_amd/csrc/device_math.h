@@ -44,8 +44,7 @@ __device__ __forceinline__ float rcp_x86(float x, const uint32_t *tab)
    * such den (oracle/checks/exact_identities.c (4)); a NaN den only occurs
    * with a NaN numerator, whose product stays NaN.  The table load is pinned
    * (empty asm) so the select stays branch-free. */
-  const uint32_t u = __float_as_uint(x);
-  uint32_t t = tab[(u >> 12) & 0x7ff];
+  uint32_t t = tab[__builtin_amdgcn_ubfe(__float_as_uint(x), 12, 11)];
   asm volatile("" : "+v"(t));
   return rcp_x86_fix(x, t);
 }
@@ -85,7 +84,7 @@ __device__ __forceinline__ void rcp_x86_n(float (&x)[N], const uint32_t *tab)
 {
   uint32_t t[N];
 #pragma unroll
-  for (int k = 0; k < N; k++) t[k] = tab[(__float_as_uint(x[k]) >> 12) & 0x7ff];
+  for (int k = 0; k < N; k++) t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(x[k]), 12, 11)];
 #pragma unroll
   for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
 #pragma unroll
@@ -128,7 +127,7 @@ __device__ __forceinline__ void sigmoid_x86_fin_n(float (&X)[N], const uint32_t 
     num[k] = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
     den[k] = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
     num[k] = num[k] * X[k];
-    t[k] = tab[(__float_as_uint(den[k]) >> 12) & 0x7ff];
+    t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(den[k]), 12, 11)];
   }
 #pragma unroll
   for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
@@ -172,9 +171,13 @@ __device__ __forceinline__ int cvt_rne(float v)
  * min(r, 255) otherwise. */
 __device__ __forceinline__ uint32_t quant_s8(float x)
 {
-  const float r = __builtin_rintf(__builtin_fmaf(x, 127.f, 127.f));
-  const uint32_t q = (uint32_t)__builtin_amdgcn_fmed3f(r, 0.f, 255.f);
-  return (r < 2147483648.f ? q : 0u) ^ 0x80u;
+  /* v_cvt_pk_u8_f32 = min(255, max(0, rne(v))), NaN -> 0 (measured over
+   * every 1/64 step of [-4, 258], the halves and the specials:
+   * tools/probes/cvt_u8_probe.hip); only v >= 2^31 (-> 255 here, 0 on x86)
+   * needs the select */
+  const float v = __builtin_fmaf(x, 127.f, 127.f);
+  const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(v, 0, 0u);
+  return (v < 2147483648.f ? q : 0u) ^ 0x80u;
 }
 
 constexpr float kScale = 128.f * 127.f;          /* vec_avx.h:686 */
