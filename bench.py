@@ -224,6 +224,9 @@ def latency(L, blob, B, measured_ms):
             "sampler_post": float(sm[12]),
             "sampler_wait_at_Y": float(sm[1]),
         }
+        if os.environ.get("LPCNET_WALK_STAMPS"):
+            out["walk_cycles"] = {"level0_3_logit": float(sm[2]), "level0_3_decide_and_w47": float(sm[3]),
+                                  "level4_7_logit": float(sm[15]), "decide_select": float(sm[11])}
         if os.environ.get("LPCNET_FINE_STAMPS"):
             out["gru_a_waves"] = {f"w{w}": {"gathers": float(ga[w, 10]), "inputs": float(ga[w, 11]), "sigmoid": float(ga[w, 12]),
                                             "tanh_update": float(ga[w, 13]), "quant_store": float(ga[w, 0]),

@@ -405,8 +405,21 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         }
       }
       stamp(9);
+#ifdef MF_WALKFINE
+      auto wst = [&](int k, float v) {
+        if (stamping) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const int u = __builtin_amdgcn_readfirstlane(__float_as_int(v));
+          asm volatile("" ::"s"(u));
+          stamp(k);
+        }
+      };
+      const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
+                                            deemph, wst);
+#else
       const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
                                             deemph);
+#endif
       stamp(11);
       if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + ms * 4) = make_int4(R.su, R.pu, R.exc, 0);
       if (tracing && samp_w && hl < 8 && my_active) {

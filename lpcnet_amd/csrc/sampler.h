@@ -84,15 +84,21 @@ __device__ __forceinline__ void lane_thresholds(const FcLane &F, const float *lo
  * history and coefficients.  teach != nullptr: teacher forcing with input
  * *teach (lpcnet.c:256-259).  Uniform per half.  TRACE: also return the
  * 8 logits along the path. */
-template <bool TRACE>
+/* phase-stamp hook of dual_fc_walk (diagnostic builds: mf_kernel -DMF_WALKFINE) */
+struct WalkNoStamp {
+  __device__ __forceinline__ void operator()(int, float) const {}
+};
+
+template <bool TRACE, class ST = WalkNoStamp>
 __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, float t47, const float (&xv)[NB], float pred,
                                                 const float (&lsr)[NLPC], const float (&lpr)[NLPC], const short *teach,
-                                                float deemph)
+                                                float deemph, ST st = ST())
 {
   WalkOut R;
   int val = 0;
   {
     const float l = F.node_logit(F.b03, F.f03, F.w03, xv);
+    st(2, l);
     const unsigned long long m = __ballot(t03 < l) >> F.hb;
 #pragma unroll
     for (int b = 0; b < 4; b++) {
@@ -117,6 +123,7 @@ __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, floa
       w47[4 * j] = v.x; w47[4 * j + 1] = v.y; w47[4 * j + 2] = v.z; w47[4 * j + 3] = v.w;
     }
   }
+  st(3, w47[NB - 1] + b47 + f47);
   /* candidate exc = 16*prefix + (hl & 15): output sample, pred(n+1), u-law
    * indices (lpcnet.c:252-261), the reference's operations in order */
   const float sp_pcm = pred + F.ulaw[(val << 4) | (F.hl & 15)];
@@ -127,6 +134,7 @@ __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, floa
   const int sp_idx = lin2ulaw_x86(sp_pcm) | (lin2ulaw_x86(sp_pred) << 8);
   {
     const float l = F.node_logit(b47, f47, w47, xv);
+    st(15, l);
     const unsigned long long m = __ballot(t47 < l) >> F.hb;
 #pragma unroll
     for (int b = 4; b < 8; b++) {
