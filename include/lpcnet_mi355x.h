@@ -102,6 +102,13 @@ LPCNET_EXPORT int lpcnet_batch_sync(LPCNetBatch *b);
  * the default (2^20 polls); tiny values exist to test the reporting. */
 LPCNET_EXPORT int lpcnet_batch_set_spin_limit(LPCNetBatch *b, int polls);
 
+/* Multi-frame path for batches above 128 streams with the matrix-core or
+ * fp32 sample kernel: the frame network of each run of up to 32 frames
+ * (>= 4) is computed in one launch before their sample kernels (chunk_kernel,
+ * f32 matrix cores; identical outputs).  enable = 0 selects the per-frame
+ * frame kernel instead (A/B and parity tests); default 1. */
+LPCNET_EXPORT int lpcnet_batch_set_frame_chunking(LPCNetBatch *b, int enable);
+
 /* Device memory helpers (so callers need no HIP headers). */
 LPCNET_EXPORT void *lpcnet_batch_device_alloc(LPCNetBatch *b, size_t bytes);
 LPCNET_EXPORT int lpcnet_batch_device_free(LPCNetBatch *b, void *p);
@@ -110,7 +117,8 @@ LPCNET_EXPORT int lpcnet_batch_memcpy_d2h(LPCNetBatch *b, void *dst, const void 
 
 /* Kernel timing (HIP events on the batch's stream, recorded around every
  * launch since the last reset_timers): which = 0 sample-network kernel,
- * 1 frame-network kernel.  Returns total ms and the number of launches.
+ * 1 frame-network kernel (per-frame frame kernel, or chunk_kernel once per
+ * run of frames).  Returns total ms and the number of launches.
  * enable: 0 off, 1 events around the sample kernel only, 2 (or more) around
  * both kernels. */
 LPCNET_EXPORT void lpcnet_batch_reset_timers(LPCNetBatch *b, int enable);

@@ -68,6 +68,7 @@ def _load():
         "lpcnet_batch_synthesize_frames": (i, [vp, vp, vp, vp, i, i]),
         "lpcnet_batch_sync": (i, [vp]),
         "lpcnet_batch_set_spin_limit": (i, [vp, i]),
+        "lpcnet_batch_set_frame_chunking": (i, [vp, i]),
         "lpcnet_mi355x_validate_model": (i, [C.c_char_p, i]),
         "lpcnet_batch_device_alloc": (vp, [vp, C.c_size_t]),
         "lpcnet_batch_device_free": (i, [vp, vp]),
@@ -234,6 +235,11 @@ class LPCNetBatch:
         """LDS flag-wait bound of the barrier-free kernel (0 = default); see lpcnet_mi355x.h."""
         if lib.lpcnet_batch_set_spin_limit(self._b, polls) != 0:
             raise LPCNetError("bad spin limit")
+
+    def set_frame_chunking(self, enable: bool) -> None:
+        """Chunked frame network for batches above 128 streams (default on); off = per-frame kernel."""
+        if lib.lpcnet_batch_set_frame_chunking(self._b, 1 if enable else 0) != 0:
+            raise LPCNetError("set_frame_chunking failed")
 
     def info(self) -> ModelInfo:
         mi = ModelInfo()

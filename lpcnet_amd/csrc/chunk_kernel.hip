@@ -1,0 +1,306 @@
+/*
+ * chunk_kernel.hip -- run_frame_network (lpcnet.c:82-120) for every frame of
+ * a chunk of up to LPC_CHUNK frames at once, on the f32 matrix cores.
+ *
+ * The frame network never reads the sample network's outputs: frame f's
+ * inputs are the features of frames f-2..f (conv1), conv1's outputs of
+ * frames f-2..f (conv2) and the LPC of frame f-2.  So a chunk of frames is
+ * one batch of columns (stream, frame) through the five layers, and every
+ * weight is fetched once per 64 columns instead of once per 4.
+ *
+ * Numerics: v_mfma_f32_16x16x4_f32 computes
+ *   D = fma(a3, b3, fma(a2, b2, fma(a1, b1, fma(a0, b0, C))))
+ * in k order, one rounding per product (cdna_hip_programming.md, FP32-input
+ * MFMA) -- the sequential fmaf chain of sgemv_accum16 (vec_avx.h:618-643)
+ * started from the bias, so a row chained over its inputs 4 at a time is the
+ * per-frame frame_kernel's result bit for bit.  tanh is the Pade form with
+ * emulated rcpps (device_math.h).
+ *
+ * Workgroup = 64 columns = CkGeom<NFR>::SC streams x NFR frames (frames
+ * >= nframes are computed on zero inputs and never stored); 8 waves.
+ * Layers with 128 rows: wave w owns row tile w for all 4 column tiles (one
+ * weight fragment feeds 4 MFMAs).  Projections (1200 rows = 75 tiles): wave w
+ * owns tiles w, w + 8, ...  Activations live in LDS as [column][input] rows
+ * whose stride makes the B-operand reads (16 columns x 4 inputs per
+ * wave-instruction) bank-conflict free; weights stream from L2 in the blob's
+ * [in][out] layout, PD steps ahead (the device copies carry FRAME_PREFETCH
+ * zero input rows, so the prefetch needs no clamp).
+ */
+#include <hip/hip_runtime.h>
+
+#include "device_math.h"
+#include "lpcnet_engine.h"
+
+namespace lpcnet_mi355x {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int CK_THREADS = 512;
+constexpr int CK_COLS = 64;       /* (stream, frame) columns per workgroup */
+constexpr int CK_RS = COND + 4;   /* row stride of 128-wide activation rows: 4c + k banks */
+constexpr int CK_PROJ = GA_ROWS + GB_ROWS;
+constexpr int CK_PROJ_TILES = CK_PROJ / 16;
+static_assert(CK_PROJ % 16 == 0 && COND == 8 * 16, "row tiles");
+
+/* smallest stride >= v that is 32 mod 64 floats: a 16-column tile that spans
+ * two streams (NFR = 8) then reads 64 distinct banks */
+constexpr int ck_stride32(int v) { return v + ((32 - v % 64) + 64) % 64; }
+constexpr int ck_max(int a, int b) { return a > b ? a : b; }
+
+template <int NFR>
+struct CkGeom {
+  static constexpr int SC = CK_COLS / NFR;                 /* streams per workgroup */
+  static constexpr int INF = NFR + 2;                      /* frames -2 .. NFR-1 */
+  static constexpr int IN_SS = ck_stride32(INF * FIN);     /* conv1 inputs: stream stride */
+  static constexpr int C1_SS = ck_stride32(INF * CK_RS);   /* conv1 outputs: stream stride */
+  static constexpr int R0 = ck_max(SC * IN_SS, CK_COLS * CK_RS); /* conv1 inputs, then dense1 outputs */
+  static constexpr int R1 = SC * C1_SS;
+  static constexpr int R2 = CK_COLS * CK_RS;               /* conv2, then dense2 outputs */
+  static constexpr int FLOATS = R0 + R1 + R2;
+};
+
+/* Row tile rt (16 rows) of a layer for the 4 column tiles:
+ *   acc[j][i] = bias[row] + sum_k W[k][row] * X(col, k),  row = 16 rt + 4 g + i,
+ * col = 16 j + (lane & 15), the chain in k order.  X(col, k) =
+ * xs[xb[j] + (k / SEG) * SST + k % SEG]: a column's inputs as segments of SEG
+ * values SST apart (conv windows over padded frame rows). */
+template <int K, int NOUT, int SEG, int SST>
+__device__ __forceinline__ void ck_tile(const float *__restrict__ W, const float *__restrict__ bias, int rt,
+                                        const float *xs, const int (&xb)[4], f32x4 (&acc)[4])
+{
+  static_assert(K % 4 == 0 && SEG % 4 == 0, "k quads stay inside a segment");
+  constexpr int KS = K / 4;
+  constexpr int PD = 16; /* weight fragments in flight */
+  static_assert(4 * PD <= FRAME_PREFETCH, "prefetch beyond the padding");
+  const int l = threadIdx.x & 63, g = l >> 4, r = l & 15;
+  const float *wp = W + (size_t)g * NOUT + 16 * rt + r;
+  float w[PD];
+#pragma unroll
+  for (int d = 0; d < PD; d++) w[d] = wp[(size_t)(4 * d) * NOUT];
+  const float4 b4 = *(const float4 *)(bias + 16 * rt + 4 * g);
+#pragma unroll
+  for (int j = 0; j < 4; j++) acc[j] = f32x4{b4.x, b4.y, b4.z, b4.w};
+  float xv[4], xn[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) xv[j] = xs[xb[j] + g];
+#pragma unroll
+  for (int kk = 0; kk < KS; kk++) {
+    if (kk + 1 < KS) {
+      const int o = ((4 * (kk + 1)) / SEG) * SST + (4 * (kk + 1)) % SEG;
+#pragma unroll
+      for (int j = 0; j < 4; j++) xn[j] = xs[xb[j] + g + o];
+    }
+    const float a = w[kk % PD];
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xv[j], acc[j], 0, 0, 0);
+    w[kk % PD] = wp[(size_t)(4 * (kk + PD)) * NOUT];
+#pragma unroll
+    for (int j = 0; j < 4; j++) xv[j] = xn[j];
+  }
+}
+
+/* frame_count before frame f's update, given its value fc0 at the chunk start
+ * (lpcnet.c:119: incremented while below 1000) */
+__device__ __forceinline__ int ck_fc(int fc0, int f) { return fc0 >= 1000 ? fc0 : min(fc0 + f, 1000); }
+
+template <int NFR>
+__global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
+{
+  using G = CkGeom<NFR>;
+  extern __shared__ float4 lds4_[];
+  float *lds = (float *)lds4_;
+  float *inl = lds;          /* [SC][IN_SS]: frame inputs, row f + 2 = frame f (FIN values) */
+  float *yb = lds;           /* [64][CK_RS]: dense1 outputs (inl is dead by then) */
+  float *c1 = lds + G::R0;   /* [SC][C1_SS]: conv1 outputs, row f + 2 = frame f (stride CK_RS) */
+  float *ya = c1 + G::R1;    /* [64][CK_RS]: conv2, then dense2 outputs */
+  __shared__ int fcs[G::SC];
+  __shared__ float olpc[G::SC][FEATURES_DELAY][NLPC];
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, g = l >> 4, r = l & 15;
+  const int s0 = blockIdx.x * G::SC;
+  const int n = A.nframes, B = A.nstreams;
+  const uint32_t *rcp = A.rcp;
+
+  /* inputs (lpcnet.c:91-99): frames -2, -1 from the conv1 memory, then
+   * features | pitch embedding of each frame of the chunk */
+  for (int e = tid; e < G::SC * G::INF * FIN; e += CK_THREADS) {
+    const int s = e / (G::INF * FIN), rem = e % (G::INF * FIN);
+    const int fr = rem / FIN - 2, j = rem % FIN, sid = s0 + s;
+    float v = 0.f;
+    if (sid < B) {
+      if (fr < 0) {
+        v = A.st[sid].conv1_mem[(fr + 2) * FIN + j];
+      } else if (fr < n) {
+        const float *ft = A.features + ((size_t)fr * B + sid) * NF;
+        if (j < NF) {
+          v = ft[j];
+        } else {
+          /* lpcnet.c:93-94: the 0.1 avoids rounding issues */
+          int pitch = (int)floor(.1 + (double)(50.f * ft[18]) + 100);
+          pitch = min(255, max(33, pitch));
+          v = A.embed_pitch[pitch * EP + (j - NF)];
+        }
+      }
+    }
+    inl[s * G::IN_SS + rem] = v;
+  }
+  /* conv1 outputs of frames -2, -1: the conv2 memory */
+  for (int e = tid; e < G::SC * 2 * COND; e += CK_THREADS) {
+    const int s = e / (2 * COND), j = e % (2 * COND), sid = s0 + s;
+    c1[s * G::C1_SS + (j / COND) * CK_RS + j % COND] = sid < B ? A.st[sid].conv2_mem[j] : 0.f;
+  }
+  if (tid < G::SC * FEATURES_DELAY * NLPC) {
+    const int s = tid / (FEATURES_DELAY * NLPC), q = tid % (FEATURES_DELAY * NLPC), sid = s0 + s;
+    olpc[s][q / NLPC][q % NLPC] = sid < B ? A.st[sid].old_lpc[q / NLPC][q % NLPC] : 0.f;
+  }
+  if (tid < G::SC) fcs[tid] = s0 + tid < B ? A.st[s0 + tid].frame_count : 1000;
+  __syncthreads();
+
+  /* this lane's column of each column tile */
+  int cs[4], cf[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    cs[j] = (16 * j + r) / NFR;
+    cf[j] = (16 * j + r) % NFR;
+  }
+  int xb[4];
+  f32x4 acc[4];
+
+  /* conv1 (nnet.c:452-470): 252 inputs -> 128, tanh; cleared while frame_count < 1 (lpcnet.c:99) */
+#pragma unroll
+  for (int j = 0; j < 4; j++) xb[j] = cs[j] * G::IN_SS + cf[j] * FIN; /* window = frames f-2..f */
+  ck_tile<3 * FIN, COND, 3 * FIN, 3 * FIN>(A.conv1_w, A.conv1_b, wave, inl, xb, acc);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const bool clr = ck_fc(fcs[cs[j]], cf[j]) < 1;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const float t = tanh_x86(acc[j][i], rcp);
+      c1[cs[j] * G::C1_SS + (cf[j] + 2) * CK_RS + 16 * wave + 4 * g + i] = clr ? 0.f : t;
+    }
+  }
+  __syncthreads();
+
+  /* the conv1 memory after the chunk: inputs of frames n-2, n-1 (nnet.c:469) */
+  for (int e = tid; e < G::SC * 2 * FIN; e += CK_THREADS) {
+    const int s = e / (2 * FIN), j = e % (2 * FIN), sid = s0 + s;
+    if (sid < B) A.st[sid].conv1_mem[j] = inl[s * G::IN_SS + n * FIN + j];
+  }
+  /* conv2: 384 inputs -> 128, tanh; cleared while frame_count < FEATURES_DELAY (lpcnet.c:101) */
+#pragma unroll
+  for (int j = 0; j < 4; j++) xb[j] = cs[j] * G::C1_SS + cf[j] * CK_RS;
+  ck_tile<3 * COND, COND, COND, CK_RS>(A.conv2_w, A.conv2_b, wave, c1, xb, acc);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const bool clr = ck_fc(fcs[cs[j]], cf[j]) < FEATURES_DELAY;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const float t = tanh_x86(acc[j][i], rcp);
+      ya[(16 * j + r) * CK_RS + 16 * wave + 4 * g + i] = clr ? 0.f : t;
+    }
+  }
+  __syncthreads();
+
+  /* dense1, dense2 (lpcnet.c:104-105) */
+#pragma unroll
+  for (int j = 0; j < 4; j++) xb[j] = (16 * j + r) * CK_RS;
+  ck_tile<COND, COND, COND, CK_RS>(A.dense1_w, A.dense1_b, wave, ya, xb, acc);
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+#pragma unroll
+    for (int i = 0; i < 4; i++) yb[(16 * j + r) * CK_RS + 16 * wave + 4 * g + i] = tanh_x86(acc[j][i], rcp);
+  __syncthreads();
+  ck_tile<COND, COND, COND, CK_RS>(A.dense2_w, A.dense2_b, wave, yb, xb, acc);
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+#pragma unroll
+    for (int i = 0; i < 4; i++) ya[(16 * j + r) * CK_RS + 16 * wave + 4 * g + i] = tanh_x86(acc[j][i], rcp);
+  __syncthreads();
+
+  /* conditioning projections (lpcnet.c:106-107), linear: gadf | gbdf as one
+   * [128][1200] matrix, 75 row tiles over the 8 waves; frame f's outputs go
+   * to cond[f], the last frame's also to the stream state */
+#pragma unroll 1
+  for (int rt = wave; rt < CK_PROJ_TILES; rt += CK_THREADS / 64) {
+    ck_tile<COND, CK_PROJ, COND, CK_RS>(A.proj_w, A.proj_b, rt, ya, xb, acc);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int sid = s0 + cs[j], f = cf[j];
+      if (sid >= B || f >= n) continue;
+      FrameCond *q = &A.cond[(size_t)f * B + sid];
+      StreamState *p = &A.st[sid];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int row = 16 * rt + 4 * g + i;
+        const float v = acc[j][i];
+        if (row < GA_ROWS) {
+          q->gru_a_cond[row] = v;
+          if (f == n - 1) p->gru_a_cond[row] = v;
+        } else {
+          q->gru_b_cond[row - GA_ROWS] = v;
+          if (f == n - 1) p->gru_b_cond[row - GA_ROWS] = v;
+        }
+      }
+    }
+  }
+
+  /* per frame: the LPC it synthesises with (lpcnet.c:110-118: the ring's
+   * older slot, i.e. lpc_from_cepstrum of frame f - 2; LPC_GAMMA = 1) and
+   * frame_count after its update */
+  for (int e = tid; e < G::SC * NFR * (NLPC + 1); e += CK_THREADS) {
+    const int s = e / (NFR * (NLPC + 1)), rem = e % (NFR * (NLPC + 1));
+    const int f = rem / (NLPC + 1), k = rem % (NLPC + 1), sid = s0 + s;
+    if (sid >= B || f >= n) continue;
+    FrameCond *q = &A.cond[(size_t)f * B + sid];
+    if (k == NLPC) {
+      const int fc = ck_fc(fcs[s], f);
+      q->frame_count = fc < 1000 ? fc + 1 : fc;
+    } else {
+      const int t = f - 2;
+      q->lpc[k] = (t >= 0 ? A.lpc_new[((size_t)t * B + sid) * NLPC + k] : olpc[s][-1 - t][k]) * 1.0f;
+    }
+  }
+  /* the stream state after the chunk: conv2 memory = conv1 outputs of frames
+   * n-2, n-1; LPC ring; lpc of the last frame; frame_count */
+  for (int e = tid; e < G::SC * 2 * COND; e += CK_THREADS) {
+    const int s = e / (2 * COND), j = e % (2 * COND), sid = s0 + s;
+    if (sid < B) A.st[sid].conv2_mem[j] = c1[s * G::C1_SS + (n + j / COND) * CK_RS + j % COND];
+  }
+  if (tid < G::SC * NLPC) {
+    const int s = tid / NLPC, k = tid % NLPC, sid = s0 + s;
+    if (sid < B) {
+      auto L = [&](int t) { return t >= 0 ? A.lpc_new[((size_t)t * B + sid) * NLPC + k] : olpc[s][-1 - t][k]; };
+      StreamState *p = &A.st[sid];
+      p->lpc[k] = L(n - 3) * 1.0f;
+      p->old_lpc[0][k] = L(n - 1);
+      p->old_lpc[1][k] = L(n - 2);
+    }
+  }
+  if (tid < G::SC && s0 + tid < B) A.st[s0 + tid].frame_count = ck_fc(fcs[tid], n);
+}
+
+template <int NFR>
+static int launch_chunk_t(const FrameArgs &a, void *stream)
+{
+  using G = CkGeom<NFR>;
+  static bool attr = false;
+  const int bytes = G::FLOATS * 4;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void *)chunk_kernel<NFR>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) !=
+        hipSuccess)
+      return -1;
+    attr = true;
+  }
+  const int grid = (a.nstreams + G::SC - 1) / G::SC;
+  hipLaunchKernelGGL(chunk_kernel<NFR>, dim3(grid), dim3(CK_THREADS), bytes, (hipStream_t)stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_chunk(const FrameArgs &a, void *stream)
+{
+  if (a.nframes < 1 || a.nframes > LPC_CHUNK || !a.cond) return -1;
+  if (a.nframes <= 8) return launch_chunk_t<8>(a, stream);
+  if (a.nframes <= 16) return launch_chunk_t<16>(a, stream);
+  return launch_chunk_t<32>(a, stream);
+}
+
+}  // namespace lpcnet_mi355x

@@ -281,6 +281,11 @@ struct LPCNetBatch {
   hipEvent_t ev_frame[2] = {nullptr, nullptr}, ev_samp[2] = {nullptr, nullptr}, ev_start = nullptr;
   bool ev_samp_used[2] = {false, false};
   hipEvent_t ev_samp_cur[2] = {nullptr, nullptr}; /* the event slot c's reuse waits on */
+  /* chunked multi-frame path (batches above OVERLAP_MAX_STREAMS): the frame
+   * network of up to LPC_CHUNK frames in one chunk_kernel launch, outputs of
+   * frame f in d_chunk[f][B] */
+  FrameCond *d_chunk = nullptr;
+  bool chunking = true;
   /* trace */
   bool trace = false;
   float *d_trace_logits = nullptr;
@@ -991,6 +996,74 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
   return 0;
 }
 
+/* Chunked form: the frame network of frames [0, n) of d_features has run
+ * (chunk_kernel, outputs in d_chunk[f]); launch the sample kernel of frame f
+ * on b->stream, reading its conditioning from d_chunk[f]. */
+int launch_chunk_samples(LPCNetBatch *b, int f, short *d_pcm, int N)
+{
+  SampleArgs sa = b->sa;
+  sa.st = b->d_state;
+  sa.cond = b->d_chunk + (size_t)f * b->B;
+  sa.nstreams = b->B;
+  sa.N = N;
+  sa.pcm = d_pcm;
+  sa.preload = 0;
+  sa.stamps = b->d_stamps;
+  sa.status = b->d_status;
+  sa.spin_limit = b->spin_limit;
+  hipEvent_t e1 = nullptr, e2 = nullptr;
+  if (b->timing >= 1) {
+    e1 = get_event(b);
+    e2 = get_event(b);
+    HIPCHK(hipEventRecord(e1, b->stream));
+  }
+  const int lrc = N <= 0 ? 0 : b->fp ? launch_fp(sa, b->stream) : launch_mf(sa, b->S, b->info.lds_bytes, b->stream);
+  if (lrc) {
+    set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return -1;
+  }
+  if (e1) {
+    HIPCHK(hipEventRecord(e2, b->stream));
+    b->ev_pairs[0].push_back(e1);
+    b->ev_pairs[0].push_back(e2);
+    b->ev_taken.push_back(e1);
+    b->ev_taken.push_back(e2);
+  }
+  return 0;
+}
+
+/* Chunked form: the frame network of n frames (features [n][B][NF], their
+ * LPC already in d_lpc) in one launch on b->stream. */
+int launch_chunk_frames(LPCNetBatch *b, const float *d_features, int n)
+{
+  FrameArgs fa = b->fa;
+  fa.st = b->d_state;
+  fa.nstreams = b->B;
+  fa.features = d_features;
+  fa.lpc_new = b->d_lpc;
+  fa.nframes = n;
+  fa.cond = b->d_chunk;
+  fa.stamps = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (b->timing >= 2) {
+    e0 = get_event(b);
+    e1 = get_event(b);
+    HIPCHK(hipEventRecord(e0, b->stream));
+  }
+  if (launch_chunk(fa, b->stream)) {
+    set_err("chunk kernel launch failed");
+    return -1;
+  }
+  if (e0) {
+    HIPCHK(hipEventRecord(e1, b->stream));
+    b->ev_pairs[1].push_back(e0);
+    b->ev_pairs[1].push_back(e1);
+    b->ev_taken.push_back(e0);
+    b->ev_taken.push_back(e1);
+  }
+  return 0;
+}
+
 /* After a sync of b->stream: report (and clear) a device-side abort. */
 int check_status(LPCNetBatch *b)
 {
@@ -1105,6 +1178,7 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
   (void)hipFree(b->d_stamps);
   (void)hipFree(b->d_lpc);
   (void)hipFree(b->d_lpc_tab);
+  (void)hipFree(b->d_chunk);
   for (int i = 0; i < 2; i++) {
     (void)hipFree(b->d_cond[i]);
     if (b->ev_frame[i]) (void)hipEventDestroy(b->ev_frame[i]);
@@ -1225,6 +1299,19 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
     HIPCHK(hipEventRecord(b->ev_start, b->stream));
     HIPCHK(hipStreamWaitEvent(b->fstream, b->ev_start, 0));
   }
+  /* chunked frame network: batches too large for the overlapped path (the
+   * sample kernels fill the GPU), matrix-core and fp32 sample kernels (the
+   * ones reading FrameCond) */
+  const bool chunked = !ovl && b->chunking && (b->mf || b->fp) && b->B > OVERLAP_MAX_STREAMS && !b->d_stamps &&
+                       !getenv("LPCNET_NO_CHUNK");
+  if (chunked && !b->d_chunk) {
+    HIPCHK(hipStreamSynchronize(b->stream));
+    if (hipMalloc(&b->d_chunk, sizeof(FrameCond) * (size_t)LPC_CHUNK * b->B) != hipSuccess) {
+      b->d_chunk = nullptr;
+      set_err("hipMalloc of the chunk conditioning buffer failed");
+      return -1;
+    }
+  }
   hipStream_t fs = ovl ? b->fstream : b->stream;
   for (int c0 = 0; c0 < nframes; c0 += LPC_CHUNK) {
     /* lpc_from_cepstrum depends only on the features: one launch for up to
@@ -1235,6 +1322,12 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
     if (launch_lpc(d_features + c0 * fstride, b->d_lpc, n * b->B, b->d_lpc_tab, fs)) {
       set_err("lpc kernel launch failed");
       return -1;
+    }
+    if (chunked && n >= CHUNK_MIN_FRAMES) {
+      if (launch_chunk_frames(b, d_features + c0 * fstride, n)) return -1;
+      for (int f = c0; f < c0 + n; f++)
+        if (launch_chunk_samples(b, f - c0, d_pcm + (size_t)f * b->B * N, N)) return -1;
+      continue;
     }
     for (int f = c0; f < c0 + n; f++)
       if (launch_frame_step(b, d_features + f * fstride, b->d_lpc + (size_t)(f - c0) * b->B * NLPC, false,
@@ -1249,6 +1342,13 @@ LPCNET_EXPORT int lpcnet_batch_sync(LPCNetBatch *b)
   if (!b || b->set_device()) return -1;
   HIPCHK(hipStreamSynchronize(b->stream));
   return check_status(b);
+}
+
+LPCNET_EXPORT int lpcnet_batch_set_frame_chunking(LPCNetBatch *b, int enable)
+{
+  if (!b) return -1;
+  b->chunking = enable != 0;
+  return 0;
 }
 
 LPCNET_EXPORT int lpcnet_batch_set_spin_limit(LPCNetBatch *b, int polls)

@@ -123,6 +123,10 @@ struct FrameArgs {
   const float *embed_pitch;
   const uint32_t *rcp; /* 2048-entry table in global memory */
   unsigned long long *stamps; /* optional diagnostics [grid][16] s_memtime per phase */
+  /* chunk_kernel only: features = [nframes][B][NF], lpc_new = [nframes][B][NLPC],
+   * outputs of frame f into cond[f * B .. f * B + B) */
+  int nframes;
+  FrameCond *cond;
 };
 
 struct SampleArgs {
@@ -210,13 +214,10 @@ int frame_groups(int nstreams);        /* frame kernel workgroups (stamp rows) f
 int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, void *stream);
 int launch_sample(const SampleArgs &a, int S, int variant, int sat, int reg, int lds_bytes, void *stream);
 
-/* Wave-per-stream sample kernel (int8 quad layout): nw streams per workgroup. */
-int wave_lds_bytes(int nw, int image_bytes);
-int launch_wave(const SampleArgs &a, int nw, int sat, int lds_bytes, void *stream);
-/* Pipelined int8 quad-layout kernel: the GRU_A recurrent product of sample
- * n+1 overlaps the sampling of sample n (fixed wave roles). */
-int pipe_lds_bytes(int S, int image_bytes);
-int launch_pipe(const SampleArgs &a, int S, int sat, int lds_bytes, void *stream);
+/* Frame network of up to LPC_CHUNK frames in one launch (chunk_kernel.hip):
+ * f32 matrix cores, 64 (stream, frame) columns per workgroup. */
+int launch_chunk(const FrameArgs &a, void *stream);
+constexpr int CHUNK_MIN_FRAMES = 4; /* shorter runs use the per-frame kernel */
 /* Matrix-core kernel (non-saturating int8 models within the MF_* limits):
  * GRU_A recurrent product on v_mfma_i32_4x4x4_16b_i8 in the GRU_A waves,
  * GRU_B products on v_mfma_i32_16x16x64_i8 in the sampler waves, two

@@ -349,6 +349,32 @@ def test_batch256_auto_kernel_matches_oracle(require_gpu, blobs):
     assert np.array_equal(got, np.stack(outs))
 
 
+@pytest.mark.parametrize("B,name", [(129, "streams_int8"), (256, "streams_int8"), (1024, "streams_int8"),
+                                    (200, "streams_fp32")])
+def test_chunked_frame_network_equals_per_frame(require_gpu, blobs, B, name):
+    """Above 128 streams lpcnet_batch_synthesize_frames runs the frame network
+    of up to 32 frames in one chunk_kernel launch (f32 matrix cores).  Runs of
+    37 frames (chunks of 32 and 5: both column layouts) then 3 frames (below
+    CHUNK_MIN_FRAMES: per-frame kernel) must give the PCM and the complete
+    stream state (conv memories, LPC ring, frame_count, conditioning, GRU
+    states, RNG) of the per-frame frame kernel, byte for byte, every stream."""
+    F = 40
+    blob = blobs[name]
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    outs, states = [], []
+    for chunking in (False, True):
+        b = L.LPCNetBatch(B, 0, blob)
+        b.set_frame_chunking(chunking)
+        got = np.concatenate([_frames(b, allf, 0, 37), _frames(b, allf, 37, F)], 0)
+        outs.append(got)
+        states.append([bytes(b.save_state(s)) for s in range(B)])
+        b.close()
+    assert np.abs(outs[0][2:].astype(np.float64)).mean() > 100
+    assert np.array_equal(outs[1], outs[0])
+    bad = [s for s in range(B) if states[1][s] != states[0][s]]
+    assert not bad, bad[:8]
+
+
 @pytest.mark.parametrize("B,name", [(1, "streams_int8"), (1, "streams_fp32"), (64, "streams_int8"),
                                     (300, "streams_int8")])
 def test_unsynced_frames_then_single_frame(require_gpu, blobs, B, name):
