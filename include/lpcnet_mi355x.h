@@ -163,12 +163,15 @@ LPCNET_EXPORT const uint32_t *lpcnet_mi355x_rcp_table(void);
 /* Device numerics self-test (diagnostics, not the synthesis path): runs one
  * routine of the kernels' arithmetic (lpcnet_amd/csrc/device_math.h) on GPU
  * `device` elementwise over n 32-bit inputs: op 0 tanh8_approx, 1
- * sigmoid8_approx (vec_avx.h:393-440, emulated rcpps), 2 / 3 the batched
- * forms of 0 / 1, 4 vector_ps_to_epi8 byte (vec_avx.h:321-336), 5 lin2ulaw
+ * sigmoid8_approx (vec_avx.h:393-440, rcpps from the table), 2 / 3 the
+ * batched forms of 0 / 1 with the hardware rcpps form, 4 vector_ps_to_epi8 byte (vec_avx.h:321-336), 5 lin2ulaw
  * (common.h:47-58), 6 floor(.5 + x) (lpcnet.c:266), 7 _mm256_cvtps_epi32;
  * op 8: n kiss99 draws (kiss99.c:59-81) from the 4-word state in[0..3];
  * op 9: the band power of lpc_from_cepstrum, (float)(pow(10, x) *
- * compensation[i % 18]) (freq.c:318, pow10_dd.h).
+ * compensation[i % 18]) (freq.c:318, pow10_dd.h); op 10 _mm256_rcp_ps of a
+ * Pade denominator (vec_avx.h:408,437, hardware form); op 11 / 12
+ * sigmoid8_approx of the int8 gates' inputs (|x| < 2^18, device_math.h
+ * sigmoid_x86_fin_n), hardware / table rcpps.
  * Returns 0, or -1 on bad arguments / HIP failure. */
 LPCNET_EXPORT int lpcnet_mi355x_device_numerics(int device, int op, const void *in, void *out, int n);
 /* Validate a weight blob with every rule lpcnet_load_model applies

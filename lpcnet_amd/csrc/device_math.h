@@ -34,8 +34,37 @@ __device__ __forceinline__ float clamp_x86(float v, float lo, float hi)
   return v != v ? v : __builtin_amdgcn_fmed3f(v, lo, hi);
 }
 
+/* rcpps of a Pade denominator in [2^9, 2^126), without the table: the x86
+ * entry for mantissa prefix i (11 bits) is 1/(1 + (i + 1/2)/2048) rounded to
+ * 12 significant bits (checked against every entry of tests/golden/
+ * rcp_x86.bin).  On gfx950, round12(v_rcp_f32(m)) with m = the prefix
+ * followed by 0x7FF and the rounding increment 0x3FF reproduces the table
+ * (times the exponent) for every prefix and every exponent of that range
+ * (tools/probes/rcp12_probe.hip, exhaustive; tests/test_gpu_numerics.py
+ * pins it).  Four VALU ops, no LDS read on the activation's critical path. */
+__device__ __forceinline__ float rcp12_hw(float den)
+{
+  const float m = __uint_as_float((__float_as_uint(den) & 0xFFFFF000u) | 0x7FFu);
+  return __uint_as_float((__float_as_uint(__builtin_amdgcn_rcpf(m)) + 0x3FFu) & 0xFFFFF800u);
+}
+
+/* the same for every Pade denominator: den >= 2^126 (rcpps result below
+ * 2^-126, flushed), +inf and NaN (sign bit set or not: the unsigned compare
+ * catches both) give +0, as rcp_x86_fix does */
+__device__ __forceinline__ float rcp_x86_hw(float den)
+{
+  return __float_as_uint(den) >= 0x7E800000u ? 0.f : rcp12_hw(den);
+}
+
+/* rcpps from the LDS table or (HW) from rcp_x86_hw.  The table costs an
+ * LDS read with bank conflicts (random index) and its latency; the hardware
+ * form costs a transcendental issue slot and three more VALU ops: HW wins on
+ * latency-bound chains (the samplers, one stream per lane), the table on
+ * VALU-throughput-bound ones (GRU_A elementwise over 2-4 streams per lane). */
+template <bool HW = false>
 __device__ __forceinline__ float rcp_x86(float x, const uint32_t *tab)
 {
+  if constexpr (HW) return rcp_x86_hw(x);
   /* _mm256_rcp_ps of a Pade denominator (its only use, tanh8_approx and
    * sigmoid8_approx): den = fma(fma(D2,X2,D1),X2,D0) with positive D's and
    * X2 = X*X lies in [952.72, +inf] or is NaN.  rcpps there is the
@@ -54,34 +83,41 @@ __device__ __forceinline__ float mm_min(float a, float b) { return a < b ? a : b
 __device__ __forceinline__ float mm_max(float a, float b) { return a > b ? a : b; }
 
 /* vec_avx.h:393-411 tanh8_approx */
+template <bool HW = false>
 __device__ __forceinline__ float tanh_x86(float X, const uint32_t *tab)
 {
   float X2 = X * X;
   float num = __builtin_fmaf(__builtin_fmaf(0.60863042f, X2, 96.39235687f), X2, 952.52801514f);
   float den = __builtin_fmaf(__builtin_fmaf(11.88600922f, X2, 413.36801147f), X2, 952.72399902f);
   num = num * X;
-  den = rcp_x86(den, tab);
+  den = rcp_x86<HW>(den, tab);
   num = num * den;
   return clamp_x86(num, -1.f, 1.f);
 }
 
 /* vec_avx.h:421-440 sigmoid8_approx */
+template <bool HW = false>
 __device__ __forceinline__ float sigmoid_x86(float X, const uint32_t *tab)
 {
   float X2 = X * X;
   float num = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
   float den = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
   num = num * X;
-  den = rcp_x86(den, tab);
+  den = rcp_x86<HW>(den, tab);
   num = __builtin_fmaf(num, den, 0.5f);
   return clamp_x86(num, 0.f, 1.f);
 }
 
 /* N independent rcp_x86: all N table reads are issued before any is pinned,
  * so their LDS latencies overlap (rcp_x86's pin alone serialises a chain). */
-template <int N>
+template <int N, bool HW = false>
 __device__ __forceinline__ void rcp_x86_n(float (&x)[N], const uint32_t *tab)
 {
+  if constexpr (HW) {
+#pragma unroll
+    for (int k = 0; k < N; k++) x[k] = rcp_x86_hw(x[k]);
+    return;
+  }
   uint32_t t[N];
 #pragma unroll
   for (int k = 0; k < N; k++) t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(x[k]), 12, 11)];
@@ -93,7 +129,7 @@ __device__ __forceinline__ void rcp_x86_n(float (&x)[N], const uint32_t *tab)
 
 /* N sigmoid8_approx / tanh8_approx lanes with one batched rcp (same
  * arithmetic as sigmoid_x86 / tanh_x86, term for term) */
-template <int N>
+template <int N, bool HW = false>
 __device__ __forceinline__ void sigmoid_x86_n(float (&X)[N], const uint32_t *tab)
 {
   float num[N], den[N];
@@ -104,7 +140,7 @@ __device__ __forceinline__ void sigmoid_x86_n(float (&X)[N], const uint32_t *tab
     den[k] = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
     num[k] = num[k] * X[k];
   }
-  rcp_x86_n<N>(den, tab);
+  rcp_x86_n<N, HW>(den, tab);
 #pragma unroll
   for (int k = 0; k < N; k++) X[k] = clamp_x86(__builtin_fmaf(num[k], den[k], 0.5f), 0.f, 1.f);
 }
@@ -116,10 +152,22 @@ __device__ __forceinline__ void sigmoid_x86_n(float (&X)[N], const uint32_t *tab
  * rcp_x86_fix) and no NaN can arise, so the result is rcp_x86 / clamp_x86
  * without the flush select and the NaN select: identical to sigmoid_x86_n
  * for every such input.  Used for the int8 products' z / r gates. */
-template <int N>
+template <int N, bool HW = false>
 __device__ __forceinline__ void sigmoid_x86_fin_n(float (&X)[N], const uint32_t *tab)
 {
   float num[N], den[N];
+  if constexpr (HW) {
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      const float X2 = X[k] * X[k];
+      num[k] = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
+      den[k] = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
+      num[k] = num[k] * X[k];
+    }
+#pragma unroll
+    for (int k = 0; k < N; k++) X[k] = __builtin_amdgcn_fmed3f(__builtin_fmaf(num[k], rcp12_hw(den[k]), 0.5f), 0.f, 1.f);
+    return;
+  }
   uint32_t t[N];
 #pragma unroll
   for (int k = 0; k < N; k++) {
@@ -138,7 +186,7 @@ __device__ __forceinline__ void sigmoid_x86_fin_n(float (&X)[N], const uint32_t 
   }
 }
 
-template <int N>
+template <int N, bool HW = false>
 __device__ __forceinline__ void tanh_x86_n(float (&X)[N], const uint32_t *tab)
 {
   float num[N], den[N];
@@ -149,7 +197,7 @@ __device__ __forceinline__ void tanh_x86_n(float (&X)[N], const uint32_t *tab)
     den[k] = __builtin_fmaf(__builtin_fmaf(11.88600922f, X2, 413.36801147f), X2, 952.72399902f);
     num[k] = num[k] * X[k];
   }
-  rcp_x86_n<N>(den, tab);
+  rcp_x86_n<N, HW>(den, tab);
 #pragma unroll
   for (int k = 0; k < N; k++) X[k] = clamp_x86(num[k] * den[k], -1.f, 1.f);
 }

@@ -390,6 +390,128 @@ void choose_kernel(LPCNetBatch *b)
  * passes (the SampleArgs are built locally and committed at the end), so a
  * failed reload leaves either the previous model intact or, after the old
  * buffers were freed, no model at all (have_model false). */
+/* mf_kernel GRU_A layout helpers (host side, deterministic).
+ *
+ * Unit blocks (8 units = one block row of each gate) are dealt to the six
+ * GRU_A waves.  A wave runs as many 4x4x4 MFMA slots per gate as its
+ * longest block row has blocks (rounded up to 4), so the assignment
+ * decides both the padding and the balance between the two waves sharing
+ * each SIMD (w, w+4; waves 2 and 3 share theirs with the samplers). */
+static int mf_wave_cost(const std::vector<std::vector<int>> &ga, const int *ub8)
+{
+  size_t mz = 0, mh = 0;
+  for (int j = 0; j < 8; j++) {
+    mz = std::max(mz, std::max(ga[ub8[j]].size(), ga[NA / 8 + ub8[j]].size()));
+    mh = std::max(mh, ga[2 * (NA / 8) + ub8[j]].size());
+  }
+  return 8 * (int)((mz + 3) / 4) + 4 * (int)((mh + 3) / 4);
+}
+
+static std::vector<int> mf_assign_unit_blocks(const std::vector<std::vector<int>> &ga)
+{
+  constexpr int NUB = NA / 8;
+  std::vector<int> perm(NUB);
+  /* start: unit blocks by descending z/r length, dealt in order */
+  for (int u = 0; u < NUB; u++) perm[u] = u;
+  auto zr = [&](int u) { return std::max(ga[u].size(), ga[NUB + u].size()); };
+  std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return zr(a) > zr(b); });
+  auto score = [&](const std::vector<int> &p, long &sum) {
+    int c[SAMPLE_WAVES];
+    sum = 0;
+    for (int w = 0; w < SAMPLE_WAVES; w++) sum += (c[w] = mf_wave_cost(ga, &p[8 * w]));
+    /* per-SIMD load: waves 0/4 and 1/5 pair up; 2 and 3 pair with a sampler */
+    return std::max(std::max(c[0] + c[4], c[1] + c[5]), 2 * std::max(c[2], c[3]));
+  };
+  long best_sum;
+  int best = score(perm, best_sum);
+  uint32_t rng = 12345u;
+  for (int it = 0; it < 40000; it++) {
+    rng = rng * 1664525u + 1013904223u;
+    const int a = (rng >> 8) % NUB;
+    rng = rng * 1664525u + 1013904223u;
+    const int b = (rng >> 8) % NUB;
+    if (a / 8 == b / 8) continue;
+    std::swap(perm[a], perm[b]);
+    long sum;
+    const int sc = score(perm, sum);
+    if (sc < best || (sc == best && sum <= best_sum)) {
+      best = sc;
+      best_sum = sum;
+    } else {
+      std::swap(perm[a], perm[b]);
+    }
+  }
+  return perm;
+}
+
+/* Slot order of the 4 block rows one 32-lane LDS group reads in the same
+ * ds_read_b32 (rows4[k]: input offsets of row k's blocks).  Input quad c of
+ * stream m sits at dword c + 104 m, bank (c + 8 m) mod 32: quads of
+ * different c mod 8 never share a bank, equal quads broadcast.  Each row's
+ * blocks are matched to slots (Kuhn augmenting paths) so that every slot's
+ * quads are bank-disjoint; blocks that cannot be placed so take any free
+ * slot.  Empty positions (zero weights) read a quad another row reads in
+ * that slot.  Integer sums do not depend on the order. */
+static void mf_bank_slots(const std::vector<int> *const rows4[4], int nslot, int slot_of[4][MF_HMAX], int cb_at[4][MF_HMAX])
+{
+  int owner[4][MF_HMAX];
+  int cls[MF_HMAX][8];
+  for (int t = 0; t < MF_HMAX; t++)
+    for (int c = 0; c < 8; c++) cls[t][c] = -1;
+  for (int k = 0; k < 4; k++)
+    for (int t = 0; t < MF_HMAX; t++) owner[k][t] = -1;
+  int order[4] = {0, 1, 2, 3};
+  std::stable_sort(order, order + 4, [&](int a, int b) { return rows4[a]->size() > rows4[b]->size(); });
+  for (int oi = 0; oi < 4; oi++) {
+    const int k = order[oi];
+    const std::vector<int> &row = *rows4[k];
+    const int n = (int)row.size();
+    auto ok = [&](int i, int t) {
+      const int cb = row[i] / 4, c = cb & 7;
+      return cls[t][c] < 0 || cls[t][c] == cb;
+    };
+    int match_slot[MF_HMAX];  /* slot -> item of this row */
+    for (int t = 0; t < nslot; t++) match_slot[t] = -1;
+    std::vector<int> item_slot(n, -1);
+    for (int i = 0; i < n; i++) {
+      bool seen[MF_HMAX] = {};
+      std::function<bool(int)> aug = [&](int it) -> bool {
+        for (int t = 0; t < nslot; t++) {
+          if (seen[t] || !ok(it, t)) continue;
+          seen[t] = true;
+          if (match_slot[t] < 0 || aug(match_slot[t])) {
+            match_slot[t] = it;
+            item_slot[it] = t;
+            return true;
+          }
+        }
+        return false;
+      };
+      aug(i);
+    }
+    for (int i = 0; i < n; i++)
+      if (item_slot[i] < 0)
+        for (int t = 0; t < nslot; t++)
+          if (match_slot[t] < 0) {
+            match_slot[t] = i;
+            item_slot[i] = t;
+            break;
+          }
+    for (int i = 0; i < n; i++) {
+      const int t = item_slot[i], cb = row[i] / 4;
+      slot_of[k][i] = t;
+      owner[k][t] = cb;
+      if (cls[t][cb & 7] < 0) cls[t][cb & 7] = cb;
+    }
+  }
+  for (int t = 0; t < nslot; t++) {
+    int any = 0;
+    for (int k = 0; k < 4; k++)
+      if (owner[k][t] >= 0) { any = owner[k][t]; break; }
+    for (int k = 0; k < 4; k++) cb_at[k][t] = owner[k][t] >= 0 ? owner[k][t] : any;
+  }
+}
+
 int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload = true)
 {
   std::vector<Arr> L;
@@ -632,26 +754,44 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
           (int)ga_blocks[2 * (NA / 8) + w * 8 + j].size() > MF_HMAX)
         mf_ok = false;
     }
+  std::vector<int> mf_units;
   if (mf_ok) {
     const int8_t *wa = (const int8_t *)gaw->data, *wb = (const int8_t *)gbw, *wr = (const int8_t *)gbrec;
-    /* GRU_A: lane l of wave w = unit 64w + l, row l%8 of row block 8w + l/8 of each gate */
+    /* GRU_A: lane l of wave w = row l%8 of unit block perm[8w + l/8] of each
+     * gate (units 8 perm[.] .. +7); D row of that lane = that unit */
+    const std::vector<int> perm = mf_assign_unit_blocks(ga_blocks);
     mft.assign((size_t)SAMPLE_WAVES * MF_LANE_U32 * 64, 0);
+    mf_units.assign((size_t)SAMPLE_WAVES * 64, 0);
     for (int w = 0; w < SAMPLE_WAVES; w++) {
       auto word = [&](int k, int l) -> uint32_t & { return mft[((size_t)w * MF_LANE_U32 + k) * 64 + l]; };
       int kz = 0, kh = 0;
       for (int j = 0; j < 8; j++) {
-        kz = std::max(kz, (int)std::max(ga_blocks[w * 8 + j].size(), ga_blocks[NA / 8 + w * 8 + j].size()));
-        kh = std::max(kh, (int)ga_blocks[2 * (NA / 8) + w * 8 + j].size());
+        const int ub = perm[w * 8 + j];
+        kz = std::max(kz, (int)std::max(ga_blocks[ub].size(), ga_blocks[NA / 8 + ub].size()));
+        kh = std::max(kh, (int)ga_blocks[2 * (NA / 8) + ub].size());
       }
       sa.mf_nzr[w] = (kz + 3) / 4;
       sa.mf_nh[w] = (kh + 3) / 4;
-      for (int l = 0; l < 64; l++) {
-        const int j = l >> 3, r = l & 7;
-        for (int g = 0; g < 3; g++) {
-          const int rb = g * (NA / 8) + w * 8 + j, base = g == 0 ? 0 : (g == 1 ? MF_ZMAX : 2 * MF_ZMAX);
-          for (int t = 0; t < (int)ga_blocks[rb].size(); t++) {
-            memcpy(&word(base + t, l), wa + 32 * (ga_first[rb] + t) + 4 * r, 4);
-            word(MF_GA + (base + t) / 4, l) |= (uint32_t)(ga_blocks[rb][t] / 4) << (8 * ((base + t) & 3));
+      for (int l = 0; l < 64; l++) mf_units[w * 64 + l] = 8 * perm[w * 8 + (l >> 3)] + (l & 7);
+      for (int g = 0; g < 3; g++) {
+        const int base = g == 0 ? 0 : (g == 1 ? MF_ZMAX : 2 * MF_ZMAX);
+        const int nslot = 4 * (g < 2 ? sa.mf_nzr[w] : sa.mf_nh[w]);
+        for (int half = 0; half < 2; half++) {
+          /* the 4 block rows read by one 32-lane LDS group: slot order
+           * chosen so their x words fall in distinct banks (mf_bank_slots) */
+          const std::vector<int> *rows4[4];
+          for (int k = 0; k < 4; k++) rows4[k] = &ga_blocks[g * (NA / 8) + perm[w * 8 + 4 * half + k]];
+          int slot_of[4][MF_HMAX], cb_at[4][MF_HMAX];
+          mf_bank_slots(rows4, nslot, slot_of, cb_at);
+          for (int k = 0; k < 4; k++) {
+            const int j = 4 * half + k, ub = perm[w * 8 + j], rb = g * (NA / 8) + ub;
+            for (int r = 0; r < 8; r++) {
+              const int l = 8 * j + r;
+              for (int t = 0; t < (int)ga_blocks[rb].size(); t++)
+                memcpy(&word(base + slot_of[k][t], l), wa + 32 * (ga_first[rb] + t) + 4 * r, 4);
+              for (int t = 0; t < nslot; t++)
+                word(MF_GA + (base + t) / 4, l) |= (uint32_t)cb_at[k][t] << (8 * ((base + t) & 3));
+            }
           }
         }
       }
@@ -808,6 +948,20 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   UP(sa.image, img.data(), img.size());
   if (mf_ok) {
     UP(sa.mf, mft.data(), mft.size() * 4);
+    UP(sa.mf_unit, mf_units.data(), mf_units.size() * 4);
+    {
+      /* embedding tables with their columns in lane order (coalesced gathers) */
+      std::vector<float> pt((size_t)256 * GA_ROWS);
+      const float *src[3] = {emb_sig, emb_pred, emb_exc};
+      for (int t = 0; t < 3; t++) {
+        for (int row = 0; row < 256; row++)
+          for (int g = 0; g < 3; g++)
+            for (int p = 0; p < NA; p++) pt[(size_t)row * GA_ROWS + g * NA + p] = src[t][(size_t)row * GA_ROWS + g * NA + mf_units[p]];
+        const float *d = nullptr;
+        UP(d, pt.data(), pt.size() * 4);
+        sa.mf_emb[t] = d;
+      }
+    }
     UP(sa.mf_gb, mfgb.data(), mfgb.size() * 4);
   }
   if (fp_ok) {

@@ -174,7 +174,10 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
   short *pcmbuf = (short *)((unsigned char *)sync + L::sync);
   unsigned char *img = lds + L::total;
 
-  if (l2_warm_role(A, A.nstreams)) return;
+  {
+    const float *const fp_tabs[3] = {A.emb_sig, A.emb_pred, A.emb_exc};
+    if (l2_warm_role(fp_tabs, A.nstreams)) return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int sid = blockIdx.x;
   const uint32_t *rcp = (const uint32_t *)(img + IMG_RCP);
@@ -317,9 +320,9 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
       stamp(2);
       /* compute_sparse_gru elementwise (nnet.c:442-447) */
       float zr2[2] = {acc.x, acc.y};
-      sigmoid_x86_n<2>(zr2, rcp);
+      sigmoid_x86_n<2, true>(zr2, rcp);
       float hv[1] = {hpre * zr2[1] + inh};
-      tanh_x86_n<1>(hv, rcp);
+      tanh_x86_n<1, true>(hv, rcp);
       st = zr2[0] * st + (1.f - zr2[0]) * hv[0];
       ((float *)xn)[i] = st;
       if (lane == 0) flag_publish(done + g, n + 1);
@@ -394,7 +397,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
 #pragma unroll
       for (int j = NLPC - 1; j > 0; j--) lsr[j] = lsr[j - 1];
       lsr[0] = pend_pcm;
-      last_exc = pend_exc;
+        last_exc = pend_exc;
       pred = pend_pred;
       float o = pend_pcm + kPreemph * deemph;
       deemph = o;
@@ -461,9 +464,9 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
         const float hin = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(y), __float_as_uint(y), false, false)[1]);
         const float hrec = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(y2), __float_as_uint(y2), false, false)[1]);
         float zr2[2] = {zin, rin};
-        sigmoid_x86_n<2>(zr2, rcp);
+        sigmoid_x86_n<2, true>(zr2, rcp);
         float hh[1] = {hin + hrec * zr2[1]};
-        tanh_x86_n<1>(hh, rcp);
+        tanh_x86_n<1, true>(hh, rcp);
         sbv = zr2[0] * sbv + (1.f - zr2[0]) * hh[0];
         if (lane < NB) sbuf[lane] = sbv;
       }

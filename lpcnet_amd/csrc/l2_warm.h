@@ -26,7 +26,7 @@ constexpr int WARM_SLICES = 8;
 inline int warm_grid(int groups, int nstreams) { return nstreams == 1 ? groups + 8 * WARM_SLICES : groups; }
 
 /* true: this workgroup is a warmer (or idle) and has done its part */
-__device__ __forceinline__ bool l2_warm_role(const SampleArgs &A, int groups)
+__device__ __forceinline__ bool l2_warm_role(const float *const tabs[3], int groups)
 {
   if ((int)blockIdx.x < groups) return false;
   if (blockIdx.x % 8 != 0) return true;
@@ -34,7 +34,7 @@ __device__ __forceinline__ bool l2_warm_role(const SampleArgs &A, int groups)
   constexpr int per_table = 256 * GA_ROWS / 4; /* float4 */
   uint32_t acc = 0;
   for (int t = 0; t < 3; t++) {
-    const uint4 *p = (const uint4 *)(t == 0 ? A.emb_sig : (t == 1 ? A.emb_pred : A.emb_exc));
+    const uint4 *p = (const uint4 *)tabs[t];
     for (int o = slice * blockDim.x + threadIdx.x; o < per_table; o += nsl * blockDim.x) {
       const uint4 v = p[o];
       acc ^= v.x ^ v.y ^ v.z ^ v.w;

@@ -46,8 +46,11 @@ constexpr int MF_ZMAX = 16;         /* z / r slots per lane */
 constexpr int MF_HMAX = 32;         /* h slots per lane */
 constexpr int MF_GA = 2 * MF_ZMAX + MF_HMAX;
 constexpr int MF_LANE_U32 = MF_GA + MF_GA / 4; /* 80 */
-constexpr int MF_GB_TILES = 3 * 6 + 3;
-constexpr int MF_XSTR = 400;        /* LDS bytes per stream of the quantized GRU_A state (stream-major) */
+constexpr int MF_GB_IN = 3 * 6;                 /* GRU_B input tiles (3 gates x 6 K tiles) */
+constexpr int MF_GB_TILES = MF_GB_IN + 3;        /* + the 3 recurrent tiles */
+constexpr int MF_XSTR = 416;        /* LDS bytes per stream of the quantized GRU_A state (stream-major):
+                                       104 dwords = 8 banks (mod 32) apart, so the 4 streams of
+                                       input quad c occupy banks c + {0, 8, 16, 24} (mod 32) */
 constexpr int MF_THREADS = 512;     /* 6 GRU_A waves + 2 sampler waves */
 /* fp32 latency kernel (fp_kernel.hip), one stream per workgroup.
  * GRU_A per-lane tables (lane l of wave w = unit 64w + l = row l%8 of row
@@ -160,6 +163,9 @@ struct SampleArgs {
    * lanes], 4-slot groups per wave (z/r padded to a common count, h); GRU_B
    * A tiles [MF_GB_TILES][64] */
   const uint32_t *mf;
+  const int *mf_unit;                /* [SAMPLE_WAVES * 64]: GRU_A unit of each lane */
+  const float *mf_emb[3];            /* sig/pred/exc tables with columns in lane order:
+                                        [256][3][SAMPLE_WAVES * 64], column p = unit mf_unit[p] */
   int mf_nzr[SAMPLE_WAVES];
   int mf_nh[SAMPLE_WAVES];
   const uint4 *mf_gb;

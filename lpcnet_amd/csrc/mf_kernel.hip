@@ -68,10 +68,13 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   int *gbr = gbs + S * GB_ROWS;
   unsigned char *img = lds + L::total; /* fixed image sections: tables and dual_fc */
 
-  if (l2_warm_role(A, (A.nstreams + S - 1) / S)) return;
+  if (l2_warm_role(A.mf_emb, (A.nstreams + S - 1) / S)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = blockIdx.x * S;
   const uint32_t *rcp = (const uint32_t *)(img + IMG_RCP);
+  /* GRU_A elementwise: one stream per lane is latency-bound (hardware rcp),
+   * 2-4 streams per lane are VALU-bound (LDS table) */
+  constexpr bool kHwA = S == 1;
 
   bool active[S];
   bool any = false;
@@ -112,7 +115,9 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
 
   if (wv < SAMPLE_WAVES) {
     /* ======================= GRU_A role ================================== */
-    const int i = tid;
+    /* this lane's GRU_A unit (the host deals 8-unit blocks to the waves for
+     * MFMA balance); the embedding tables' columns are stored in lane order */
+    const int i = A.mf_unit[tid];
     const float bz = A.ga_par[i], br = A.ga_par[NA + i], bh = A.ga_par[2 * NA + i];
     const float dz = A.ga_par[3 * NA + i], dr = A.ga_par[4 * NA + i], dh = A.ga_par[5 * NA + i];
     const int wsz = A.ga_wsum[i], wsr = A.ga_wsum[NA + i], wsh = A.ga_wsum[2 * NA + i];
@@ -201,14 +206,14 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         for (int s = 0; s < S; s++) {
           /* the indices are the same in every lane: scalar row addresses */
           const int4 v = *(const int4 *)(ix + s * 4);
-          const float *e1 = A.emb_sig + (__builtin_amdgcn_readfirstlane(v.x) & 0xFF) * GA_ROWS;
-          const float *e2 = A.emb_pred + (__builtin_amdgcn_readfirstlane(v.y) & 0xFF) * GA_ROWS;
-          const float *e3 = A.emb_exc + (__builtin_amdgcn_readfirstlane(v.z) & 0xFF) * GA_ROWS;
+          const float *e1 = A.mf_emb[0] + (__builtin_amdgcn_readfirstlane(v.x) & 0xFF) * GA_ROWS;
+          const float *e2 = A.mf_emb[1] + (__builtin_amdgcn_readfirstlane(v.y) & 0xFF) * GA_ROWS;
+          const float *e3 = A.mf_emb[2] + (__builtin_amdgcn_readfirstlane(v.z) & 0xFF) * GA_ROWS;
 #pragma unroll
           for (int g = 0; g < 3; g++) {
-            e[s][g] = e1[g * NA + i];
-            e[s][3 + g] = e2[g * NA + i];
-            e[s][6 + g] = e3[g * NA + i];
+            e[s][g] = e1[g * NA + tid];
+            e[s][3 + g] = e2[g * NA + tid];
+            e[s][6 + g] = e3[g * NA + tid];
           }
         }
         if (stamping) {
@@ -237,12 +242,12 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
 #ifdef MF_FINE
         if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(11); }
 #endif
-        sigmoid_x86_fin_n<2 * S>(zrv, rcp);
+        sigmoid_x86_fin_n<2 * S, kHwA>(zrv, rcp);
 #ifdef MF_FINE
         if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(12); }
 #endif
         for (int s = 0; s < S; s++) hv[s] = hv[s] * zrv[S + s] + inh[s];
-        tanh_x86_n<S>(hv, rcp);
+        tanh_x86_n<S, kHwA>(hv, rcp);
         for (int s = 0; s < S; s++) st[s] = zrv[s] * st[s] + (1.f - zrv[s]) * hv[s];
 #ifdef MF_FINE
         if (stamping) { float g = 0.f; for (int k = 0; k < S; k++) g += st[k]; asm volatile("" ::"v"(g)); stamp(13); }
@@ -332,7 +337,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
 #pragma unroll
       for (int j = NLPC - 1; j > 0; j--) lsr[j] = lsr[j - 1];
       lsr[0] = pend_pcm;
-      last_exc = pend_exc;
+        last_exc = pend_exc;
       pred = pend_pred;
       float o = pend_pcm + kPreemph * deemph;
       deemph = o;
@@ -363,7 +368,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
           accr[g] = *(const v4i *)(gbr + 16 * g + 4 * gq);
         }
 #pragma unroll
-        for (int g = 0; g < 3; g++) accr[g] = mfma16(wt[18 + g], xr, accr[g]);
+        for (int g = 0; g < 3; g++) accr[g] = mfma16(wt[MF_GB_IN + g], xr, accr[g]);
       }
       stamp(0);
       __syncthreads(); /* Y */
@@ -385,10 +390,10 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         /* GRU_B elementwise (nnet.c:362-371), unit gu of stream sl */
         float zrb[2] = {(float)pick(acc[0]) * kScale1 + (float)pick(accr[0]) * kScale1,
                         (float)pick(acc[1]) * kScale1 + (float)pick(accr[1]) * kScale1};
-        sigmoid_x86_fin_n<2>(zrb, rcp);
+        sigmoid_x86_fin_n<2, true>(zrb, rcp);
         float hh[1] = {(float)pick(acc[2]) * kScale1 + ((float)pick(accr[2]) * kScale1) * zrb[1]};
         stamp(14);
-        tanh_x86_n<1>(hh, rcp);
+        tanh_x86_n<1, true>(hh, rcp);
         sbv = zrb[0] * sbv + (1.f - zrb[0]) * hh[0];
         if (gown) sbuf[gs * NB + gu] = sbv;
       }

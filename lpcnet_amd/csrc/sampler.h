@@ -51,8 +51,14 @@ struct FcLane {
     float sum = bias;
 #pragma unroll
     for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
+    return node_logit_tail(sum, factor);
+  }
+
+  /* the same from the finished dot product sum */
+  __device__ __forceinline__ float node_logit_tail(float sum, float factor) const
+  {
     float v[1] = {sum};
-    tanh_x86_n<1>(v, rcp);
+    tanh_x86_n<1, true>(v, rcp);
     const float vv = factor * v[0];
     const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(vv), 0xB1, 0xF, 0xF, false));
     return ch2 ? o + vv : vv + o;
@@ -79,38 +85,74 @@ __device__ __forceinline__ void lane_thresholds(const FcLane &F, const float *lo
   t47 = logit_tab[(r1 >> (8 * F.lvl_in)) & 0xFF];
 }
 
-/* One sample of stream (half): t03/t47 = this lane's thresholds
- * (lane_thresholds), xv = GRU_B state, pred = pred(n), lsr/lpr = LPC
- * history and coefficients.  teach != nullptr: teacher forcing with input
- * *teach (lpcnet.c:256-259).  Uniform per half.  TRACE: also return the
- * 8 logits along the path. */
+/* Decisions of one 4-level tree round from the lane's half of the ballot
+ * (bit 2q = the q-th node of the round, both channel lanes of a node vote
+ * alike): level b's node sits at lane pair (1 << b) - 1 + (the b bits
+ * decided so far).  Three dependent 32-bit ops per level. */
+__device__ __forceinline__ int walk_round(uint32_t m)
+{
+  int v = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++) v = (v << 1) | (int)__builtin_amdgcn_ubfe(m, 2 * v + 2 * ((1 << b) - 1), 1);
+  return v;
+}
+
+/* this lane's half of a wave ballot */
+__device__ __forceinline__ uint32_t half_bits(unsigned long long m, int half)
+{
+  return half ? (uint32_t)(m >> 32) : (uint32_t)m;
+}
+
+#ifndef WALK_INTERLEAVE
+#define WALK_INTERLEAVE 1
+#endif
+
 /* phase-stamp hook of dual_fc_walk (diagnostic builds: mf_kernel -DMF_WALKFINE) */
 struct WalkNoStamp {
   __device__ __forceinline__ void operator()(int, float) const {}
 };
 
+/* One sample of stream (half): t03/t47 = this lane's thresholds
+ * (lane_thresholds), xv = GRU_B state, pred = pred(n), lsr/lpr = LPC
+ * history and coefficients.  teach != nullptr:
+ * teacher forcing with input *teach (lpcnet.c:256-259).  Uniform per half.
+ * TRACE: also return the 8 logits along the path.
+ *
+ * Critical-path shape: round 1 (levels 0..3, all 15 nodes at once) ->
+ * decisions -> round 2 (levels 4..7 under the prefix) with the 16
+ * candidates' outputs computed beside it -> decisions -> one lane select.
+ * Lanes hl and hl + 16 hold the same candidate c = hl & 15; the low 16
+ * convert its output sample to u-law, the high 16 its pred(n+1), so one
+ * lin2ulaw serves both indices. */
 template <bool TRACE, class ST = WalkNoStamp>
 __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, float t47, const float (&xv)[NB], float pred,
                                                 const float (&lsr)[NLPC], const float (&lpr)[NLPC], const short *teach,
                                                 float deemph, ST st = ST())
 {
   WalkOut R;
-  int val = 0;
+  /* the candidate-independent products of pred(n+1) (lpcnet.c:252 after the
+   * history shift), issued beside round 1's dependent chain: the reference
+   * multiplies and subtracts separately (no FMA), so a product computed
+   * ahead is the same float */
+  float lprod[NLPC];
+#pragma unroll
+  for (int j = 1; j < NLPC; j++) lprod[j] = lsr[j - 1] * lpr[j];
+  int val;
   {
     const float l = F.node_logit(F.b03, F.f03, F.w03, xv);
     st(2, l);
-    const unsigned long long m = __ballot(t03 < l) >> F.hb;
+    val = walk_round(half_bits(__ballot(t03 < l), F.half));
+    if (TRACE) {
+      int v = 0;
 #pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const int nd = (1 << b) | val;
-      if (TRACE) R.lg[b] = __shfl(l, F.hb + 2 * (nd - 1));
-      val = (val << 1) | (int)((m >> (2 * (nd - 1))) & 1ull);
+      for (int b = 0; b < 4; b++) {
+        const int nd = (1 << b) | v;
+        R.lg[b] = __shfl(l, F.hb + 2 * (nd - 1));
+        v = (v << 1) | ((val >> (3 - b)) & 1);
+      }
     }
   }
-  /* level 4..7 node of this lane under the chosen prefix: its parameters
-   * are loaded first, so their LDS latency overlaps the speculation below
-   * (one basic block: the speculation is computed unconditionally and simply
-   * unused when teaching, a branch would serialise the two) */
+  /* level 4..7 node of this lane under the chosen prefix */
   const int lvl = 4 + F.lvl_in;
   const int node = (1 << lvl) | (val << (lvl - 4)) | (F.qq + 1 - (1 << (lvl - 4)));
   const float b47 = F.fcb[F.ch2 * 256 + node], f47 = F.fcf[F.ch2 * 256 + node];
@@ -124,45 +166,71 @@ __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, floa
     }
   }
   st(3, w47[NB - 1] + b47 + f47);
-  /* candidate exc = 16*prefix + (hl & 15): output sample, pred(n+1), u-law
-   * indices (lpcnet.c:252-261), the reference's operations in order */
+  /* candidate exc = 16*prefix + (hl & 15): output sample, pred(n+1) and one
+   * u-law index (lpcnet.c:252-261), the reference's operations in order.
+   * Its subtraction chain is pinned step for step beside round 2's dot
+   * chain (two independent dependency chains interleaved); left to the
+   * scheduler it runs before the w47 loads are even issued. */
   const float sp_pcm = pred + F.ulaw[(val << 4) | (F.hl & 15)];
   float p2 = 0.f - sp_pcm * lpr[0];
+#if WALK_INTERLEAVE
+  float sum = b47;
 #pragma unroll
-  for (int j = 1; j < NLPC; j++) p2 = p2 - lsr[j - 1] * lpr[j];
-  const float sp_pred = p2;
-  const int sp_idx = lin2ulaw_x86(sp_pcm) | (lin2ulaw_x86(sp_pred) << 8);
+  for (int j = 0; j < NB; j++) {
+    sum = sum + w47[j] * xv[j];
+    if (j > 0) p2 = p2 - lprod[j];
+    asm volatile("" : "+v"(sum), "+v"(p2));
+  }
+#else
+  float sum = b47;
+#pragma unroll
+  for (int j = 0; j < NB; j++) sum = sum + w47[j] * xv[j];
+#pragma unroll
+  for (int j = 1; j < NLPC; j++) p2 = p2 - lprod[j];
+#endif
+  float sp_pred = p2;
+  int sp_u = lin2ulaw_x86(F.hl < 16 ? sp_pcm : sp_pred);
+  int low;
   {
-    const float l = F.node_logit(b47, f47, w47, xv);
+    const float l = F.node_logit_tail(sum, f47);
     st(15, l);
-    const unsigned long long m = __ballot(t47 < l) >> F.hb;
+    /* the speculation is needed only when not teaching: pin it before the
+     * ballot, or the compiler sinks it into that branch, after the round */
+    asm volatile("" : "+v"(sp_u), "+v"(sp_pred));
+    low = walk_round(half_bits(__ballot(t47 < l), F.half));
+    if (TRACE) {
+      const int s = low;
+      int v = 0;
 #pragma unroll
-    for (int b = 4; b < 8; b++) {
-      const int qi = (1 << (b - 4)) - 1 + (val & ((1 << (b - 4)) - 1));
-      if (TRACE) R.lg[b] = __shfl(l, F.hb + 2 * qi);
-      val = (val << 1) | (int)((m >> (2 * qi)) & 1ull);
+      for (int b = 0; b < 4; b++) {
+        R.lg[4 + b] = __shfl(l, F.hb + 2 * ((1 << b) - 1 + v));
+        v = (v << 1) | ((s >> (3 - b)) & 1);
+      }
     }
   }
-  R.exc = val;
+  R.exc = (val << 4) | low;
   if (teach != nullptr) {
     /* teacher forcing (lpcnet.c:256-259) */
     const float o_in = (float)*teach;
     const float pd = kPreemph * deemph;
     R.exc = lin2ulaw_x86((o_in - pd) - pred);
     R.pcm = o_in - pd;
-    float p2 = 0.f - R.pcm * lpr[0];
+    float q = 0.f - R.pcm * lpr[0];
 #pragma unroll
-    for (int j = 1; j < NLPC; j++) p2 = p2 - lsr[j - 1] * lpr[j];
-    R.pn = p2;
+    for (int j = 1; j < NLPC; j++) q = q - lprod[j];
+    R.pn = q;
     R.su = lin2ulaw_x86(R.pcm);
     R.pu = lin2ulaw_x86(R.pn);
   } else {
-    const int src = F.hb + (R.exc & 15);
-    const int ic = __shfl(sp_idx, src);
+    /* the chosen candidate's lane hb + low: its u-law pair (the pred
+     * index comes over from lane + 16), output sample and pred(n+1) */
+    const int pu = (int)__builtin_amdgcn_permlane16_swap((uint32_t)sp_u, (uint32_t)sp_u, false, false)[1];
+    const int src = (F.hb + low) << 2;
+    const int ic = __builtin_amdgcn_ds_bpermute(src, sp_u | (pu << 8));
     R.su = ic & 0xFF;
     R.pu = ic >> 8;
-    R.pcm = __shfl(sp_pcm, src);
-    R.pn = __shfl(sp_pred, src);
+    R.pcm = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(sp_pcm)));
+    R.pn = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(sp_pred)));
   }
   return R;
 }

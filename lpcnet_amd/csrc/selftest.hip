@@ -40,13 +40,13 @@ __global__ void numerics_kernel(int op, const uint32_t *__restrict__ in, uint32_
     case 1: out[e] = __float_as_uint(sigmoid_x86(x, rcp)); break;
     case 2: {
       float v[1] = {x};
-      tanh_x86_n<1>(v, rcp);
+      tanh_x86_n<1, true>(v, rcp);
       out[e] = __float_as_uint(v[0]);
       break;
     }
     case 3: {
       float v[1] = {x};
-      sigmoid_x86_n<1>(v, rcp);
+      sigmoid_x86_n<1, true>(v, rcp);
       out[e] = __float_as_uint(v[0]);
       break;
     }
@@ -61,6 +61,20 @@ __global__ void numerics_kernel(int op, const uint32_t *__restrict__ in, uint32_
       out[e] = __float_as_uint((float)(pow10_dd((double)x) * (double)comp[e % 18]));
       break;
     }
+    case 10: out[e] = __float_as_uint(rcp_x86<true>(x, rcp)); break; /* rcpps of a Pade denominator, hardware form */
+    case 11: {
+      /* sigmoid of the int8 products' gates: inputs |x| < 2^18 only */
+      float v[1] = {x};
+      sigmoid_x86_fin_n<1, true>(v, rcp);
+      out[e] = __float_as_uint(v[0]);
+      break;
+    }
+    case 12: {
+      float v[1] = {x};
+      sigmoid_x86_fin_n<1, false>(v, rcp); /* the table form */
+      out[e] = __float_as_uint(v[0]);
+      break;
+    }
     default: out[e] = 0; break;
   }
 }
@@ -71,7 +85,7 @@ using namespace lpcnet_mi355x;
 
 extern "C" LPCNET_EXPORT int lpcnet_mi355x_device_numerics(int device, int op, const void *in, void *out, int n)
 {
-  if (op < 0 || op > 9 || n < 0 || (n > 0 && (!in || !out))) return -1;
+  if (op < 0 || op > 12 || n < 0 || (n > 0 && (!in || !out))) return -1;
   if (n == 0) return 0;
   if (hipSetDevice(device) != hipSuccess) return -1;
   const size_t nin = op == 8 ? 4 : (size_t)n;

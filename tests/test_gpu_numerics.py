@@ -74,3 +74,44 @@ def test_kiss99_on_device(require_gpu):
     seed = np.array(list(ctx), np.uint32)
     got = L.device_numerics(8, seed, n=256)
     assert np.array_equal(got, K["kiss99_lpcnet"])
+
+
+def _rcp_x86_expected(bits):
+    """rcpps of a Pade denominator from the tabulated x86 instruction
+    (tests/golden/rcp_x86.bin: top 11 mantissa bits, exponent-invariant;
+    results below 2^-126, +inf and NaN -> +0)."""
+    tab = np.fromfile(os.path.join(O.GOLDEN, "rcp_x86.bin"), np.uint32).astype(np.int64)
+    t = tab[(bits >> 12) & 0x7FF] + (127 << 23)
+    q = t - (bits & 0x7F800000).astype(np.int64)
+    return np.where(q < 0x00800000, 0, q).astype(np.uint32)
+
+
+def test_rcpps_every_prefix_and_exponent_on_device(require_gpu):
+    """The device rcpps (device_math.h rcp12_hw: hardware reciprocal of the
+    interval midpoint rounded to 12 bits) equals the x86 table for every
+    11-bit mantissa prefix at every exponent a Pade denominator can have
+    ([952.72, 2^128)), three low-bit patterns each, plus +inf and NaNs."""
+    e = np.arange(136, 255, dtype=np.uint32)
+    i = np.arange(2048, dtype=np.uint32)
+    lo = np.array([0, 0x5A5, 0xFFF], np.uint32)
+    bits = ((e[:, None, None] << 23) | (i[None, :, None] << 12) | lo[None, None, :]).ravel()
+    bits = bits[bits >= np.float32(952.72399902).view(np.uint32)]
+    bits = np.concatenate([bits, np.array([0x7F800000, 0x7FC00000, 0xFFC00000, 0x7F800001], np.uint32)])
+    got = L.device_numerics(10, bits)
+    exp = _rcp_x86_expected(bits)
+    bad = np.flatnonzero(got != exp)
+    assert bad.size == 0, f"{bad.size} mismatches, first den bits {bits[bad[:4]]}"
+
+
+def test_sigmoid_fin_on_device(require_gpu):
+    """sigmoid_x86_fin_n (the int8 gates' sigmoid, inputs (float)int32 *
+    2^-14 plus such a term: |x| < 2^18) against the reference's compiled
+    sigmoid8_approx on the golden inputs of that range and a dense sweep."""
+    x = np.ascontiguousarray(K["act_x"], np.float32)
+    keep = np.isfinite(x) & (np.abs(x) < 2.0 ** 18)
+    got = L.device_numerics(11, x[keep])
+    assert np.array_equal(got, f32bits(K["act_sigmoid"])[keep])
+    sweep = (np.arange(-2 ** 22, 2 ** 22, 97, dtype=np.int64) * 2.0 ** -14).astype(np.float32)
+    assert np.array_equal(L.device_numerics(11, sweep), L.device_numerics(1, sweep))
+    assert np.array_equal(L.device_numerics(12, x[keep]), f32bits(K["act_sigmoid"])[keep])
+    assert np.array_equal(L.device_numerics(12, sweep), L.device_numerics(1, sweep))
