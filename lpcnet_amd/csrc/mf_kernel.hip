@@ -122,13 +122,15 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     const float dz = A.ga_par[3 * NA + i], dr = A.ga_par[4 * NA + i], dh = A.ga_par[5 * NA + i];
     const int wsz = A.ga_wsum[i], wsr = A.ga_wsum[NA + i], wsh = A.ga_wsum[2 * NA + i];
     float st[S];
+    /* conditioning in LDS by lane position (conflict-free [gate][lane][stream]
+     * reads), taken from the unit's column */
     for (int s = 0; s < S; s++) {
       const int sid = min(s0 + s, A.nstreams - 1);
       st[s] = A.st[sid].gru_a_state[i];
       const float *ca = gru_a_cond_of(A, sid);
-      cnd[i * S + s] = ca[i];
-      cnd[(NA + i) * S + s] = ca[NA + i];
-      cnd[(2 * NA + i) * S + s] = ca[2 * NA + i];
+      cnd[tid * S + s] = ca[i];
+      cnd[(NA + tid) * S + s] = ca[NA + i];
+      cnd[(2 * NA + tid) * S + s] = ca[2 * NA + i];
     }
     /* GRU_B accumulator seeds, frame constants (nnet.c:347-356 with the
      * offset-128 correction): cvt_rne((bias + cond) * SCALE) + 128 rowsum(w) */
@@ -232,9 +234,9 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
          * (measured: 7,450 -> 7,240 cycles per sample at 1024 streams) */
         float zrv[2 * S], hv[S], inh[S];
         for (int s = 0; s < S; s++) {
-          const float inz = ((cnd[i * S + s] + e[s][0]) + e[s][3]) + e[s][6];
-          const float inr = ((cnd[(NA + i) * S + s] + e[s][1]) + e[s][4]) + e[s][7];
-          inh[s] = ((cnd[(2 * NA + i) * S + s] + e[s][2]) + e[s][5]) + e[s][8];
+          const float inz = ((cnd[tid * S + s] + e[s][0]) + e[s][3]) + e[s][6];
+          const float inr = ((cnd[(NA + tid) * S + s] + e[s][1]) + e[s][4]) + e[s][7];
+          inh[s] = ((cnd[(2 * NA + tid) * S + s] + e[s][2]) + e[s][5]) + e[s][8];
           zrv[s] = (float)(az[s] + cvt_rne((tz[s] + inz) * kScale)) * kScale1;
           zrv[S + s] = (float)(ar[s] + cvt_rne((tr[s] + inr) * kScale)) * kScale1;
           hv[s] = hpre[s];
