@@ -407,6 +407,10 @@ static int mf_wave_cost(const std::vector<std::vector<int>> &ga, const int *ub8)
   return 8 * (int)((mz + 3) / 4) + 4 * (int)((mh + 3) / 4);
 }
 
+#ifndef MF_SAMPLER_SIMD_WEIGHT
+#define MF_SAMPLER_SIMD_WEIGHT 27
+#endif
+
 static std::vector<int> mf_assign_unit_blocks(const std::vector<std::vector<int>> &ga)
 {
   constexpr int NUB = NA / 8;
@@ -419,8 +423,10 @@ static std::vector<int> mf_assign_unit_blocks(const std::vector<std::vector<int>
     int c[SAMPLE_WAVES];
     sum = 0;
     for (int w = 0; w < SAMPLE_WAVES; w++) sum += (c[w] = mf_wave_cost(ga, &p[8 * w]));
-    /* per-SIMD load: waves 0/4 and 1/5 pair up; 2 and 3 pair with a sampler */
-    return std::max(std::max(c[0] + c[4], c[1] + c[5]), 2 * std::max(c[2], c[3]));
+    /* per-SIMD load: waves 0/4 and 1/5 pair up; 2 and 3 pair with a sampler
+     * (its priority chain takes most of their SIMD: measured ~74 cycles per
+     * slot there against ~27 per slot of a wave pair) */
+    return std::max(std::max(c[0] + c[4], c[1] + c[5]), (MF_SAMPLER_SIMD_WEIGHT * std::max(c[2], c[3])) / 10);
   };
   long best_sum;
   int best = score(perm, best_sum);

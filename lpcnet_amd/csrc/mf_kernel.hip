@@ -186,8 +186,34 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
       mf_opaque(oz);
       mf_opaque(orr);
       mf_opaque(oh);
-      mf_zr<1>(lds, wz, wr, oz, orr, nzr, vz, vr);
-      mf_run<MF_HMAX, 2>(lds, wh, oh, nh, vh);
+      if (TRACE) {
+        mf_zr<1>(lds, wz, wr, oz, orr, nzr, vz, vr);
+        mf_run<MF_HMAX, 2>(lds, wh, oh, nh, vh);
+      } else {
+        /* straight-line code for this wave's group counts: with runtime
+         * counts the per-group branches make the compiler copy the x
+         * prefetch registers and wait for the next group's LDS reads
+         * before each group's last MFMA (measured: ~48 -> ~26 cycles per
+         * MFMA on a wave's own SIMD half) */
+        switch (nzr * 16 + nh) {
+#define MF_CASE(Z, H)                                 \
+  case Z * 16 + H:                                    \
+    mf_zr<1>(lds, wz, wr, oz, orr, Z, vz, vr);        \
+    mf_run<MF_HMAX, 2>(lds, wh, oh, H, vh);           \
+    break;
+#define MF_CASES(Z) MF_CASE(Z, 1) MF_CASE(Z, 2) MF_CASE(Z, 3) MF_CASE(Z, 4) MF_CASE(Z, 5) MF_CASE(Z, 6) MF_CASE(Z, 7) MF_CASE(Z, 8)
+          MF_CASES(1)
+          MF_CASES(2)
+          MF_CASES(3)
+          MF_CASES(4)
+#undef MF_CASES
+#undef MF_CASE
+          default:
+            mf_zr<1>(lds, wz, wr, oz, orr, nzr, vz, vr);
+            mf_run<MF_HMAX, 2>(lds, wh, oh, nh, vh);
+            break;
+        }
+      }
       for (int s = 0; s < S; s++) {
         az[s] = vz[0][s];
         ar[s] = vr[0][s];
