@@ -228,6 +228,15 @@ __device__ __forceinline__ uint32_t quant_s8(float x)
   return (v < 2147483648.f ? q : 0u) ^ 0x80u;
 }
 
+/* quant_s8 for GRU states: |x| <= 1 (+ rounding) or NaN by construction
+ * (convex combinations of states and tanh outputs; lpcnet_batch_restore_state
+ * refuses snapshots outside [-2, 2]), so v = 127 x + 127 < 2^31 and the
+ * out-of-range select of quant_s8 is dead: identical for every such x */
+__device__ __forceinline__ uint32_t quant_s8_state(float x)
+{
+  return __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fmaf(x, 127.f, 127.f), 0, 0u) ^ 0x80u;
+}
+
 constexpr float kScale = 128.f * 127.f;          /* vec_avx.h:686 */
 constexpr float kScale1 = 1.f / 128.f / 127.f;   /* vec_avx.h:687 */
 constexpr float kLog256 = 5.5451774445f;         /* common.h:17 */

@@ -1436,6 +1436,23 @@ LPCNET_EXPORT int lpcnet_batch_save_state(LPCNetBatch *b, int stream, void *buf)
 LPCNET_EXPORT int lpcnet_batch_restore_state(LPCNetBatch *b, int stream, const void *buf)
 {
   if (!b || stream < 0 || stream >= b->B || !buf || b->set_device()) return -1;
+  {
+    /* GRU states are convex combinations of earlier states and tanh outputs:
+     * |x| <= 1 (+ rounding) or NaN for every state the recurrence produces.
+     * The int8 kernels' state quantiser relies on |x| < 2^24 (quant_s8_state),
+     * so a snapshot outside that range is not one of ours: refuse it. */
+    StreamState tmp;
+    memcpy(&tmp, buf, sizeof(tmp));
+    auto bad = [](const float *v, int n) {
+      for (int k = 0; k < n; k++)
+        if (v[k] > 2.f || v[k] < -2.f) return true;
+      return false;
+    };
+    if (bad(tmp.gru_a_state, NA) || bad(tmp.gru_b_state, NB)) {
+      set_err("snapshot GRU state outside [-2, 2]: not a state this engine produced");
+      return -1;
+    }
+  }
   HIPCHK(hipStreamSynchronize(b->stream));
   HIPCHK(hipMemcpy(&b->d_state[stream], buf, sizeof(StreamState), hipMemcpyHostToDevice));
   return 0;

@@ -66,7 +66,11 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   float *cnd = (float *)((unsigned char *)pcmbuf + L::pcm);
   int *gbs = (int *)((unsigned char *)cnd + L::cnd);
   int *gbr = gbs + S * GB_ROWS;
-  unsigned char *img = lds + L::total; /* fixed image sections: tables and dual_fc */
+  /* fixed image sections (rcpps / u-law / logit tables, dual_fc) in static
+   * LDS: addresses into dynamic LDS carry an extra add of its base per
+   * access, on the activation and walk chains */
+  __shared__ uint4 img_s[IMG_VAR / 16];
+  unsigned char *img = (unsigned char *)img_s;
 
   if (l2_warm_role(A.mf_emb, (A.nstreams + S - 1) / S)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -90,10 +94,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     }
     return;
   }
-  {
-    uint4 *img4 = (uint4 *)img;
-    for (int o = tid; o < IMG_VAR / 16; o += MF_THREADS) img4[o] = A.image[o];
-  }
+  for (int o = tid; o < IMG_VAR / 16; o += MF_THREADS) img_s[o] = A.image[o];
   for (int e = tid; e < S * A.preload; e += MF_THREADS) {
     const int s = e / A.preload, n = e % A.preload;
     pcmbuf[s * FRAME + n] = A.pcm[(size_t)min(s0 + s, A.nstreams - 1) * A.N + n];
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     }
     const int nzr = A.mf_nzr[wv], nh = A.mf_nh[wv];
     __syncthreads(); /* image in LDS */
-    for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8(st[s]);
+    for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8_state(st[s]);
     __syncthreads(); /* initial q(h_A), q(h_B), ix, seeds */
     stamp_start();
 #ifdef MF_PRIO45
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
 #ifdef MF_FINE
         if (stamping) { float g = 0.f; for (int k = 0; k < S; k++) g += st[k]; asm volatile("" ::"v"(g)); stamp(13); }
 #endif
-        for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8(st[s]);
+        for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8_state(st[s]);
       }
       stamp(0);
       __syncthreads(); /* Y */
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
       wt[t] = v4i{(int)u.x, (int)u.y, (int)u.z, (int)u.w};
     }
     auto put_xb = [&]() {
-      if (gown) xb[gs * NB + gu] = (unsigned char)quant_s8(sbv);
+      if (gown) xb[gs * NB + gu] = (unsigned char)quant_s8_state(sbv);
     };
     auto pick = [&](const v4i &a) -> int { return gi == 0 ? a[0] : (gi == 1 ? a[1] : (gi == 2 ? a[2] : a[3])); };
     __syncthreads(); /* image in LDS */
@@ -498,13 +499,14 @@ static int launch_mf_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
 {
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)mf_kernel<S, TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+    if (hipFuncSetAttribute((const void *)mf_kernel<S, TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - IMG_VAR) !=
         hipSuccess)
       return -1;
     attr_set = true;
   }
   const int grid = warm_grid((a.nstreams + S - 1) / S, a.nstreams);
-  hipLaunchKernelGGL((mf_kernel<S, TRACE>), dim3(grid), dim3(MF_THREADS), lds_bytes, stream, a);
+  /* lds_bytes counts the static image too (mf_lds_bytes) */
+  hipLaunchKernelGGL((mf_kernel<S, TRACE>), dim3(grid), dim3(MF_THREADS), lds_bytes - IMG_VAR, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

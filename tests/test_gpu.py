@@ -309,6 +309,35 @@ def test_state_save_restore_rollback(require_gpu, blobs):
     assert np.array_equal(first[:, 1], second[:, 1])
 
 
+def test_restore_refuses_out_of_range_gru_state(require_gpu, blobs):
+    """A snapshot whose GRU state lies outside [-2, 2] cannot come from the
+    recurrence (states are convex combinations of tanh outputs) and would
+    break the int8 state quantiser's range: restore refuses it.  NaN states
+    (what NaN features produce) are accepted."""
+    import struct
+    blob = blobs["streams_int8"]
+    B, F = 2, 5
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    b = L.LPCNetBatch(B, 0, blob)
+    for f in range(4):
+        b.synthesize(allf[f])
+    snap = bytes(b.save_state(0))
+    off = snap.find(b.get_state(0)["gru_a_state"].tobytes())
+    assert off >= 0
+    bad = bytearray(snap)
+    struct.pack_into("<f", bad, off + 4 * 5, 3.0)
+    with pytest.raises(L.LPCNetError):
+        b.restore_state(0, bytes(bad))
+    nan = bytearray(snap)
+    struct.pack_into("<f", nan, off, float("nan"))
+    b.restore_state(0, bytes(nan))
+    b.restore_state(0, snap)
+    ref = L.LPCNetBatch(B, 0, blob)
+    for f in range(4):
+        ref.synthesize(allf[f])
+    assert np.array_equal(b.synthesize(allf[4]), ref.synthesize(allf[4]))
+
+
 CHECK256 = (0, 1, 128, 254, 255)
 
 
