@@ -172,7 +172,9 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
   int *sync = (int *)((unsigned char *)sbuf + L::sb);
   int *ix = sync, *ixseq = sync + 4, *abort_w = sync + 5, *done = sync + 8;
   short *pcmbuf = (short *)((unsigned char *)sync + L::sync);
-  unsigned char *img = lds + L::total;
+  /* fixed image in static LDS: no dynamic-base add per table / dual-FC address */
+  __shared__ uint4 img_s[IMG_VAR / 16];
+  unsigned char *img = (unsigned char *)img_s;
 
   {
     const float *const fp_tabs[3] = {A.emb_sig, A.emb_pred, A.emb_exc};
@@ -188,8 +190,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
   }
   const StreamState *ps = &A.st[sid];
   {
-    uint4 *img4 = (uint4 *)img;
-    for (int o = tid; o < IMG_VAR / 16; o += FP_THREADS) img4[o] = A.image[o];
+    for (int o = tid; o < IMG_VAR / 16; o += FP_THREADS) img_s[o] = A.image[o];
     for (int o = tid; o < (NA / 4) * GB_ROWS; o += FP_THREADS) gbw[o] = A.fp_gb[o];
   }
   for (int n = tid; n < A.preload; n += FP_THREADS) pcmbuf[n] = A.pcm[(size_t)sid * A.N + n];
@@ -530,12 +531,12 @@ static int launch_fp_t(const SampleArgs &a, hipStream_t stream)
 {
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)fp_kernel<TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+    if (hipFuncSetAttribute((const void *)fp_kernel<TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - IMG_VAR) !=
         hipSuccess)
       return -1;
     attr_set = true;
   }
-  hipLaunchKernelGGL((fp_kernel<TRACE>), dim3(warm_grid(a.nstreams, a.nstreams)), dim3(FP_THREADS), fp_lds_bytes(), stream, a);
+  hipLaunchKernelGGL((fp_kernel<TRACE>), dim3(warm_grid(a.nstreams, a.nstreams)), dim3(FP_THREADS), fp_lds_bytes() - IMG_VAR, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
