@@ -202,6 +202,47 @@ __device__ __forceinline__ void tanh_x86_n(float (&X)[N], const uint32_t *tab)
   for (int k = 0; k < N; k++) X[k] = clamp_x86(num[k] * den[k], -1.f, 1.f);
 }
 
+/* tanh8_approx for finite inputs below 2^60 in magnitude: the Pade
+ * denominator lies in [952.72, 2^125), so rcpps never flushes and no NaN
+ * arises: rcp_x86 / clamp_x86 without their flush and NaN selects, identical
+ * to tanh_x86_n for every such input (mf_kernel's bounded-input path). */
+template <int N, bool HW = false>
+__device__ __forceinline__ void tanh_x86_fin_n(float (&X)[N], const uint32_t *tab)
+{
+  float num[N], den[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const float X2 = X[k] * X[k];
+    num[k] = __builtin_fmaf(__builtin_fmaf(0.60863042f, X2, 96.39235687f), X2, 952.52801514f);
+    den[k] = __builtin_fmaf(__builtin_fmaf(11.88600922f, X2, 413.36801147f), X2, 952.72399902f);
+    num[k] = num[k] * X[k];
+  }
+  if constexpr (HW) {
+#pragma unroll
+    for (int k = 0; k < N; k++) X[k] = __builtin_amdgcn_fmed3f(num[k] * rcp12_hw(den[k]), -1.f, 1.f);
+    return;
+  }
+  uint32_t t[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(den[k]), 12, 11)];
+#pragma unroll
+  for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const float r = __int_as_float((int)(t[k] - (__float_as_uint(den[k]) & 0x7f800000u)));
+    X[k] = __builtin_amdgcn_fmed3f(num[k] * r, -1.f, 1.f);
+  }
+}
+
+/* cvt_rne for |v| < 2^31 (finite): v_cvt_i32_f32 of the rounded value */
+__device__ __forceinline__ int cvt_rne_fin(float v)
+{
+  const float r = __builtin_rintf(v);
+  int c;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(c) : "v"(r));
+  return c;
+}
+
 /* _mm256_cvtps_epi32: round to nearest even, out of range / NaN -> INT_MIN.
  * v_cvt_i32_f32 saturates (-big -> INT_MIN, +big -> INT_MAX) and maps NaN
  * to 0: only r >= 2^31 and NaN need the fix, and both fail r < 2^31. */

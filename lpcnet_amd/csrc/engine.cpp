@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <functional>
 #include <mutex>
@@ -955,6 +956,44 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   if (mf_ok) {
     UP(sa.mf, mft.data(), mft.size() * 4);
     UP(sa.mf_unit, mf_units.data(), mf_units.size() * 4);
+    {
+      /* Range of the GRU_A gates' inputs for the elementwise fast path:
+       * z/r: cvt_rne((bias + diag st + ((cond + Esig) + Epred) + Eexc) * 16256)
+       * cannot leave int32 (x86: INT_MIN) while |that sum| < 2^31 / 16256, with
+       * |st| <= 2 (restore-enforced); h: tanh's Pade denominator cannot overflow
+       * nor go NaN while its input is finite and < 2^60.  The kernel checks a
+       * workgroup's conditioning against these bounds once per launch. */
+      double bz = 0, bh = 0, ez = 0, eh = 0;
+      bool finite = true;
+      for (int i = 0; i < NA; i++)
+        for (int g = 0; g < 3; g++) {
+          const double b = fabs((double)ga_par[g * NA + i]) + 2.0 * fabs((double)ga_par[(3 + g) * NA + i]);
+          finite &= std::isfinite(b);
+          (g < 2 ? bz : bh) = std::max(g < 2 ? bz : bh, b);
+        }
+      const float *tabs[3] = {emb_sig, emb_pred, emb_exc};
+      for (int g = 0; g < 3; g++) {
+        double e = 0;
+        for (int t = 0; t < 3; t++) {
+          double m = 0;
+          for (int row = 0; row < 256; row++)
+            for (int i = 0; i < NA; i++) {
+              const float v = tabs[t][(size_t)row * GA_ROWS + g * NA + i];
+              finite &= std::isfinite(v);
+              m = std::max(m, (double)fabsf(v));
+            }
+          e += m;
+        }
+        (g < 2 ? ez : eh) = std::max(g < 2 ? ez : eh, e);
+      }
+      const double zr = 0.99 * (2147483648.0 / 16256.0) - bz - ez, hb = 1e17 - bh - eh;
+      sa.mf_zr_bound = finite && zr > 0 ? (float)zr : -1.f;
+      sa.mf_h_bound = finite && hb > 0 ? (float)hb : -1.f;
+      /* test hooks: force the exact path everywhere, or lower the z/r bound
+       * so that some workgroups take each path */
+      if (getenv("LPCNET_MF_EXACT")) sa.mf_zr_bound = sa.mf_h_bound = -1.f;
+      if (const char *v = getenv("LPCNET_MF_ZR_BOUND")) sa.mf_zr_bound = std::min(sa.mf_zr_bound, (float)atof(v));
+    }
     {
       /* embedding tables with their columns in lane order (coalesced gathers) */
       std::vector<float> pt((size_t)256 * GA_ROWS);

@@ -164,6 +164,10 @@ struct SampleArgs {
    * A tiles [MF_GB_TILES][64] */
   const uint32_t *mf;
   const int *mf_unit;                /* [SAMPLE_WAVES * 64]: GRU_A unit of each lane */
+  float mf_zr_bound;                 /* |GRU_A z/r conditioning| below this (and finite) for a workgroup's
+                                        streams: the elementwise step's range selects are dead (mf_kernel);
+                                        negative: never */
+  float mf_h_bound;                  /* the same for the h gate's conditioning (tanh range) */
   const float *mf_emb[3];            /* sig/pred/exc tables with columns in lane order:
                                         [256][3][SAMPLE_WAVES * 64], column p = unit mf_unit[p] */
   int mf_nzr[SAMPLE_WAVES];

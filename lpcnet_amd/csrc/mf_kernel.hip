@@ -44,7 +44,8 @@ struct MfLds {
   static constexpr int cnd = GA_ROWS * S * 4; /* GRU_A conditioning [3][NA][S] */
   static constexpr int gbs = S * GB_ROWS * 4; /* GRU_B input accumulator seeds [S][48] */
   static constexpr int gbr = GB_ROWS * 4;     /* GRU_B recurrent accumulator seeds [48] */
-  static constexpr int total = x + xb + sb + ix + pcm + cnd + gbs + gbr;
+  static constexpr int okw = 8 * 4;           /* per-GRU_A-wave "inputs in range" words */
+  static constexpr int total = x + xb + sb + ix + pcm + cnd + gbs + gbr + okw;
 };
 
 int mf_lds_bytes(int S)
@@ -66,6 +67,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   float *cnd = (float *)((unsigned char *)pcmbuf + L::pcm);
   int *gbs = (int *)((unsigned char *)cnd + L::cnd);
   int *gbr = gbs + S * GB_ROWS;
+  int *okw = gbr + GB_ROWS;
   /* fixed image sections (rcpps / u-law / logit tables, dual_fc) in static
    * LDS: addresses into dynamic LDS carry an extra add of its base per
    * access, on the activation and walk chains */
@@ -125,14 +127,20 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     float st[S];
     /* conditioning in LDS by lane position (conflict-free [gate][lane][stream]
      * reads), taken from the unit's column */
+    bool in_range = true;
     for (int s = 0; s < S; s++) {
       const int sid = min(s0 + s, A.nstreams - 1);
       st[s] = A.st[sid].gru_a_state[i];
       const float *ca = gru_a_cond_of(A, sid);
-      cnd[tid * S + s] = ca[i];
-      cnd[(NA + tid) * S + s] = ca[NA + i];
-      cnd[(2 * NA + tid) * S + s] = ca[2 * NA + i];
+      const float cz = ca[i], cr = ca[NA + i], ch = ca[2 * NA + i];
+      cnd[tid * S + s] = cz;
+      cnd[(NA + tid) * S + s] = cr;
+      cnd[(2 * NA + tid) * S + s] = ch;
+      /* NaN fails every compare: such a workgroup takes the exact path */
+      in_range &= fabsf(st[s]) <= 2.f && fabsf(cz) <= A.mf_zr_bound && fabsf(cr) <= A.mf_zr_bound &&
+                  fabsf(ch) <= A.mf_h_bound;
     }
+    if (lane == 0) okw[wv] = __ballot(!in_range) == 0ull;
     /* GRU_B accumulator seeds, frame constants (nnet.c:347-356 with the
      * offset-128 correction): cvt_rne((bias + cond) * SCALE) + 128 rowsum(w) */
     for (int e = tid; e < S * GB_ROWS; e += SAMPLE_THREADS) {
@@ -167,6 +175,11 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     }
     const int nzr = A.mf_nzr[wv], nh = A.mf_nh[wv];
     __syncthreads(); /* image in LDS */
+    /* every input of this launch within the host's range bounds
+     * (SampleArgs::mf_zr_bound): the elementwise step's range selects are
+     * dead, take the select-free forms (uniform per workgroup) */
+    bool fast = true;
+    for (int w = 0; w < SAMPLE_WAVES; w++) fast &= okw[w] != 0;
     for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8_state(st[s]);
     __syncthreads(); /* initial q(h_A), q(h_B), ix, seeds */
     stamp_start();
@@ -264,8 +277,13 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
           const float inz = ((cnd[tid * S + s] + e[s][0]) + e[s][3]) + e[s][6];
           const float inr = ((cnd[(NA + tid) * S + s] + e[s][1]) + e[s][4]) + e[s][7];
           inh[s] = ((cnd[(2 * NA + tid) * S + s] + e[s][2]) + e[s][5]) + e[s][8];
-          zrv[s] = (float)(az[s] + cvt_rne((tz[s] + inz) * kScale)) * kScale1;
-          zrv[S + s] = (float)(ar[s] + cvt_rne((tr[s] + inr) * kScale)) * kScale1;
+          if (fast) {
+            zrv[s] = (float)(az[s] + cvt_rne_fin((tz[s] + inz) * kScale)) * kScale1;
+            zrv[S + s] = (float)(ar[s] + cvt_rne_fin((tr[s] + inr) * kScale)) * kScale1;
+          } else {
+            zrv[s] = (float)(az[s] + cvt_rne((tz[s] + inz) * kScale)) * kScale1;
+            zrv[S + s] = (float)(ar[s] + cvt_rne((tr[s] + inr) * kScale)) * kScale1;
+          }
           hv[s] = hpre[s];
         }
 #ifdef MF_FINE
@@ -276,7 +294,10 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(12); }
 #endif
         for (int s = 0; s < S; s++) hv[s] = hv[s] * zrv[S + s] + inh[s];
-        tanh_x86_n<S, kHwA>(hv, rcp);
+        if (fast)
+          tanh_x86_fin_n<S, kHwA>(hv, rcp);
+        else
+          tanh_x86_n<S, kHwA>(hv, rcp);
         for (int s = 0; s < S; s++) st[s] = zrv[s] * st[s] + (1.f - zrv[s]) * hv[s];
 #ifdef MF_FINE
         if (stamping) { float g = 0.f; for (int k = 0; k < S; k++) g += st[k]; asm volatile("" ::"v"(g)); stamp(13); }

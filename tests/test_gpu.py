@@ -142,6 +142,31 @@ def test_matrix_core_kernel_edge_cases_at_bench_size(require_gpu, blobs):
         assert np.array_equal(bits(st["gru_b_state"]), bits(g)), s
 
 
+@pytest.mark.parametrize("env", ["LPCNET_MF_EXACT", "LPCNET_MF_ZR_BOUND=0.05", "LPCNET_MF_ZR_BOUND=1.5"])
+@pytest.mark.parametrize("B,check", [(1030, (0, 1, 2, 3, 517, 1029)), (70, (0, 37, 69))])
+def test_matrix_core_range_paths_match_oracle(require_gpu, blobs, monkeypatch, env, B, check):
+    """mf_kernel's GRU_A elementwise has a select-free form for workgroups
+    whose conditioning and states lie within the host's range bounds, and the
+    exact form with x86's out-of-range/NaN selects otherwise.  Force the exact
+    form everywhere, or lower the z/r bound so workgroups split between the
+    two (the bound is a launch-time property of each workgroup's streams):
+    PCM and final GRU_A states against the oracle."""
+    name, _, val = env.partition("=")
+    monkeypatch.setenv(name, val or "1")
+    F = 6
+    blob = blobs["streams_int8"]
+    b = L.LPCNetBatch(B, 0, blob)
+    b.set_kernel(4)
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    out = np.stack([b.synthesize(allf[f]) for f in range(F)], 1)
+    for s in check:
+        o = O.Oracle(blob, 0)
+        exp = np.stack([o.synthesize(allf[f, s]) for f in range(F)])
+        assert np.array_equal(out[s], exp), s
+        a, _ = o.state()
+        assert np.array_equal(bits(b.get_state(s)["gru_a_state"]), bits(a)), s
+
+
 @pytest.mark.parametrize("B,check", [(1, (0,)), (70, (0, 37, 69))])
 def test_fp32_latency_kernel_matches_oracle(require_gpu, blobs, B, check):
     """fp_kernel (one stream per workgroup) against the fp32 oracle, with a
