@@ -144,6 +144,7 @@ def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1)
     barrier_sync(timed_dist, b)
     dt = time.perf_counter() - t0
     ks, kn = b.kernel_ms(0)
+    kf = b.kernel_frames(0)
     pcm = np.zeros((F, B, 160), np.int16)
     b.d2h(pcm, d_pcm)
     b.reset_timers(2)
@@ -154,7 +155,7 @@ def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1)
     b.device_free(d_feat)
     b.device_free(d_pcm)
     b.close()
-    return dt, (ks, kn, fs / max(extra, 1), fn), info, pcm
+    return dt, (ks, kn, kf, fs / max(extra, 1), fn), info, pcm
 
 
 def algorithmic_bytes_per_launch(info, B):
@@ -163,13 +164,18 @@ def algorithmic_bytes_per_launch(info, B):
     return per * 160 * B, per
 
 
-def roofline(info, B, launch_ms, config):
-    bytes_launch, per = algorithmic_bytes_per_launch(info, B)
+def roofline(info, B, frame_ms, config, frames_per_launch=1.0):
+    """frame_ms: sample-kernel time per frame (a multi-frame launch of F
+    frames takes F x frame_ms); bytes and ops per launch = per frame x F"""
+    bytes_frame, per = algorithmic_bytes_per_launch(info, B)
+    launch_ms = frame_ms * frames_per_launch
+    bytes_launch = bytes_frame * frames_per_launch
     achieved = bytes_launch / (launch_ms * 1e-3) / 1e9
     pmc, src = measured_pmc(config, info.kernel_name)
     traffic = pmc.get("hbm_bytes_per_launch")
     r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
          "traffic": traffic, "kernel": info.kernel_name, "avg_launch_ms": launch_ms,
+         "frames_per_launch": frames_per_launch, "ms_per_frame": frame_ms,
          "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_stream_sample": per,
          "pmc_source": src,
          # what the counters say actually moves: HBM bytes / launch time, and the
@@ -180,7 +186,7 @@ def roofline(info, B, launch_ms, config):
     mf = None
     if info.mfma_ops_per_group_sample > 0:
         groups = (B + info.streams_per_workgroup - 1) // info.streams_per_workgroup
-        ops = info.mfma_ops_per_group_sample * groups * 160
+        ops = info.mfma_ops_per_group_sample * groups * 160 * frames_per_launch
         mf = {"achieved_tops": ops / (launch_ms * 1e-3) / 1e12, "peak_tops": I8_PEAK_TOPS,
               "ops_per_launch": ops, "busy_frac_pmc": pmc.get("mfma_util")}
     return r, mf
@@ -210,7 +216,7 @@ def latency(L, blob, B, measured_ms):
     clock = st[:, :, 6].max() / (stamped_ms * 1e-3) / 1e9
     out = {"kernel": info.kernel_name, "cycles_per_sample": loop, "clock_ghz_stamped": clock,
            "stamped_launch_ms": stamped_ms, "predicted_launch_ms": loop * 160 / (clock * 1e9) * 1e3,
-           "measured_launch_ms": measured_ms,
+           "measured_ms_per_frame": measured_ms,
            "cycles_per_sample_at_measured": loop * measured_ms / stamped_ms}
     if info.quad_path == 4:
         ga = per[:, :6, :].mean(axis=0)   # GRU_A waves [6][16]
@@ -300,11 +306,12 @@ def cpu_baseline(seconds):
 
 def side_line(L, blob, B, args, config, variant_name):
     nf = max(args.steps, 20)
-    dt, (k, n, _, _), info, _ = run_batch(L, blob, B, 0, args.warmup, nf, None, args.timers)
-    launch = k / max(n, 1)
-    rf, mf = roofline(info, B, launch, config)
+    dt, (k, n, kf, _, _), info, _ = run_batch(L, blob, B, 0, args.warmup, nf, None, args.timers)
+    frame_ms = k / max(kf, 1)
+    rf, mf = roofline(info, B, frame_ms, config, kf / max(n, 1))
     out = {"samples_per_s": B * nf * 160 / dt, "rt_streams": B * nf * 160 / dt / 16000.0, "x_realtime_per_stream":
-           nf * 160 / dt / 16000.0, "ms_per_frame": dt / nf * 1e3, "sample_kernel_avg_ms": launch,
+           nf * 160 / dt / 16000.0, "ms_per_frame": dt / nf * 1e3, "sample_kernel_ms_per_frame": frame_ms,
+           "sample_kernel_avg_launch_ms": k / max(n, 1),
            "kernel": info.kernel_name, "path": variant_name, "roofline": rf}
     if mf:
         out["mfma"] = mf
@@ -319,14 +326,15 @@ def main():
     blob = L.synthetic_model(1, variant)
     B = args.streams
     from lpcnet_amd.shard import weak_shard
-    dt, (ks, kn, fs, fn), info, pcm = run_batch(L, blob, B, weak_shard(rank, B).start, args.warmup, args.steps, dist,
+    dt, (ks, kn, kf, fs, fn), info, pcm = run_batch(L, blob, B, weak_shard(rank, B).start, args.warmup, args.steps, dist,
                                                 args.timers)
     dt = max_over_ranks(dist, dt)
     samples = world * B * 160 * args.steps
     value = samples / dt
-    sample_ms = ks / kn if kn else dt / args.steps * 1e3  # timers off: the frame step bounds the launch
+    # sample-kernel time per frame (timers off: the frame step bounds it)
+    sample_ms = ks / kf if kf else dt / args.steps * 1e3
     config = {1024: "b1024", 256: "b256", 1: "b1"}.get(B, f"b{B}") + ("_fp32" if variant else "")
-    rf, mf = roofline(info, B, sample_ms, config)
+    rf, mf = roofline(info, B, sample_ms, config, kf / kn if kn else 1.0)
     out = {
         "metric": "real-time 16 kHz streams/GPU; samples/s at batch=1 and batch=1024",
         "value": value,

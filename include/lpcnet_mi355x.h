@@ -123,6 +123,9 @@ LPCNET_EXPORT int lpcnet_batch_memcpy_d2h(LPCNetBatch *b, void *dst, const void 
  * both kernels. */
 LPCNET_EXPORT void lpcnet_batch_reset_timers(LPCNetBatch *b, int enable);
 LPCNET_EXPORT double lpcnet_batch_kernel_ms(LPCNetBatch *b, int which, int *launches);
+/* Frames covered by those timed launches (a multi-frame sample launch or a
+ * chunk_kernel launch covers several). */
+LPCNET_EXPORT int lpcnet_batch_kernel_frames(LPCNetBatch *b, int which);
 
 /* Debug / parity: per-sample trace of the pre-sampling logits (8 per sample,
  * nnet.c:186-211) and the sampled excitation of the LAST synthesize call.

@@ -76,6 +76,7 @@ def _load():
         "lpcnet_batch_memcpy_d2h": (i, [vp, vp, vp, C.c_size_t]),
         "lpcnet_batch_reset_timers": (None, [vp, i]),
         "lpcnet_batch_kernel_ms": (C.c_double, [vp, i, C.POINTER(C.c_int)]),
+        "lpcnet_batch_kernel_frames": (i, [vp, i]),
         "lpcnet_batch_set_stamps": (i, [vp, i]),
         "lpcnet_batch_get_stamps": (i, [vp, vp]),
         "lpcnet_batch_get_frame_stamps": (i, [vp, vp]),
@@ -322,9 +323,14 @@ class LPCNetBatch:
         lib.lpcnet_batch_reset_timers(self._b, 2 if enable is True else int(enable))
 
     def kernel_ms(self, which: int = 0) -> tuple[float, int]:
+        """(total ms, launches) of the timed launches since reset_timers."""
         n = C.c_int(0)
         ms = lib.lpcnet_batch_kernel_ms(self._b, which, C.byref(n))
         return ms, n.value
+
+    def kernel_frames(self, which: int = 0) -> int:
+        """Frames covered by the timed launches (multi-frame launches count each frame)."""
+        return lib.lpcnet_batch_kernel_frames(self._b, which)
 
     def set_stamps(self, enable: bool = True) -> None:
         if lib.lpcnet_batch_set_stamps(self._b, 1 if enable else 0) != 0:

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <atomic>
 #include <functional>
 #include <mutex>
@@ -303,7 +304,13 @@ struct LPCNetBatch {
   int timing = 0;        /* 0 off, 1 sample kernel, 2 sample + frame kernel */
   std::vector<hipEvent_t> ev_taken; /* events handed out since the last reset */
   std::vector<hipEvent_t> ev_pairs[2];
+  std::vector<int> ev_frames[2];    /* frames covered by each pair */
   std::vector<hipEvent_t> ev_free;
+  /* lower bound of every stream's frame_count (lpcnet.c:119) before the next
+   * frame: the multi-frame sample launches start where no stream can still
+   * be inside its first FEATURES_DELAY frames */
+  int min_fc = 0;
+  void frames_done(int n) { min_fc = min_fc >= 1000 ? min_fc : std::min(min_fc + n, 1000); }
   int set_device() { return hipSetDevice(device) == hipSuccess ? 0 : -1; }
 };
 
@@ -1184,27 +1191,33 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
   if (e[0]) {
     b->ev_pairs[1].push_back(e[0]);
     b->ev_pairs[1].push_back(ef ? ef : e[1]);
+    b->ev_frames[1].push_back(1);
   }
   if (ef) b->ev_taken.push_back(ef);
   if (e[1]) {
     b->ev_pairs[0].push_back(e[1]);
     b->ev_pairs[0].push_back(e[2]);
+    b->ev_frames[0].push_back(1);
   }
+  b->frames_done(1);
   for (hipEvent_t x : e)
     if (x) b->ev_taken.push_back(x);
   return 0;
 }
 
 /* Chunked form: the frame network of frames [0, n) of d_features has run
- * (chunk_kernel, outputs in d_chunk[f]); launch the sample kernel of frame f
- * on b->stream, reading its conditioning from d_chunk[f]. */
-int launch_chunk_samples(LPCNetBatch *b, int f, short *d_pcm, int N)
+ * (chunk_kernel, outputs in d_chunk[f]); launch the sample kernel of frames
+ * f .. f + nfr - 1 on b->stream, reading their conditioning from d_chunk[f..]
+ * and writing d_pcm [nfr][B][N].  nfr > 1: matrix-core kernel only, every
+ * stream past its first FEATURES_DELAY frames (SampleArgs::nframes). */
+int launch_chunk_samples(LPCNetBatch *b, int f, short *d_pcm, int N, int nfr = 1)
 {
   SampleArgs sa = b->sa;
   sa.st = b->d_state;
   sa.cond = b->d_chunk + (size_t)f * b->B;
   sa.nstreams = b->B;
   sa.N = N;
+  sa.nframes = nfr;
   sa.pcm = d_pcm;
   sa.preload = 0;
   sa.stamps = b->d_stamps;
@@ -1225,6 +1238,7 @@ int launch_chunk_samples(LPCNetBatch *b, int f, short *d_pcm, int N)
     HIPCHK(hipEventRecord(e2, b->stream));
     b->ev_pairs[0].push_back(e1);
     b->ev_pairs[0].push_back(e2);
+    b->ev_frames[0].push_back(nfr);
     b->ev_taken.push_back(e1);
     b->ev_taken.push_back(e2);
   }
@@ -1257,9 +1271,11 @@ int launch_chunk_frames(LPCNetBatch *b, const float *d_features, int n)
     HIPCHK(hipEventRecord(e1, b->stream));
     b->ev_pairs[1].push_back(e0);
     b->ev_pairs[1].push_back(e1);
+    b->ev_frames[1].push_back(n);
     b->ev_taken.push_back(e0);
     b->ev_taken.push_back(e1);
   }
+  b->frames_done(n);
   return 0;
 }
 
@@ -1271,6 +1287,9 @@ int check_status(LPCNetBatch *b)
   __atomic_store_n(b->h_status, 0, __ATOMIC_RELEASE);
   if (st & STATUS_FLAG_TIMEOUT)
     set_err("device abort: an LDS flag wait in the sample kernel exceeded its spin limit; the PCM of this call is invalid");
+  else if (st & STATUS_ACTIVITY)
+    set_err("device abort: a multi-frame sample launch saw a stream turn active mid-launch (frame_count bound out of "
+            "date); the PCM of this call is invalid");
   else
     set_err("device abort: unknown status " + std::to_string(st));
   return -1;
@@ -1338,6 +1357,9 @@ LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
   if (ok) *b->h_status = 0;
   ok = ok && hipMalloc(&b->d_lpc, sizeof(float) * NLPC * (size_t)nb_streams * LPC_CHUNK) == hipSuccess;
   ok = ok && hipMalloc(&b->d_lpc_tab, sizeof(LpcTables)) == hipSuccess;
+  /* frame-network outputs of a chunk of frames (chunk_kernel -> multi-frame
+   * sample launches): allocated here, not inside the first synthesize call */
+  ok = ok && hipMalloc(&b->d_chunk, sizeof(FrameCond) * (size_t)LPC_CHUNK * nb_streams) == hipSuccess;
   if (ok) {
     LpcTables T;
     build_lpc_tables(T);
@@ -1428,6 +1450,7 @@ LPCNET_EXPORT int lpcnet_batch_reset_stream(LPCNetBatch *b, int stream)
   host_reset_state(s);
   HIPCHK(hipMemcpyAsync(&b->d_state[stream], &s, sizeof(s), hipMemcpyHostToDevice, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
+  b->min_fc = std::min(b->min_fc, s.frame_count);
   return 0;
 }
 
@@ -1439,6 +1462,7 @@ LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b)
   for (int i = 1; i < b->B; i++) v[i] = v[0];
   (void)hipMemcpyAsync(b->d_state, v.data(), sizeof(StreamState) * v.size(), hipMemcpyHostToDevice, b->stream);
   (void)hipStreamSynchronize(b->stream);
+  b->min_fc = v[0].frame_count;
 }
 
 LPCNET_EXPORT int lpcnet_batch_synthesize_impl(LPCNetBatch *b, const float *features, short *pcm, int N, int preload)
@@ -1494,6 +1518,9 @@ LPCNET_EXPORT int lpcnet_batch_restore_state(LPCNetBatch *b, int stream, const v
   }
   HIPCHK(hipStreamSynchronize(b->stream));
   HIPCHK(hipMemcpy(&b->d_state[stream], buf, sizeof(StreamState), hipMemcpyHostToDevice));
+  int fc;
+  memcpy(&fc, (const unsigned char *)buf + offsetof(StreamState, frame_count), sizeof(fc));
+  b->min_fc = std::min(b->min_fc, fc);
   return 0;
 }
 
@@ -1507,9 +1534,15 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
   if (ensure_trace(b, N)) return -1;
   const size_t fstride = (size_t)b->B * NF;
   if (nframes == 0) return 0;
-  /* overlapped frame kernels: matrix-core and fp32 latency kernels (the only
-   * ones reading the frame outputs through FrameCond), when CUs are free */
-  const bool ovl = b->fstream && (b->mf || b->fp) && nframes >= 2 && !b->d_stamps && !getenv("LPCNET_NO_OVERLAP");
+  /* multi-frame matrix-core sample launches (SampleArgs::nframes): one
+   * launch per chunk instead of one per frame (each costs a ~10 us dispatch
+   * gap plus its prologue), behind the chunked frame network */
+  const bool mfm = b->mf && b->chunking && !b->sa.trace_logits && N > 0 &&
+                   nframes >= CHUNK_MIN_FRAMES && !getenv("LPCNET_NO_MULTIFRAME");
+  /* otherwise overlapped frame kernels: matrix-core and fp32 latency kernels
+   * (the only ones reading the frame outputs through FrameCond), when CUs
+   * are free */
+  const bool ovl = !mfm && b->fstream && (b->mf || b->fp) && nframes >= 2 && !b->d_stamps && !getenv("LPCNET_NO_OVERLAP");
   if (ovl) {
     /* the first frame kernel follows everything already on stream */
     HIPCHK(hipEventRecord(b->ev_start, b->stream));
@@ -1518,16 +1551,8 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
   /* chunked frame network: batches too large for the overlapped path (the
    * sample kernels fill the GPU), matrix-core and fp32 sample kernels (the
    * ones reading FrameCond) */
-  const bool chunked = !ovl && b->chunking && (b->mf || b->fp) && b->B > OVERLAP_MAX_STREAMS && !b->d_stamps &&
-                       !getenv("LPCNET_NO_CHUNK");
-  if (chunked && !b->d_chunk) {
-    HIPCHK(hipStreamSynchronize(b->stream));
-    if (hipMalloc(&b->d_chunk, sizeof(FrameCond) * (size_t)LPC_CHUNK * b->B) != hipSuccess) {
-      b->d_chunk = nullptr;
-      set_err("hipMalloc of the chunk conditioning buffer failed");
-      return -1;
-    }
-  }
+  const bool chunked = mfm || (!ovl && b->chunking && (b->mf || b->fp) && b->B > OVERLAP_MAX_STREAMS && !b->d_stamps &&
+                               !getenv("LPCNET_NO_CHUNK"));
   hipStream_t fs = ovl ? b->fstream : b->stream;
   for (int c0 = 0; c0 < nframes; c0 += LPC_CHUNK) {
     /* lpc_from_cepstrum depends only on the features: one launch for up to
@@ -1540,9 +1565,13 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
       return -1;
     }
     if (chunked && n >= CHUNK_MIN_FRAMES) {
+      const int fc0 = b->min_fc;
       if (launch_chunk_frames(b, d_features + c0 * fstride, n)) return -1;
-      for (int f = c0; f < c0 + n; f++)
+      /* frames in which a stream may still turn active: one launch each */
+      const int k = mfm ? std::min(n, std::max(0, FEATURES_DELAY - fc0)) : n;
+      for (int f = c0; f < c0 + k; f++)
         if (launch_chunk_samples(b, f - c0, d_pcm + (size_t)f * b->B * N, N)) return -1;
+      if (k < n && launch_chunk_samples(b, k, d_pcm + (size_t)(c0 + k) * b->B * N, N, n - k)) return -1;
       continue;
     }
     for (int f = c0; f < c0 + n; f++)
@@ -1610,7 +1639,10 @@ LPCNET_EXPORT void lpcnet_batch_reset_timers(LPCNetBatch *b, int enable)
   if (!b) return;
   b->set_device();
   (void)hipStreamSynchronize(b->stream);
-  for (int k = 0; k < 2; k++) b->ev_pairs[k].clear();
+  for (int k = 0; k < 2; k++) {
+    b->ev_pairs[k].clear();
+    b->ev_frames[k].clear();
+  }
   /* stream is idle (and fstream with it): no slot reuse needs a wait */
   b->ev_samp_used[0] = b->ev_samp_used[1] = false;
   for (hipEvent_t e : b->ev_taken) b->ev_free.push_back(e);
@@ -1631,6 +1663,14 @@ LPCNET_EXPORT double lpcnet_batch_kernel_ms(LPCNetBatch *b, int which, int *laun
   }
   if (launches) *launches = (int)(v.size() / 2);
   return tot;
+}
+
+LPCNET_EXPORT int lpcnet_batch_kernel_frames(LPCNetBatch *b, int which)
+{
+  if (!b || which < 0 || which > 1) return -1;
+  int n = 0;
+  for (int k : b->ev_frames[which]) n += k;
+  return n;
 }
 
 static int stamp_groups(const LPCNetBatch *b)

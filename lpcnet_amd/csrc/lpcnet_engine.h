@@ -137,6 +137,10 @@ struct SampleArgs {
   const FrameCond *cond; /* optional [B]: read the frame's outputs here instead of st */
   int nstreams;
   int N;                 /* samples to produce (<= FRAME) */
+  int nframes;           /* mf_kernel: frames per launch (0 = 1).  Frame f reads cond + f B and
+                            writes pcm + f B N; needs cond, preload 0, no trace, and every
+                            stream active in all or none of the frames (the host splits a run
+                            at the FEATURES_DELAY transition, STATUS_ACTIVITY otherwise) */
   short *pcm;            /* [B][N] */
   int preload;           /* samples 0..preload-1 are teacher-forced from pcm (lpcnet.c:256-259) */
   const float *emb_sig, *emb_pred, *emb_exc; /* [256][GA_ROWS] */
@@ -192,10 +196,28 @@ struct SampleArgs {
 constexpr int FLAG_SPIN_LIMIT_DEFAULT = 1 << 20; /* lpcnet_batch_set_spin_limit */
 /* Status bits a sample kernel reports to the host (SampleArgs::status). */
 constexpr int STATUS_FLAG_TIMEOUT = 1; /* an LDS flag wait exceeded spin_limit: output invalid */
+constexpr int STATUS_ACTIVITY = 2;     /* a multi-frame launch saw a stream become active mid-launch */
 
 /* The frame step's outputs as a sample kernel reads them: the FrameCond
  * copy when the launch has one, else the stream state. */
 #if defined(__HIP__) || defined(__HIPCC__)
+/* the same with the frame's conditioning array given (multi-frame launches) */
+__device__ __forceinline__ int frame_count_of(const SampleArgs &A, const FrameCond *cf, int sid)
+{
+  return cf ? cf[sid].frame_count : A.st[sid].frame_count;
+}
+__device__ __forceinline__ const float *gru_a_cond_of(const FrameCond *cf, const SampleArgs &A, int sid)
+{
+  return cf ? cf[sid].gru_a_cond : A.st[sid].gru_a_cond;
+}
+__device__ __forceinline__ const float *gru_b_cond_of(const FrameCond *cf, const SampleArgs &A, int sid)
+{
+  return cf ? cf[sid].gru_b_cond : A.st[sid].gru_b_cond;
+}
+__device__ __forceinline__ const float *lpc_of(const FrameCond *cf, const SampleArgs &A, int sid)
+{
+  return cf ? cf[sid].lpc : A.st[sid].lpc;
+}
 __device__ __forceinline__ int frame_count_of(const SampleArgs &A, int sid)
 {
   return A.cond ? A.cond[sid].frame_count : A.st[sid].frame_count;

@@ -1,7 +1,9 @@
 /*
  * mf_kernel.hip -- the matrix-core sample kernel: lpcnet_synthesize_tail_impl
  * (lpcnet.c:235-271) for S <= 4 streams per 512-thread workgroup, persistent
- * over the N samples of one frame.  Default for non-saturating int8 models.
+ * over the N samples of one frame, or of several frames in one launch
+ * (SampleArgs::nframes: no ~10 us dispatch gap and prologue per frame).
+ * Default for non-saturating int8 models.
  *
  * Both int8 products run on the matrix cores, from register-resident weights,
  * with exact int32 accumulation (bit-identical to maddubs/madd whenever no
@@ -45,7 +47,8 @@ struct MfLds {
   static constexpr int gbs = S * GB_ROWS * 4; /* GRU_B input accumulator seeds [S][48] */
   static constexpr int gbr = GB_ROWS * 4;     /* GRU_B recurrent accumulator seeds [48] */
   static constexpr int okw = 8 * 4;           /* per-GRU_A-wave "inputs in range" words */
-  static constexpr int total = x + xb + sb + ix + pcm + cnd + gbs + gbr + okw;
+  static constexpr int gbw = 3 * 64 * 16;     /* GRU_B recurrent A tiles [3][64 lanes] (LDS, not registers) */
+  static constexpr int total = x + xb + sb + ix + pcm + cnd + gbs + gbr + okw + gbw;
 };
 
 int mf_lds_bytes(int S)
@@ -68,6 +71,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   int *gbs = (int *)((unsigned char *)cnd + L::cnd);
   int *gbr = gbs + S * GB_ROWS;
   int *okw = gbr + GB_ROWS;
+  v4i *gbw = (v4i *)(okw + 8);
   /* fixed image sections (rcpps / u-law / logit tables, dual_fc) in static
    * LDS: addresses into dynamic LDS carry an extra add of its base per
    * access, on the activation and walk chains */
@@ -81,6 +85,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   /* GRU_A elementwise: one stream per lane is latency-bound (hardware rcp),
    * 2-4 streams per lane are VALU-bound (LDS table) */
   constexpr bool kHwA = S == 1;
+  constexpr bool kGbwLds = S == 4;
 
   bool active[S];
   bool any = false;
@@ -89,10 +94,29 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     active[s] = sid < A.nstreams && frame_count_of(A, sid) > FEATURES_DELAY;
     any |= active[s];
   }
-  if (!any) {
-    for (int e = tid; e < S * A.N; e += MF_THREADS) {
-      const int s = e / A.N, n = e % A.N;
-      if (s0 + s < A.nstreams) A.pcm[(size_t)(s0 + s) * A.N + n] = 0;
+  /* multi-frame launches (A.nframes > 1): frame f reads cond + f B and
+   * writes pcm + f B N, the states stay in registers from frame to frame,
+   * the GRU_A waves stage the next frame's inputs (GRU_A conditioning, GRU_B
+   * seeds, range words) after the last sample's barrier Y, and one extra
+   * barrier separates the frames.  Activity (lpcnet.c:265-268: the first
+   * FEATURES_DELAY frames of a stream give zeros and leave its state alone)
+   * must be the same in every frame of the launch: the host splits runs at
+   * that transition; a launch that sees one anyway reports STATUS_ACTIVITY. */
+  const int nfr = A.nframes > 1 ? A.nframes : 1;
+  const int total = nfr * A.N;
+  bool bad = false;
+  if (nfr > 1) {
+    const FrameCond *cl = A.cond + (size_t)(nfr - 1) * A.nstreams;
+    for (int s = 0; s < S; s++) {
+      const int sid = s0 + s;
+      bad |= sid < A.nstreams && (frame_count_of(A, cl, sid) > FEATURES_DELAY) != active[s];
+    }
+    if (bad && tid == 0 && A.status) A.status[0] = STATUS_ACTIVITY; /* plain vector store to the pinned host word */
+  }
+  if (!any || bad) {
+    for (int e = tid; e < S * total; e += MF_THREADS) {
+      const int s = e / total, fn = e % total, f = fn / A.N, n = fn % A.N;
+      if (s0 + s < A.nstreams) A.pcm[((size_t)f * A.nstreams + s0 + s) * A.N + n] = 0;
     }
     return;
   }
@@ -125,28 +149,35 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     const float dz = A.ga_par[3 * NA + i], dr = A.ga_par[4 * NA + i], dh = A.ga_par[5 * NA + i];
     const int wsz = A.ga_wsum[i], wsr = A.ga_wsum[NA + i], wsh = A.ga_wsum[2 * NA + i];
     float st[S];
-    /* conditioning in LDS by lane position (conflict-free [gate][lane][stream]
-     * reads), taken from the unit's column */
-    bool in_range = true;
-    for (int s = 0; s < S; s++) {
-      const int sid = min(s0 + s, A.nstreams - 1);
-      st[s] = A.st[sid].gru_a_state[i];
-      const float *ca = gru_a_cond_of(A, sid);
-      const float cz = ca[i], cr = ca[NA + i], ch = ca[2 * NA + i];
-      cnd[tid * S + s] = cz;
-      cnd[(NA + tid) * S + s] = cr;
-      cnd[(2 * NA + tid) * S + s] = ch;
-      /* NaN fails every compare: such a workgroup takes the exact path */
-      in_range &= fabsf(st[s]) <= 2.f && fabsf(cz) <= A.mf_zr_bound && fabsf(cr) <= A.mf_zr_bound &&
-                  fabsf(ch) <= A.mf_h_bound;
-    }
-    if (lane == 0) okw[wv] = __ballot(!in_range) == 0ull;
-    /* GRU_B accumulator seeds, frame constants (nnet.c:347-356 with the
-     * offset-128 correction): cvt_rne((bias + cond) * SCALE) + 128 rowsum(w) */
-    for (int e = tid; e < S * GB_ROWS; e += SAMPLE_THREADS) {
-      const int s = e / GB_ROWS, r = e % GB_ROWS;
-      gbs[e] = cvt_rne((A.gb_par[r] + gru_b_cond_of(A, min(s0 + s, A.nstreams - 1))[r]) * kScale) + A.gb_wsum[r];
-    }
+    for (int s = 0; s < S; s++) st[s] = A.st[min(s0 + s, A.nstreams - 1)].gru_a_state[i];
+    /* a frame's inputs: the conditioning in LDS by lane
+     * position (conflict-free [gate][lane][stream] reads, from the unit's
+     * column; read by this thread only: one buffer), the range word of this
+     * wave and the GRU_B accumulator seeds (nnet.c:347-356 with the
+     * offset-128 correction: cvt_rne((bias + cond) * SCALE) + 128 rowsum(w)) */
+    auto stage = [&](const FrameCond *cf) {
+      bool in_range = true;
+      for (int s = 0; s < S; s++) {
+        const int sid = min(s0 + s, A.nstreams - 1);
+        const float *ca = gru_a_cond_of(cf, A, sid);
+        const float cz = ca[i], cr = ca[NA + i], ch = ca[2 * NA + i];
+        cnd[tid * S + s] = cz;
+        cnd[(NA + tid) * S + s] = cr;
+        cnd[(2 * NA + tid) * S + s] = ch;
+        /* NaN fails every compare: such a workgroup takes the exact path */
+        in_range &= fabsf(st[s]) <= 2.f && fabsf(cz) <= A.mf_zr_bound && fabsf(cr) <= A.mf_zr_bound &&
+                    fabsf(ch) <= A.mf_h_bound;
+      }
+      if (lane == 0) okw[wv] = __ballot(!in_range) == 0ull;
+      for (int e = tid; e < S * GB_ROWS; e += SAMPLE_THREADS) {
+        const int s = e / GB_ROWS, r = e % GB_ROWS;
+        gbs[e] =
+            cvt_rne((A.gb_par[r] + gru_b_cond_of(cf, A, min(s0 + s, A.nstreams - 1))[r]) * kScale) + A.gb_wsum[r];
+      }
+    };
+    const FrameCond *cf = A.cond;
+    stage(cf);
+    short *pcm_out = A.pcm; /* frame of the next write-out */
     if (tid < GB_ROWS) gbr[tid] = cvt_rne(A.gb_par[GB_ROWS + tid] * kScale) + A.gb_wsum[GB_ROWS + tid];
     /* this lane's GRU_A weight rows and x offsets, for all N samples */
     uint32_t wz[MF_ZMAX], wr[MF_ZMAX], wh[MF_HMAX], oz[MF_ZMAX / 2], orr[MF_ZMAX / 2], oh[MF_HMAX / 2];
@@ -175,11 +206,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     }
     const int nzr = A.mf_nzr[wv], nh = A.mf_nh[wv];
     __syncthreads(); /* image in LDS */
-    /* every input of this launch within the host's range bounds
-     * (SampleArgs::mf_zr_bound): the elementwise step's range selects are
-     * dead, take the select-free forms (uniform per workgroup) */
     bool fast = true;
-    for (int w = 0; w < SAMPLE_WAVES; w++) fast &= okw[w] != 0;
     for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8_state(st[s]);
     __syncthreads(); /* initial q(h_A), q(h_B), ix, seeds */
     stamp_start();
@@ -238,77 +265,97 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
       }
     };
     recurrent();
-    for (int n = 0; n < A.N; n++) {
-      stamp(4);
-      __syncthreads(); /* X */
-      stamp(5);
-      {
-        /* GRU_A input (nnet.c:484-491): all 9*S gathers in flight at once */
-        float e[S][9];
-        for (int s = 0; s < S; s++) {
-          /* the indices are the same in every lane: scalar row addresses */
-          const int4 v = *(const int4 *)(ix + s * 4);
-          const float *e1 = A.mf_emb[0] + (__builtin_amdgcn_readfirstlane(v.x) & 0xFF) * GA_ROWS;
-          const float *e2 = A.mf_emb[1] + (__builtin_amdgcn_readfirstlane(v.y) & 0xFF) * GA_ROWS;
-          const float *e3 = A.mf_emb[2] + (__builtin_amdgcn_readfirstlane(v.z) & 0xFF) * GA_ROWS;
-#pragma unroll
-          for (int g = 0; g < 3; g++) {
-            e[s][g] = e1[g * NA + tid];
-            e[s][3 + g] = e2[g * NA + tid];
-            e[s][6 + g] = e3[g * NA + tid];
-          }
+    for (int f = 0; f < nfr; f++) {
+      if (f > 0) {
+        __syncthreads(); /* frame start: inputs staged, the previous frame's PCM complete */
+        for (int e = tid; e < S * A.N; e += SAMPLE_THREADS) {
+          const int s = e / A.N, k = e % A.N;
+          if (s0 + s < A.nstreams) pcm_out[(size_t)(s0 + s) * A.N + k] = active[s] ? pcmbuf[s * FRAME + k] : (short)0;
         }
-        if (stamping) {
-          /* diagnostic only: wait for every gather before the stamp */
-          float g = 0.f;
-          for (int s = 0; s < S; s++)
-#pragma unroll
-            for (int k = 0; k < 9; k++) g += e[s][k];
-          asm volatile("" ::"v"(g));
-          stamp(10);
-        }
-        /* compute_sparse_gru elementwise (nnet.c:431-447).  Scalar float ops
-         * only: packed v_pk_add/mul_f32 (explicit or SLP-formed -- this file
-         * is built with -fno-slp-vectorize) cost more SIMD issue cycles than
-         * the scalar pairs, and waves 0/4 and 1/5 share one SIMD's VALU here
-         * (measured: 7,450 -> 7,240 cycles per sample at 1024 streams) */
-        float zrv[2 * S], hv[S], inh[S];
-        for (int s = 0; s < S; s++) {
-          const float inz = ((cnd[tid * S + s] + e[s][0]) + e[s][3]) + e[s][6];
-          const float inr = ((cnd[(NA + tid) * S + s] + e[s][1]) + e[s][4]) + e[s][7];
-          inh[s] = ((cnd[(2 * NA + tid) * S + s] + e[s][2]) + e[s][5]) + e[s][8];
-          if (fast) {
-            zrv[s] = (float)(az[s] + cvt_rne_fin((tz[s] + inz) * kScale)) * kScale1;
-            zrv[S + s] = (float)(ar[s] + cvt_rne_fin((tr[s] + inr) * kScale)) * kScale1;
-          } else {
-            zrv[s] = (float)(az[s] + cvt_rne((tz[s] + inz) * kScale)) * kScale1;
-            zrv[S + s] = (float)(ar[s] + cvt_rne((tr[s] + inr) * kScale)) * kScale1;
-          }
-          hv[s] = hpre[s];
-        }
-#ifdef MF_FINE
-        if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(11); }
-#endif
-        sigmoid_x86_fin_n<2 * S, kHwA>(zrv, rcp);
-#ifdef MF_FINE
-        if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(12); }
-#endif
-        for (int s = 0; s < S; s++) hv[s] = hv[s] * zrv[S + s] + inh[s];
-        if (fast)
-          tanh_x86_fin_n<S, kHwA>(hv, rcp);
-        else
-          tanh_x86_n<S, kHwA>(hv, rcp);
-        for (int s = 0; s < S; s++) st[s] = zrv[s] * st[s] + (1.f - zrv[s]) * hv[s];
-#ifdef MF_FINE
-        if (stamping) { float g = 0.f; for (int k = 0; k < S; k++) g += st[k]; asm volatile("" ::"v"(g)); stamp(13); }
-#endif
-        for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8_state(st[s]);
+        pcm_out += (size_t)A.nstreams * A.N;
       }
-      stamp(0);
-      __syncthreads(); /* Y */
-      stamp(1);
-      if (n + 1 < A.N) recurrent(); /* W q(h_A(n)) for sample n+1, beside GRU_B and the sampling of n */
-      stamp(2);
+      /* every input of this frame within the host's range bounds
+       * (SampleArgs::mf_zr_bound): the elementwise step's range selects are
+       * dead, take the select-free forms (uniform per workgroup) */
+      fast = true;
+      for (int w = 0; w < SAMPLE_WAVES; w++) fast &= okw[w] != 0;
+      for (int n = 0; n < A.N; n++) {
+        stamp(4);
+        __syncthreads(); /* X */
+        stamp(5);
+        {
+          /* GRU_A input (nnet.c:484-491): all 9*S gathers in flight at once */
+          float e[S][9];
+          for (int s = 0; s < S; s++) {
+            /* the indices are the same in every lane: scalar row addresses */
+            const int4 v = *(const int4 *)(ix + s * 4);
+            const float *e1 = A.mf_emb[0] + (__builtin_amdgcn_readfirstlane(v.x) & 0xFF) * GA_ROWS;
+            const float *e2 = A.mf_emb[1] + (__builtin_amdgcn_readfirstlane(v.y) & 0xFF) * GA_ROWS;
+            const float *e3 = A.mf_emb[2] + (__builtin_amdgcn_readfirstlane(v.z) & 0xFF) * GA_ROWS;
+#pragma unroll
+            for (int g = 0; g < 3; g++) {
+              e[s][g] = e1[g * NA + tid];
+              e[s][3 + g] = e2[g * NA + tid];
+              e[s][6 + g] = e3[g * NA + tid];
+            }
+          }
+          if (stamping) {
+            /* diagnostic only: wait for every gather before the stamp */
+            float g = 0.f;
+            for (int s = 0; s < S; s++)
+#pragma unroll
+              for (int k = 0; k < 9; k++) g += e[s][k];
+            asm volatile("" ::"v"(g));
+            stamp(10);
+          }
+          /* compute_sparse_gru elementwise (nnet.c:431-447).  Scalar float ops
+           * only: packed v_pk_add/mul_f32 (explicit or SLP-formed -- this file
+           * is built with -fno-slp-vectorize) cost more SIMD issue cycles than
+           * the scalar pairs, and waves 0/4 and 1/5 share one SIMD's VALU here
+           * (measured: 7,450 -> 7,240 cycles per sample at 1024 streams) */
+          float zrv[2 * S], hv[S], inh[S];
+          for (int s = 0; s < S; s++) {
+            const float inz = ((cnd[tid * S + s] + e[s][0]) + e[s][3]) + e[s][6];
+            const float inr = ((cnd[(NA + tid) * S + s] + e[s][1]) + e[s][4]) + e[s][7];
+            inh[s] = ((cnd[(2 * NA + tid) * S + s] + e[s][2]) + e[s][5]) + e[s][8];
+            if (fast) {
+              zrv[s] = (float)(az[s] + cvt_rne_fin((tz[s] + inz) * kScale)) * kScale1;
+              zrv[S + s] = (float)(ar[s] + cvt_rne_fin((tr[s] + inr) * kScale)) * kScale1;
+            } else {
+              zrv[s] = (float)(az[s] + cvt_rne((tz[s] + inz) * kScale)) * kScale1;
+              zrv[S + s] = (float)(ar[s] + cvt_rne((tr[s] + inr) * kScale)) * kScale1;
+            }
+            hv[s] = hpre[s];
+          }
+#ifdef MF_FINE
+          if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(11); }
+#endif
+          sigmoid_x86_fin_n<2 * S, kHwA>(zrv, rcp);
+#ifdef MF_FINE
+          if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(12); }
+#endif
+          for (int s = 0; s < S; s++) hv[s] = hv[s] * zrv[S + s] + inh[s];
+          if (fast)
+            tanh_x86_fin_n<S, kHwA>(hv, rcp);
+          else
+            tanh_x86_n<S, kHwA>(hv, rcp);
+          for (int s = 0; s < S; s++) st[s] = zrv[s] * st[s] + (1.f - zrv[s]) * hv[s];
+#ifdef MF_FINE
+          if (stamping) { float g = 0.f; for (int k = 0; k < S; k++) g += st[k]; asm volatile("" ::"v"(g)); stamp(13); }
+#endif
+          for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8_state(st[s]);
+        }
+        stamp(0);
+        __syncthreads(); /* Y */
+        stamp(1);
+        if (n + 1 < A.N || f + 1 < nfr) recurrent(); /* W q(h_A(n)) for sample n+1, beside GRU_B and the sampling of n */
+        stamp(2);
+      }
+      if (f + 1 < nfr) {
+        /* next frame's inputs, read after the frame-start barrier */
+        cf += A.nstreams;
+        stage(cf);
+      }
     }
     stamp(4);
     __syncthreads(); /* final */
@@ -349,12 +396,21 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
       rz = p->rng[0]; rw = p->rng[1]; rj = p->rng[2]; rc = p->rng[3];
     }
     float sbv = A.st[min(s0 + sl, A.nstreams - 1)].gru_b_state[gu];
-    v4i wt[MF_GB_TILES];
+    /* GRU_B weight tiles in registers; with 4 streams the 3 recurrent
+     * tiles live in LDS instead (read in the samplers' slack before barrier
+     * Y: 12 registers fewer, no spill) */
+    constexpr int kRegTiles = kGbwLds ? MF_GB_IN : MF_GB_TILES;
+    v4i wt[kRegTiles];
 #pragma unroll
-    for (int t = 0; t < MF_GB_TILES; t++) {
+    for (int t = 0; t < kRegTiles; t++) {
       const uint4 u = A.mf_gb[t * 64 + lane];
       wt[t] = v4i{(int)u.x, (int)u.y, (int)u.z, (int)u.w};
     }
+    if (kGbwLds && sw == 0)
+      for (int g = 0; g < 3; g++) {
+        const uint4 u = A.mf_gb[(MF_GB_IN + g) * 64 + lane];
+        gbw[g * 64 + lane] = v4i{(int)u.x, (int)u.y, (int)u.z, (int)u.w};
+      }
     auto put_xb = [&]() {
       if (gown) xb[gs * NB + gu] = (unsigned char)quant_s8_state(sbv);
     };
@@ -397,98 +453,122 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
       put_xb();
       pend_n = -1;
     };
-    for (int n = 0; n < A.N; n++) {
-      stamp(4);
-      __syncthreads(); /* X */
-      stamp(5);
-      v4i acc[3], accr[3];
-      if (samp) {
-        finish();
-        stamp(13);
-        /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
-        const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
-        const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
-        lane_thresholds(F, logit_tab, r0, r1, t03, t47);
-        /* GRU_B recurrent product (nnet.c:355-361) needs only q(h_B(n-1)):
-         * before barrier Y.  Seeds are the accumulator inputs. */
-        const v4i xr = *(const v4i *)(xb + sl * NB);
+    const FrameCond *cf = A.cond;
+    for (int f = 0; f < nfr; f++) {
+      if (f > 0) __syncthreads(); /* frame start */
+      for (int n = 0; n < A.N; n++) {
+        stamp(4);
+        __syncthreads(); /* X */
+        stamp(5);
+        v4i acc[3], accr[3];
+        if (samp) {
+          finish();
+          stamp(13);
+          /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
+          const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
+          const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
+          lane_thresholds(F, logit_tab, r0, r1, t03, t47);
+          /* GRU_B recurrent product (nnet.c:355-361) needs only q(h_B(n-1)):
+           * before barrier Y.  Seeds are the accumulator inputs. */
+          const v4i xr = *(const v4i *)(xb + sl * NB);
 #pragma unroll
-        for (int g = 0; g < 3; g++) {
-          acc[g] = *(const v4i *)(gbs + sl * GB_ROWS + 16 * g + 4 * gq);
-          accr[g] = *(const v4i *)(gbr + 16 * g + 4 * gq);
+          for (int g = 0; g < 3; g++) {
+            acc[g] = *(const v4i *)(gbs + sl * GB_ROWS + 16 * g + 4 * gq);
+            accr[g] = *(const v4i *)(gbr + 16 * g + 4 * gq);
+          }
+#pragma unroll
+          for (int g = 0; g < 3; g++) accr[g] = mfma16(kGbwLds ? gbw[g * 64 + lane] : wt[(MF_GB_IN + g) % kRegTiles], xr, accr[g]);
         }
+        stamp(0);
+        __syncthreads(); /* Y */
+        stamp(1);
+        if (!samp) continue;
+        {
+          /* GRU_B input product (nnet.c:345-353), 48 x 384, all S streams */
+          v4i xk[6];
 #pragma unroll
-        for (int g = 0; g < 3; g++) accr[g] = mfma16(wt[MF_GB_IN + g], xr, accr[g]);
-      }
-      stamp(0);
-      __syncthreads(); /* Y */
-      stamp(1);
-      if (!samp) continue;
-      {
-        /* GRU_B input product (nnet.c:345-353), 48 x 384, all S streams */
-        v4i xk[6];
+          for (int kt = 0; kt < 6; kt++) xk[kt] = *(const v4i *)(xa + sl * MF_XSTR + 64 * kt + 16 * gq);
+          /* z and r tiles first: their sigmoids overlap the h tile's MFMAs */
 #pragma unroll
-        for (int kt = 0; kt < 6; kt++) xk[kt] = *(const v4i *)(xa + sl * MF_XSTR + 64 * kt + 16 * gq);
-        /* z and r tiles first: their sigmoids overlap the h tile's MFMAs */
+          for (int kt = 0; kt < 6; kt++)
 #pragma unroll
-        for (int kt = 0; kt < 6; kt++)
+            for (int g = 0; g < 2; g++) acc[g] = mfma16(wt[g * 6 + kt], xk[kt], acc[g]);
 #pragma unroll
-          for (int g = 0; g < 2; g++) acc[g] = mfma16(wt[g * 6 + kt], xk[kt], acc[g]);
-#pragma unroll
-        for (int kt = 0; kt < 6; kt++) acc[2] = mfma16(wt[12 + kt], xk[kt], acc[2]);
-        stamp(10);
-        /* GRU_B elementwise (nnet.c:362-371), unit gu of stream sl */
-        float zrb[2] = {(float)pick(acc[0]) * kScale1 + (float)pick(accr[0]) * kScale1,
-                        (float)pick(acc[1]) * kScale1 + (float)pick(accr[1]) * kScale1};
-        sigmoid_x86_fin_n<2, true>(zrb, rcp);
-        float hh[1] = {(float)pick(acc[2]) * kScale1 + ((float)pick(accr[2]) * kScale1) * zrb[1]};
-        stamp(14);
-        tanh_x86_n<1, true>(hh, rcp);
-        sbv = zrb[0] * sbv + (1.f - zrb[0]) * hh[0];
-        if (gown) sbuf[gs * NB + gu] = sbv;
-      }
-      stamp(8);
-      /* same-wave LDS exchange: the half of stream ms reads its 16 GRU_B units */
-      __builtin_amdgcn_wave_barrier();
-      float xv[NB];
-      {
-        const float4 *b4 = (const float4 *)(sbuf + ms * NB);
-#pragma unroll
-        for (int j = 0; j < NB / 4; j++) {
-          const float4 v = b4[j];
-          xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
+          for (int kt = 0; kt < 6; kt++) acc[2] = mfma16(wt[12 + kt], xk[kt], acc[2]);
+          stamp(10);
+          /* GRU_B elementwise (nnet.c:362-371), unit gu of stream sl */
+          float zrb[2] = {(float)pick(acc[0]) * kScale1 + (float)pick(accr[0]) * kScale1,
+                          (float)pick(acc[1]) * kScale1 + (float)pick(accr[1]) * kScale1};
+          sigmoid_x86_fin_n<2, true>(zrb, rcp);
+          float hh[1] = {(float)pick(acc[2]) * kScale1 + ((float)pick(accr[2]) * kScale1) * zrb[1]};
+          stamp(14);
+          tanh_x86_n<1, true>(hh, rcp);
+          sbv = zrb[0] * sbv + (1.f - zrb[0]) * hh[0];
+          if (gown) sbuf[gs * NB + gu] = sbv;
         }
-      }
-      stamp(9);
+        stamp(8);
+        /* same-wave LDS exchange: the half of stream ms reads its 16 GRU_B units */
+        __builtin_amdgcn_wave_barrier();
+        float xv[NB];
+        {
+          const float4 *b4 = (const float4 *)(sbuf + ms * NB);
+#pragma unroll
+          for (int j = 0; j < NB / 4; j++) {
+            const float4 v = b4[j];
+            xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
+          }
+        }
+        stamp(9);
 #ifdef MF_WALKFINE
-      auto wst = [&](int k, float v) {
-        if (stamping) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          const int u = __builtin_amdgcn_readfirstlane(__float_as_int(v));
-          asm volatile("" ::"s"(u));
-          stamp(k);
-        }
-      };
-      const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
-                                            deemph, wst);
+        auto wst = [&](int k, float v) {
+          if (stamping) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const int u = __builtin_amdgcn_readfirstlane(__float_as_int(v));
+            asm volatile("" ::"s"(u));
+            stamp(k);
+          }
+        };
+        const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
+                                              deemph, wst);
 #else
-      const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
-                                            deemph);
+        const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
+                                              deemph);
 #endif
-      stamp(11);
-      if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + ms * 4) = make_int4(R.su, R.pu, R.exc, 0);
-      if (tracing && samp_w && hl < 8 && my_active) {
-        float v = R.lg[0];
+        stamp(11);
+        if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + ms * 4) = make_int4(R.su, R.pu, R.exc, 0);
+        if (tracing && samp_w && hl < 8 && my_active) {
+          float v = R.lg[0];
 #pragma unroll
-        for (int b = 1; b < 8; b++) v = hl == b ? R.lg[b] : v;
-        A.trace_logits[((size_t)(s0 + ms) * A.N + n) * 8 + hl] = v;
+          for (int b = 1; b < 8; b++) v = hl == b ? R.lg[b] : v;
+          A.trace_logits[((size_t)(s0 + ms) * A.N + n) * 8 + hl] = v;
+        }
+        if (A.trace_exc && samp_w && hl == 0 && my_active) A.trace_exc[(size_t)(s0 + ms) * A.N + n] = R.exc;
+        pend_pcm = R.pcm;
+        pend_pred = R.pn;
+        pend_exc = R.exc;
+        pend_n = n;
+        stamp(12);
       }
-      if (A.trace_exc && samp_w && hl == 0 && my_active) A.trace_exc[(size_t)(s0 + ms) * A.N + n] = R.exc;
-      pend_pcm = R.pcm;
-      pend_pred = R.pn;
-      pend_exc = R.exc;
-      pend_n = n;
-      stamp(12);
+      if (f + 1 < nfr) {
+        /* frame boundary (multi-frame launches): the last sample's
+         * bookkeeping, then the next frame's LPC, pred and u-law indices as
+         * at a launch start */
+        finish(); /* the GRU_A waves write the frame's PCM out after the frame-start barrier */
+        cf += A.nstreams;
+        /* the lane's stream from an opaque copy of the lane id: the address
+         * is formed here, not hoisted out of the loop into live registers */
+        int lf = lane;
+        asm volatile("" : "+v"(lf));
+        const int msf = S == 4 ? 2 * sw + (lf >> 5) : sw;
+        const float *lp = lpc_of(cf, A, min(s0 + msf, A.nstreams - 1));
+#pragma unroll
+        for (int j = 0; j < NLPC; j++) lpr[j] = lp[j];
+        float p2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < NLPC; j++) p2 = p2 - lsr[j] * lpr[j];
+        pred = p2;
+        if (samp_w && hl == 0) *(int4 *)(ix + ms * 4) = make_int4(lin2ulaw_x86(lsr[0]), lin2ulaw_x86(pred), last_exc, 0);
+      }
     }
     if (samp) finish();
     stamp(4);
@@ -506,12 +586,13 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   }
   if (stamping && lane == 0) {
     stp[6] = __builtin_amdgcn_s_memtime() - t_loop0;
-    stp[7] = (unsigned long long)A.N;
+    stp[7] = (unsigned long long)total;
     for (int k = 0; k < 16; k++) A.stamps[((size_t)blockIdx.x * STAMP_WAVES + wv) * 16 + k] = stp[k];
   }
+  short *pcm_last = A.pcm + (size_t)(nfr - 1) * A.nstreams * A.N;
   for (int e = tid; e < S * A.N; e += MF_THREADS) {
     const int s = e / A.N, n = e % A.N;
-    if (s0 + s < A.nstreams) A.pcm[(size_t)(s0 + s) * A.N + n] = active[s] ? pcmbuf[s * FRAME + n] : (short)0;
+    if (s0 + s < A.nstreams) pcm_last[(size_t)(s0 + s) * A.N + n] = active[s] ? pcmbuf[s * FRAME + n] : (short)0;
   }
 }
 

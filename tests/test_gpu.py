@@ -429,6 +429,61 @@ def test_chunked_frame_network_equals_per_frame(require_gpu, blobs, B, name):
     assert not bad, bad[:8]
 
 
+@pytest.mark.parametrize("B", [1, 2, 70, 256, 1030])
+def test_multi_frame_sample_launches_match_per_frame(require_gpu, blobs, monkeypatch, B):
+    """lpcnet_batch_synthesize_frames on the matrix-core kernel launches the
+    sample kernel once per chunk of frames (SampleArgs::nframes), carrying the
+    states in registers across frames.  Against the per-frame launches
+    (LPCNET_NO_MULTIFRAME) over runs that start at a reset (the FEATURES_DELAY
+    frames go to single-frame launches), follow a per-stream reset and a
+    state restore mid-run, and span chunk boundaries: the PCM and the complete
+    stream state byte for byte, every stream; stream 0 also against the
+    oracle.  The timers count one launch per multi-frame run."""
+    F = 44
+    blob = blobs["streams_int8"]
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    runs = [(0, 6), (6, 40), (40, F)]
+    outs, states = [], []
+    for multi in (False, True):
+        if multi:
+            monkeypatch.delenv("LPCNET_NO_MULTIFRAME", raising=False)
+        else:
+            monkeypatch.setenv("LPCNET_NO_MULTIFRAME", "1")
+        b = L.LPCNetBatch(B, 0, blob)
+        assert b.info().quad_path == 4
+        parts = []
+        for i, (f0, f1) in enumerate(runs):
+            if i == 1:
+                b.reset(B - 1)
+            if i == 2:
+                snap = bytes(b.save_state(0))
+                b.restore_state(0, snap)
+            b.reset_timers(1)
+            parts.append(_frames(b, allf, f0, f1))
+            if multi and i == 1:
+                ms, n = b.kernel_ms(0)
+                # frames 6..37: two single-frame launches (stream B-1 reset) + one of 30;
+                # frames 38..39: below CHUNK_MIN_FRAMES, per frame
+                assert b.kernel_frames(0) == 34 and n == 5, (b.kernel_frames(0), n)
+        outs.append(np.concatenate(parts, 0))
+        states.append([bytes(b.save_state(s)) for s in range(B)])
+        b.close()
+    assert np.abs(outs[0][3:].astype(np.float64)).mean() > 100
+    bad = np.nonzero((outs[1] != outs[0]).any(axis=2))
+    assert not len(bad[0]), list(zip(bad[0][:8], bad[1][:8]))
+    badst = [s for s in range(B) if states[1][s] != states[0][s]]
+    assert not badst, badst[:8]
+    if B <= 2:
+        o = O.Oracle(blob, 0)
+        ref = []
+        for f in range(F):
+            if f == 6 and B == 1:
+                o = O.Oracle(blob, 0)  # stream B-1 = 0 was reset
+            ref.append(o.synthesize(allf[f, 0]))
+        ref = np.stack(ref)
+        assert np.array_equal(outs[1][:, 0], ref)
+
+
 @pytest.mark.parametrize("B,name", [(1, "streams_int8"), (1, "streams_fp32"), (64, "streams_int8"),
                                     (300, "streams_int8")])
 def test_unsynced_frames_then_single_frame(require_gpu, blobs, B, name):
