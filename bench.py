@@ -172,7 +172,10 @@ def roofline(info, B, frame_ms, config, frames_per_launch=1.0):
     bytes_launch = bytes_frame * frames_per_launch
     achieved = bytes_launch / (launch_ms * 1e-3) / 1e9
     pmc, src = measured_pmc(config, info.kernel_name)
-    traffic = pmc.get("hbm_bytes_per_launch")
+    # HBM bytes per launch of frames_per_launch frames (the PMC passes may
+    # have run launches of another length: scale their per-frame figure)
+    traffic = (pmc["hbm_bytes_per_frame"] * frames_per_launch if "hbm_bytes_per_frame" in pmc
+               else pmc.get("hbm_bytes_per_launch"))
     r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
          "traffic": traffic, "kernel": info.kernel_name, "avg_launch_ms": launch_ms,
          "frames_per_launch": frames_per_launch, "ms_per_frame": frame_ms,

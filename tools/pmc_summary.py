@@ -11,7 +11,10 @@ per kernel: median over its non-silent launches of
                          MI355X_MICROARCH.md "HBM")
   l2_hit                 TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
   mfma_util              SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
-bench.py reads it back only when source_sha256 matches the tree it runs from.
+and, for the kernel the pass's bench line names, frames_per_launch (from
+that line: a multi-frame launch covers several frames) and
+hbm_bytes_per_frame.  bench.py reads it back only when source_sha256 matches
+the tree it runs from.
 Usage: pmc_summary.py <gpurun_out dir> <out.json>"""
 import csv
 import glob
@@ -64,10 +67,23 @@ def main(outdir, out):
             rec = res["configs"].setdefault(cfg, {}).setdefault(k, {})
             for c, vals in cs.items():
                 rec[c] = med_nonsilent(vals)
+    fpl = {}
+    for log in glob.glob(os.path.join(outdir, "pmc_*_*.log")):
+        cfg = os.path.basename(log)[:-4].split("_", 2)[2]
+        try:
+            line = json.loads(open(log).read().strip().splitlines()[-1])
+            fpl.setdefault(cfg, {})[line["roofline"]["kernel"]] = float(line["roofline"].get("frames_per_launch", 1.0))
+        except (OSError, ValueError, KeyError, IndexError):
+            pass
     for cfg, ks in res["configs"].items():
         for k, r in ks.items():
+            for name, f in fpl.get(cfg, {}).items():
+                if name in k:
+                    r["frames_per_launch"] = f
             if "FETCH_SIZE" in r and "WRITE_SIZE" in r:
                 r["hbm_bytes_per_launch"] = 2 * r["FETCH_SIZE"] * 1024 + r["WRITE_SIZE"] * 1024
+                if "frames_per_launch" in r:
+                    r["hbm_bytes_per_frame"] = r["hbm_bytes_per_launch"] / r["frames_per_launch"]
             if "TCC_HIT_sum" in r and "TCC_MISS_sum" in r:
                 r["l2_hit"] = r["TCC_HIT_sum"] / max(1.0, r["TCC_HIT_sum"] + r["TCC_MISS_sum"])
             if "SQ_VALU_MFMA_BUSY_CYCLES" in r and "GRBM_GUI_ACTIVE" in r:

@@ -2,7 +2,7 @@
 """Per-kernel launch durations from a rocprofv3 --kernel-trace CSV, with the
 silent launches (the first FEATURES_DELAY frames, which return at once)
 separated, so the average is comparable with bench.py's event-timed
-avg_launch_ms.  Usage: trace_summary.py <run_kernel_trace.csv> [out.json]"""
+avg_launch_ms, per kernel and grid size.  Usage: trace_summary.py <run_kernel_trace.csv> [out.json]"""
 import csv
 import json
 import sys
@@ -14,7 +14,10 @@ def main(path, out=None):
     spans = []
     for r in csv.DictReader(open(path)):
         t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        d[r["Kernel_Name"]].append((t1 - t0) / 1e3)
+        # one entry per (kernel, grid): the same kernel at two batch sizes
+        # (mf_kernel<1> at 1 and 256 streams) are two populations
+        g = r.get("Grid_Size") or r.get("Grid_Size_X") or "?"
+        d[f'{r["Kernel_Name"]} [grid {g}]'].append((t1 - t0) / 1e3)
         spans.append((t0, t1))
     res = {}
     for k, v in d.items():
