@@ -1000,6 +1000,9 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
        * so that some workgroups take each path */
       if (getenv("LPCNET_MF_EXACT")) sa.mf_zr_bound = sa.mf_h_bound = -1.f;
       if (const char *v = getenv("LPCNET_MF_ZR_BOUND")) sa.mf_zr_bound = std::min(sa.mf_zr_bound, (float)atof(v));
+      if (getenv("LPCNET_VERBOSE"))
+        fprintf(stderr, "lpcnet: GRU_A range bounds: z/r %g (bias+diag %g, embeddings %g), h %g\n", sa.mf_zr_bound, bz, ez,
+                sa.mf_h_bound);
     }
     {
       /* embedding tables with their columns in lane order (coalesced gathers) */

@@ -15,7 +15,7 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 lat = d.get("latency", {})
 cp = lat.get("critical_path_cycles", {})
-print("%-10s value %7.2fM frame %.4f ms  cyc/sample %6.0f  %s" % (sys.argv[2], d["value"] / 1e6, d["roofline"]["ms_per_frame"],
+print("%-10s value %7.2fM frame %.4f ms crc %s cyc/sample %6.0f  %s" % (sys.argv[2], d["value"] / 1e6, d["roofline"]["ms_per_frame"], d.get("pcm_checksum"),
       lat.get("cycles_per_sample", 0), " ".join("%s=%.0f" % (k.replace("gru_a_", "A_").replace("sampler_", "S_"), v) for k, v in cp.items())))
 PY
   done
