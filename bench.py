@@ -142,9 +142,11 @@ def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1,
         # steady state of a continuously serving GPU, then reset every stream:
         # the warmup and timed frames below compute exactly what they would
         # without the preheat (same PCM)
+        # (calls of `steps` frames: the same multi-frame launches as the
+        # timed call, so a kernel trace of the run averages one population)
         t_end = time.perf_counter() + preheat_ms * 1e-3
         while time.perf_counter() < t_end:
-            b.synthesize_frames(None, d_feat, d_pcm, F)
+            b.synthesize_frames(None, d_feat, d_pcm, steps)
             b.sync()
         b.reset()
     if warmup:
