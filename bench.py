@@ -247,6 +247,24 @@ def latency(L, blob, B, measured_ms):
             "sampler_post": float(sm[12]),
             "sampler_wait_at_Y": float(sm[1]),
         }
+    elif info.quad_path == 5:
+        # fp_kernel (fp32, one stream per workgroup): hardware wave
+        # FP_SAMPLER_HW = 3 is the sampler, the other six run GRU_A units
+        ga = np.delete(per[:, :7, :], 3, axis=1).mean(axis=0)  # [6][16]
+        sm = per[:, 3, :].mean(axis=0)
+        out["critical_path_cycles"] = {
+            "gru_a_wait_indices": float(ga[:, 0].max()),
+            "gru_a_gathers": float(ga[:, 1].max()),
+            "gru_a_zr_chains_slowest_wave": float(ga[:, 2].max()),
+            "gru_a_elementwise": float(ga[:, 3].max()),
+            "gru_a_h_chain_next": float(ga[:, 8].max()),
+            "sampler_bookkeeping_gru_b_recurrent": float(sm[0]),
+            "sampler_wait_first_units": float(sm[1]),
+            "sampler_gru_b_input_chain": float(sm[2]),
+            "sampler_gru_b_update": float(sm[3]),
+            "sampler_walk": float(sm[4]),
+        }
+    if info.quad_path == 4:
         if os.environ.get("LPCNET_WALK_STAMPS"):
             out["walk_cycles"] = {"level0_3_logit": float(sm[2]), "level0_3_decide_and_w47": float(sm[3]),
                                   "level4_7_logit": float(sm[15]), "decide_select": float(sm[11])}
@@ -332,6 +350,9 @@ def side_line(L, blob, B, args, config, variant_name):
            "kernel": info.kernel_name, "path": variant_name, "roofline": rf}
     if mf:
         out["mfma"] = mf
+    if not args.no_latency:
+        # what binds at this size: the stamped per-sample critical path
+        out["latency"] = latency(L, blob, B, frame_ms)
     return out
 
 
