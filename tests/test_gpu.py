@@ -559,3 +559,16 @@ def test_drop_in_api_error_behaviour(require_gpu, blobs):
     assert L.lib.lpcnet_init(C.c_void_p(net._st)) == 0
     for fr in range(4):
         assert np.array_equal(net.synthesize(G["features"][0, fr]), G["pcm"][0, fr]), fr
+
+
+def test_bench_preheat_computes_the_same_frames(require_gpu, blobs):
+    """bench.py's preheat (untimed load for the clock ramp, then a reset of
+    every stream) leaves the warmup and timed frames exactly as without it."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    blob = blobs["streams_int8"]
+    _, _, _, cold = bench.run_batch(L, blob, 64, 0, 3, 6, None, 1, 0.0)
+    _, _, _, warm = bench.run_batch(L, blob, 64, 0, 3, 6, None, 1, 20.0)
+    assert np.array_equal(cold, warm)
+    assert np.abs(cold[3:].astype(np.int64)).sum() > 0
