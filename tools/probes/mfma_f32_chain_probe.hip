@@ -39,6 +39,41 @@ __global__ void bench(const float *in, float *out, unsigned long long *t)
   if (l == 0) t[0] = t1 - t0;
 }
 
+/* the same chains through the compiler intrinsics (the compiler inserts
+ * whatever wait states the dependent MFMAs need): time per k step */
+template <int MODE>
+__global__ void chain_timed(const float *A, const float *B, float *out, unsigned long long *t, int K)
+{
+  const int l = threadIdx.x;
+  constexpr int R = 32; /* operands in registers, the chain repeated K / R times */
+  float a[R], b[R];
+#pragma unroll
+  for (int k = 0; k < R; k++) { a[k] = A[k * 64 + l]; b[k] = B[k * 64 + l]; }
+  v4f c = {0.f, 0.f, 0.f, 0.f};
+  float y = 0.f;
+  __syncthreads();
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < K / R; i++) {
+    if (MODE == 0) {
+#pragma unroll
+      for (int k = 0; k < R; k++) y = __builtin_fmaf(a[k], b[k], y);
+    }
+    if (MODE == 1) {
+#pragma unroll
+      for (int k = 0; k < R; k++) c = __builtin_amdgcn_mfma_f32_4x4x1f32(a[k], b[k], c, 0, 0, 0);
+    }
+    if (MODE == 2) {
+#pragma unroll
+      for (int k = 0; k < R; k += 4) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k], b[k], c, 0, 0, 0);
+    }
+    asm volatile("" : "+v"(y), "+v"(c));
+  }
+  const float s = y + c.x + c.y + c.z + c.w;
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[l] = s;
+  if (l == 0) t[0] = t1 - t0;
+}
+
 /* 4x4x1 chain over K steps with per-step operands; out[l*4+r] = D */
 __global__ void chain(const float *A, const float *B, float *out, int K)
 {
@@ -96,5 +131,16 @@ int main()
       }
     }
   printf("4x4x1_16b_f32 chain of %d steps vs fmaf: %d of 256 outputs differ\n", K, bad);
+  /* operands from global memory (L1/L2-resident after the first pass) */
+  const char *tn[3] = {"fmaf chain (intrinsic)", "4x4x1_16b_f32 chain (intrinsic)", "16x16x4_f32 chain (intrinsic)"};
+  for (int m = 0; m < 3; m++)
+    for (int rep = 0; rep < 3; rep++) {
+      if (m == 0) hipLaunchKernelGGL(chain_timed<0>, dim3(1), dim3(64), 0, 0, dA, dB, out, t, K);
+      if (m == 1) hipLaunchKernelGGL(chain_timed<1>, dim3(1), dim3(64), 0, 0, dA, dB, out, t, K);
+      if (m == 2) hipLaunchKernelGGL(chain_timed<2>, dim3(1), dim3(64), 0, 0, dA, dB, out, t, K);
+      unsigned long long h;
+      (void)hipMemcpy(&h, t, 8, hipMemcpyDeviceToHost);
+      if (rep == 2) printf("%-34s %.2f per k step (%d steps, operands in registers)\n", tn[m], h / (double)K, K);
+    }
   return 0;
 }
