@@ -450,7 +450,6 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
           }
           y = fma4(a, b, y);
           asm volatile("" : "+v"(y)); /* keep the chain here, not sunk past the flag waits */
-          __builtin_amdgcn_sched_barrier(0);
         }
       }
       stamp(2);
