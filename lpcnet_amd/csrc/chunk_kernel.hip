@@ -16,10 +16,11 @@
  * per-frame frame_kernel's result bit for bit.  tanh is the Pade form with
  * emulated rcpps (device_math.h).
  *
- * Workgroup = 64 columns = CkGeom<NFR>::SC streams x NFR frames (frames
+ * Workgroup = SC streams x NFR frames = 64 columns (80 / 96 for 20 / 24
+ * frames x 4 streams, see launch_chunk) (frames
  * >= nframes are computed on zero inputs and never stored); 8 waves.
- * Layers with 128 rows: wave w owns row tile w for all 4 column tiles (one
- * weight fragment feeds 4 MFMAs).  Projections (1200 rows = 75 tiles): wave w
+ * Layers with 128 rows: wave w owns row tile w for all column tiles (one
+ * weight fragment feeds one MFMA per column tile).  Projections (1200 rows = 75 tiles): wave w
  * owns tiles w, w + 8, ...  Activations live in LDS as [column][input] rows
  * whose stride makes the B-operand reads (16 columns x 4 inputs per
  * wave-instruction) bank-conflict free; weights stream from L2 in the blob's
@@ -36,7 +37,6 @@ namespace lpcnet_mi355x {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int CK_THREADS = 512;
-constexpr int CK_COLS = 64;       /* (stream, frame) columns per workgroup */
 constexpr int CK_RS = COND + 4;   /* row stride of 128-wide activation rows: 4c + k banks */
 constexpr int CK_PROJ = GA_ROWS + GB_ROWS;
 constexpr int CK_PROJ_TILES = CK_PROJ / 16;
@@ -47,15 +47,18 @@ static_assert(CK_PROJ % 16 == 0 && COND == 8 * 16, "row tiles");
 constexpr int ck_stride32(int v) { return v + ((32 - v % 64) + 64) % 64; }
 constexpr int ck_max(int a, int b) { return a > b ? a : b; }
 
-template <int NFR>
+template <int NFR, int SC_>
 struct CkGeom {
-  static constexpr int SC = CK_COLS / NFR;                 /* streams per workgroup */
+  static constexpr int SC = SC_;                           /* streams per workgroup */
+  static constexpr int COLS = SC * NFR;                    /* (stream, frame) columns */
+  static constexpr int NCT = COLS / 16;                    /* column tiles */
+  static_assert(COLS % 16 == 0, "whole column tiles");
   static constexpr int INF = NFR + 2;                      /* frames -2 .. NFR-1 */
   static constexpr int IN_SS = ck_stride32(INF * FIN);     /* conv1 inputs: stream stride */
   static constexpr int C1_SS = ck_stride32(INF * CK_RS);   /* conv1 outputs: stream stride */
-  static constexpr int R0 = ck_max(SC * IN_SS, CK_COLS * CK_RS); /* conv1 inputs, then dense1 outputs */
+  static constexpr int R0 = ck_max(SC * IN_SS, COLS * CK_RS); /* conv1 inputs, then dense1 outputs */
   static constexpr int R1 = SC * C1_SS;
-  static constexpr int R2 = CK_COLS * CK_RS;               /* conv2, then dense2 outputs */
+  static constexpr int R2 = COLS * CK_RS;                  /* conv2, then dense2 outputs */
   static constexpr int FLOATS = R0 + R1 + R2;
 };
 
@@ -64,9 +67,9 @@ struct CkGeom {
  * col = 16 j + (lane & 15), the chain in k order.  X(col, k) =
  * xs[xb[j] + (k / SEG) * SST + k % SEG]: a column's inputs as segments of SEG
  * values SST apart (conv windows over padded frame rows). */
-template <int K, int NOUT, int SEG, int SST>
+template <int K, int NOUT, int SEG, int SST, int NCT>
 __device__ __forceinline__ void ck_tile(const float *__restrict__ W, const float *__restrict__ bias, int rt,
-                                        const float *xs, const int (&xb)[4], f32x4 (&acc)[4])
+                                        const float *xs, const int (&xb)[NCT], f32x4 (&acc)[NCT])
 {
   static_assert(K % 4 == 0 && SEG % 4 == 0, "k quads stay inside a segment");
   constexpr int KS = K / 4;
@@ -79,23 +82,23 @@ __device__ __forceinline__ void ck_tile(const float *__restrict__ W, const float
   for (int d = 0; d < PD; d++) w[d] = wp[(size_t)(4 * d) * NOUT];
   const float4 b4 = *(const float4 *)(bias + 16 * rt + 4 * g);
 #pragma unroll
-  for (int j = 0; j < 4; j++) acc[j] = f32x4{b4.x, b4.y, b4.z, b4.w};
-  float xv[4], xn[4];
+  for (int j = 0; j < NCT; j++) acc[j] = f32x4{b4.x, b4.y, b4.z, b4.w};
+  float xv[NCT], xn[NCT];
 #pragma unroll
-  for (int j = 0; j < 4; j++) xv[j] = xs[xb[j] + g];
+  for (int j = 0; j < NCT; j++) xv[j] = xs[xb[j] + g];
 #pragma unroll
   for (int kk = 0; kk < KS; kk++) {
     if (kk + 1 < KS) {
       const int o = ((4 * (kk + 1)) / SEG) * SST + (4 * (kk + 1)) % SEG;
 #pragma unroll
-      for (int j = 0; j < 4; j++) xn[j] = xs[xb[j] + g + o];
+      for (int j = 0; j < NCT; j++) xn[j] = xs[xb[j] + g + o];
     }
     const float a = w[kk % PD];
 #pragma unroll
-    for (int j = 0; j < 4; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xv[j], acc[j], 0, 0, 0);
+    for (int j = 0; j < NCT; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xv[j], acc[j], 0, 0, 0);
     w[kk % PD] = wp[(size_t)(4 * (kk + PD)) * NOUT];
 #pragma unroll
-    for (int j = 0; j < 4; j++) xv[j] = xn[j];
+    for (int j = 0; j < NCT; j++) xv[j] = xn[j];
   }
 }
 
@@ -103,10 +106,11 @@ __device__ __forceinline__ void ck_tile(const float *__restrict__ W, const float
  * (lpcnet.c:119: incremented while below 1000) */
 __device__ __forceinline__ int ck_fc(int fc0, int f) { return fc0 >= 1000 ? fc0 : min(fc0 + f, 1000); }
 
-template <int NFR>
+template <int NFR, int SC>
 __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
 {
-  using G = CkGeom<NFR>;
+  using G = CkGeom<NFR, SC>;
+  constexpr int NCT = G::NCT;
   extern __shared__ float4 lds4_[];
   float *lds = (float *)lds4_;
   float *inl = lds;          /* [SC][IN_SS]: frame inputs, row f + 2 = frame f (FIN values) */
@@ -156,21 +160,21 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   __syncthreads();
 
   /* this lane's column of each column tile */
-  int cs[4], cf[4];
+  int cs[NCT], cf[NCT];
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
+  for (int j = 0; j < NCT; j++) {
     cs[j] = (16 * j + r) / NFR;
     cf[j] = (16 * j + r) % NFR;
   }
-  int xb[4];
-  f32x4 acc[4];
+  int xb[NCT];
+  f32x4 acc[NCT];
 
   /* conv1 (nnet.c:452-470): 252 inputs -> 128, tanh; cleared while frame_count < 1 (lpcnet.c:99) */
 #pragma unroll
-  for (int j = 0; j < 4; j++) xb[j] = cs[j] * G::IN_SS + cf[j] * FIN; /* window = frames f-2..f */
+  for (int j = 0; j < NCT; j++) xb[j] = cs[j] * G::IN_SS + cf[j] * FIN; /* window = frames f-2..f */
   ck_tile<3 * FIN, COND, 3 * FIN, 3 * FIN>(A.conv1_w, A.conv1_b, wave, inl, xb, acc);
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
+  for (int j = 0; j < NCT; j++) {
     const bool clr = ck_fc(fcs[cs[j]], cf[j]) < 1;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -187,10 +191,10 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   }
   /* conv2: 384 inputs -> 128, tanh; cleared while frame_count < FEATURES_DELAY (lpcnet.c:101) */
 #pragma unroll
-  for (int j = 0; j < 4; j++) xb[j] = cs[j] * G::C1_SS + cf[j] * CK_RS;
+  for (int j = 0; j < NCT; j++) xb[j] = cs[j] * G::C1_SS + cf[j] * CK_RS;
   ck_tile<3 * COND, COND, COND, CK_RS>(A.conv2_w, A.conv2_b, wave, c1, xb, acc);
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
+  for (int j = 0; j < NCT; j++) {
     const bool clr = ck_fc(fcs[cs[j]], cf[j]) < FEATURES_DELAY;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -202,16 +206,16 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
 
   /* dense1, dense2 (lpcnet.c:104-105) */
 #pragma unroll
-  for (int j = 0; j < 4; j++) xb[j] = (16 * j + r) * CK_RS;
+  for (int j = 0; j < NCT; j++) xb[j] = (16 * j + r) * CK_RS;
   ck_tile<COND, COND, COND, CK_RS>(A.dense1_w, A.dense1_b, wave, ya, xb, acc);
 #pragma unroll
-  for (int j = 0; j < 4; j++)
+  for (int j = 0; j < NCT; j++)
 #pragma unroll
     for (int i = 0; i < 4; i++) yb[(16 * j + r) * CK_RS + 16 * wave + 4 * g + i] = tanh_x86(acc[j][i], rcp);
   __syncthreads();
   ck_tile<COND, COND, COND, CK_RS>(A.dense2_w, A.dense2_b, wave, yb, xb, acc);
 #pragma unroll
-  for (int j = 0; j < 4; j++)
+  for (int j = 0; j < NCT; j++)
 #pragma unroll
     for (int i = 0; i < 4; i++) ya[(16 * j + r) * CK_RS + 16 * wave + 4 * g + i] = tanh_x86(acc[j][i], rcp);
   __syncthreads();
@@ -223,7 +227,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   for (int rt = wave; rt < CK_PROJ_TILES; rt += CK_THREADS / 64) {
     ck_tile<COND, CK_PROJ, COND, CK_RS>(A.proj_w, A.proj_b, rt, ya, xb, acc);
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < NCT; j++) {
       const int sid = s0 + cs[j], f = cf[j];
       if (sid >= B || f >= n) continue;
       FrameCond *q = &A.cond[(size_t)f * B + sid];
@@ -278,29 +282,44 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   if (tid < G::SC && s0 + tid < B) A.st[s0 + tid].frame_count = ck_fc(fcs[tid], n);
 }
 
-template <int NFR>
+template <int NFR, int SC>
 static int launch_chunk_t(const FrameArgs &a, void *stream)
 {
-  using G = CkGeom<NFR>;
+  using G = CkGeom<NFR, SC>;
   static bool attr = false;
   const int bytes = G::FLOATS * 4;
   if (!attr) {
-    if (hipFuncSetAttribute((const void *)chunk_kernel<NFR>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) !=
+    if (hipFuncSetAttribute((const void *)chunk_kernel<NFR, SC>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) !=
         hipSuccess)
       return -1;
     attr = true;
   }
   const int grid = (a.nstreams + G::SC - 1) / G::SC;
-  hipLaunchKernelGGL(chunk_kernel<NFR>, dim3(grid), dim3(CK_THREADS), bytes, (hipStream_t)stream, a);
+  hipLaunchKernelGGL((chunk_kernel<NFR, SC>), dim3(grid), dim3(CK_THREADS), bytes, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_chunk(const FrameArgs &a, void *stream)
 {
   if (a.nframes < 1 || a.nframes > LPC_CHUNK || !a.cond) return -1;
-  if (a.nframes <= 8) return launch_chunk_t<8>(a, stream);
-  if (a.nframes <= 16) return launch_chunk_t<16>(a, stream);
-  return launch_chunk_t<32>(a, stream);
+  /* a workgroup's time grows with its column tiles, and the grid runs in
+   * rounds of one workgroup per CU: 17..24 frames as 20 or 24 frames x 4
+   * streams (5 or 6 column tiles) when that turns two rounds of 32 x 2 into
+   * one (at 1024 streams: 20 frames 247 -> ~155 us) */
+  static int cus = 0; /* the node's GPUs are all alike */
+  if (cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  /* estimated time: rounds of workgroups x column tiles per workgroup */
+  auto cost = [&](int sc, int nct) { return ((a.nstreams + sc - 1) / sc + cus - 1) / cus * nct; };
+  if (a.nframes <= 8) return launch_chunk_t<8, 8>(a, stream);
+  if (a.nframes <= 16) return launch_chunk_t<16, 4>(a, stream);
+  if (a.nframes <= 20 && cost(4, 5) < cost(2, 4)) return launch_chunk_t<20, 4>(a, stream);
+  if (a.nframes <= 24 && cost(4, 6) < cost(2, 4)) return launch_chunk_t<24, 4>(a, stream);
+  return launch_chunk_t<32, 2>(a, stream);
 }
 
 }  // namespace lpcnet_mi355x

@@ -408,18 +408,20 @@ def test_batch256_auto_kernel_matches_oracle(require_gpu, blobs):
 def test_chunked_frame_network_equals_per_frame(require_gpu, blobs, B, name):
     """Above 128 streams lpcnet_batch_synthesize_frames runs the frame network
     of up to 32 frames in one chunk_kernel launch (f32 matrix cores).  Runs of
-    37 frames (chunks of 32 and 5: both column layouts) then 3 frames (below
-    CHUNK_MIN_FRAMES: per-frame kernel) must give the PCM and the complete
-    stream state (conv memories, LPC ring, frame_count, conditioning, GRU
-    states, RNG) of the per-frame frame kernel, byte for byte, every stream."""
-    F = 40
+    37 frames (chunks of 32 and 5), 20 and 24 frames (at 1024 streams the 20 x
+    4 and 24 x 4 column layouts), then 3 frames (below CHUNK_MIN_FRAMES:
+    per-frame kernel) must give the PCM and the complete stream state (conv
+    memories, LPC ring, frame_count, conditioning, GRU states, RNG) of the
+    per-frame frame kernel, byte for byte, every stream."""
+    F = 84
     blob = blobs[name]
     allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
     outs, states = [], []
     for chunking in (False, True):
         b = L.LPCNetBatch(B, 0, blob)
         b.set_frame_chunking(chunking)
-        got = np.concatenate([_frames(b, allf, 0, 37), _frames(b, allf, 37, F)], 0)
+        got = np.concatenate([_frames(b, allf, 0, 37), _frames(b, allf, 37, 57), _frames(b, allf, 57, 81),
+                              _frames(b, allf, 81, F)], 0)
         outs.append(got)
         states.append([bytes(b.save_state(s)) for s in range(B)])
         b.close()
