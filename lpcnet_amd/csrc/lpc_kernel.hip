@@ -1,6 +1,6 @@
 /*
  * lpc_kernel.hip -- lpc_from_cepstrum (freq.c:310-320) for every stream of a
- * batch on the GPU: one wavefront per stream, four streams per workgroup.
+ * batch on the GPU: one wavefront per stream, eight streams per workgroup.
  *
  * Restates, term for term and in the reference's operation order:
  *   idct                 freq.c:230-240   lanes 0..17, one band each
@@ -27,7 +27,10 @@ namespace lpcnet_mi355x {
 namespace {
 
 constexpr int NBANDS = LPC_NBANDS, WIN = LPC_WIN;
-constexpr int LPC_STREAMS = 4; /* streams (waves) per workgroup */
+#ifndef LPC_WG_STREAMS
+#define LPC_WG_STREAMS 8
+#endif
+constexpr int LPC_STREAMS = LPC_WG_STREAMS; /* streams (waves) per workgroup */
 
 struct alignas(8) C2 {
   float r, i;
@@ -171,13 +174,16 @@ __global__ __launch_bounds__(64 * LPC_STREAMS) void lpc_kernel(const float *feat
   }
   __syncthreads();
 
-  /* Levinson-Durbin, float build of lpcn_lpc (freq.c:86-127): fully
-   * unrolled, so lpc[] and ac[] stay in registers (a dynamic index into a
-   * register array costs a select chain per access) */
-  if (live && lane == 0) {
+  /* Levinson-Durbin, float build of lpcn_lpc (freq.c:86-127): one lane
+   * per stream of the workgroup, all in wave 0 (the recursion is serial: one
+   * lane of each wave would issue it four times); fully unrolled, so lpc[]
+   * and ac[] stay in registers (a dynamic index into a register array costs
+   * a select chain per access) */
+  const int lsid = blockIdx.x * LPC_STREAMS + lane;
+  if (w == 0 && lane < LPC_STREAMS && lsid < nstreams) {
     float ac[LPC_ORDER1];
 #pragma unroll
-    for (int i = 0; i < LPC_ORDER1; i++) ac[i] = acb[w][i];
+    for (int i = 0; i < LPC_ORDER1; i++) ac[i] = acb[lane][i];
     float lpc[LPC_ORDER1 - 1];
     float err = ac[0];
 #pragma unroll
@@ -201,7 +207,7 @@ __global__ __launch_bounds__(64 * LPC_STREAMS) void lpc_kernel(const float *feat
         if (err < .001f * ac[0]) break;
       }
     }
-    float4 *o = (float4 *)(lpc_out + (size_t)sid * NLPC);
+    float4 *o = (float4 *)(lpc_out + (size_t)lsid * NLPC);
 #pragma unroll
     for (int i = 0; i < NLPC / 4; i++) o[i] = make_float4(lpc[4 * i], lpc[4 * i + 1], lpc[4 * i + 2], lpc[4 * i + 3]);
   }
