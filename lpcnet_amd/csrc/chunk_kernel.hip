@@ -40,7 +40,7 @@ constexpr int CK_THREADS = 512;
 constexpr int CK_RS = COND + 4;   /* row stride of 128-wide activation rows: 4c + k banks */
 constexpr int CK_PROJ = GA_ROWS + GB_ROWS;
 constexpr int CK_PROJ_TILES = CK_PROJ / 16;
-static_assert(CK_PROJ % 16 == 0 && COND == 8 * 16, "row tiles");
+static_assert(CK_PROJ % 16 == 0 && GA_ROWS % 16 == 0 && COND == 8 * 16, "row tiles");
 
 /* smallest stride >= v that is 32 mod 64 floats: a 16-column tile that spans
  * two streams (NFR = 8) then reads 64 distinct banks */
@@ -232,18 +232,14 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
       if (sid >= B || f >= n) continue;
       FrameCond *q = &A.cond[(size_t)f * B + sid];
       StreamState *p = &A.st[sid];
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int row = 16 * rt + 4 * g + i;
-        const float v = acc[j][i];
-        if (row < GA_ROWS) {
-          q->gru_a_cond[row] = v;
-          if (f == n - 1) p->gru_a_cond[row] = v;
-        } else {
-          q->gru_b_cond[row - GA_ROWS] = v;
-          if (f == n - 1) p->gru_b_cond[row - GA_ROWS] = v;
-        }
-      }
+      /* this lane's 4 consecutive rows as one 16-byte store: the 4 lanes of
+       * a column write its 16 rows as one 64-byte run (GA_ROWS is a multiple
+       * of 16, so a row quad never straddles the two arrays) */
+      const int row = 16 * rt + 4 * g;
+      const float4 v = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+      float *qd = row < GA_ROWS ? q->gru_a_cond + row : q->gru_b_cond + (row - GA_ROWS);
+      *(float4 *)qd = v;
+      if (f == n - 1) *(float4 *)(row < GA_ROWS ? p->gru_a_cond + row : p->gru_b_cond + (row - GA_ROWS)) = v;
     }
   }
 
