@@ -14,7 +14,8 @@
  * MFMA) -- the sequential fmaf chain of sgemv_accum16 (vec_avx.h:618-643)
  * started from the bias, so a row chained over its inputs 4 at a time is the
  * per-frame frame_kernel's result bit for bit.  tanh is the Pade form with
- * emulated rcpps (device_math.h).
+ * rcpps from the hardware reciprocal (rcp_x86_hw, proven equal to the x86
+ * table: device_math.h), no table read from memory.
  *
  * Workgroup = SC streams x NFR frames = 64 columns (80 / 96 for 20 / 24
  * frames x 4 streams, see launch_chunk) (frames
@@ -176,11 +177,12 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
 #pragma unroll
   for (int j = 0; j < NCT; j++) {
     const bool clr = ck_fc(fcs[cs[j]], cf[j]) < 1;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const float t = tanh_x86(acc[j][i], rcp);
-      c1[cs[j] * G::C1_SS + (cf[j] + 2) * CK_RS + 16 * wave + 4 * g + i] = clr ? 0.f : t;
-    }
+    float4 t;
+    t.x = clr ? 0.f : tanh_x86<true>(acc[j][0], rcp);
+    t.y = clr ? 0.f : tanh_x86<true>(acc[j][1], rcp);
+    t.z = clr ? 0.f : tanh_x86<true>(acc[j][2], rcp);
+    t.w = clr ? 0.f : tanh_x86<true>(acc[j][3], rcp);
+    *(float4 *)&c1[cs[j] * G::C1_SS + (cf[j] + 2) * CK_RS + 16 * wave + 4 * g] = t;
   }
   __syncthreads();
 
@@ -196,11 +198,12 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
 #pragma unroll
   for (int j = 0; j < NCT; j++) {
     const bool clr = ck_fc(fcs[cs[j]], cf[j]) < FEATURES_DELAY;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const float t = tanh_x86(acc[j][i], rcp);
-      ya[(16 * j + r) * CK_RS + 16 * wave + 4 * g + i] = clr ? 0.f : t;
-    }
+    float4 t;
+    t.x = clr ? 0.f : tanh_x86<true>(acc[j][0], rcp);
+    t.y = clr ? 0.f : tanh_x86<true>(acc[j][1], rcp);
+    t.z = clr ? 0.f : tanh_x86<true>(acc[j][2], rcp);
+    t.w = clr ? 0.f : tanh_x86<true>(acc[j][3], rcp);
+    *(float4 *)&ya[(16 * j + r) * CK_RS + 16 * wave + 4 * g] = t;
   }
   __syncthreads();
 
@@ -210,14 +213,16 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   ck_tile<COND, COND, COND, CK_RS>(A.dense1_w, A.dense1_b, wave, ya, xb, acc);
 #pragma unroll
   for (int j = 0; j < NCT; j++)
-#pragma unroll
-    for (int i = 0; i < 4; i++) yb[(16 * j + r) * CK_RS + 16 * wave + 4 * g + i] = tanh_x86(acc[j][i], rcp);
+    *(float4 *)&yb[(16 * j + r) * CK_RS + 16 * wave + 4 * g] =
+        make_float4(tanh_x86<true>(acc[j][0], rcp), tanh_x86<true>(acc[j][1], rcp), tanh_x86<true>(acc[j][2], rcp),
+                    tanh_x86<true>(acc[j][3], rcp));
   __syncthreads();
   ck_tile<COND, COND, COND, CK_RS>(A.dense2_w, A.dense2_b, wave, yb, xb, acc);
 #pragma unroll
   for (int j = 0; j < NCT; j++)
-#pragma unroll
-    for (int i = 0; i < 4; i++) ya[(16 * j + r) * CK_RS + 16 * wave + 4 * g + i] = tanh_x86(acc[j][i], rcp);
+    *(float4 *)&ya[(16 * j + r) * CK_RS + 16 * wave + 4 * g] =
+        make_float4(tanh_x86<true>(acc[j][0], rcp), tanh_x86<true>(acc[j][1], rcp), tanh_x86<true>(acc[j][2], rcp),
+                    tanh_x86<true>(acc[j][3], rcp));
   __syncthreads();
 
   /* conditioning projections (lpcnet.c:106-107), linear: gadf | gbdf as one
