@@ -86,7 +86,7 @@ def test_single_stream_api_matches_golden(require_gpu, blobs):
                                             (1100, (1099, 1024, 5), 1), (1024, (0, 3, 517, 1023), 0),
                                             (1101, (1100, 1024, 5), 0), (300, (299, 7), 0),
                                             (513, (512, 1, 300), 4), (1030, (1029, 1027, 2), 4),
-                                            (1024, (0, 511, 1023), 4)])
+                                            (1024, (0, 511, 1023), 4), (4096, (0, 2047, 4095), 4)])
 def test_large_batch_streams_match_oracle(require_gpu, blobs, B, check, kernel):
     """Lockstep kernel at 2 and 4 streams/workgroup, mf_kernel at 1, 2 and 4
     streams/workgroup, ragged last workgroups, against the oracle."""
@@ -404,7 +404,7 @@ def test_batch256_auto_kernel_matches_oracle(require_gpu, blobs):
 
 
 @pytest.mark.parametrize("B,name", [(129, "streams_int8"), (256, "streams_int8"), (1024, "streams_int8"),
-                                    (200, "streams_fp32")])
+                                    (2050, "streams_int8"), (200, "streams_fp32")])
 def test_chunked_frame_network_equals_per_frame(require_gpu, blobs, B, name):
     """Above 128 streams lpcnet_batch_synthesize_frames runs the frame network
     of up to 32 frames in one chunk_kernel launch (f32 matrix cores).  Runs of
