@@ -43,8 +43,9 @@ $(BUILD)/frame_kernel.o: $(CSRC)/frame_kernel.hip $(HDRS) | $(BUILD)
 $(BUILD)/mf_kernel.o: $(CSRC)/mf_kernel.hip $(HDRS) | $(BUILD)
 	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -fno-slp-vectorize -c $< -o $@
 
+# the fp32 chains schedule better under the max-ILP machine scheduler (batch-1 fp32 +0.6 %)
 $(BUILD)/fp_kernel.o: $(CSRC)/fp_kernel.hip $(HDRS) | $(BUILD)
-	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -c $< -o $@
+	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -mllvm -amdgpu-sched-strategy=max-ilp -c $< -o $@
 
 $(BUILD)/selftest.o: $(CSRC)/selftest.hip $(HDRS) | $(BUILD)
 	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -c $< -o $@
