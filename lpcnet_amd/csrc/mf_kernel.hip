@@ -335,22 +335,42 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         {
           /* GRU_A input (nnet.c:484-491): all 9*S gathers in flight at once */
           float e[S][9];
-          for (int s = 0; s < S; s++) {
-            /* the indices are the same in every lane: scalar row addresses */
-            const int4 v = *(const int4 *)(ix + s * 4);
-            const float *e1 = A.mf_emb[0] + (__builtin_amdgcn_readfirstlane(v.x) & 0xFF) * GA_ROWS;
-            const float *e2 = A.mf_emb[1] + (__builtin_amdgcn_readfirstlane(v.y) & 0xFF) * GA_ROWS;
-            const float *e3 = A.mf_emb[2] + (__builtin_amdgcn_readfirstlane(v.z) & 0xFF) * GA_ROWS;
-            /* scalar row base + unsigned 32-bit lane offset + immediate: the
-             * global_load saddr form, no vector address arithmetic per row */
-            uint32_t ub = (uint32_t)tid * 4u;
-            asm volatile("" : "+v"(ub)); /* opaque per row: not reassociated into table + lane pairs */
-            const char *b1 = (const char *)e1, *b2 = (const char *)e2, *b3 = (const char *)e3;
+          if constexpr (S > 1) {
+            for (int s = 0; s < S; s++) {
+              /* table base in SGPRs, row + lane offset in one 32-bit VGPR: the
+               * global_load saddr form with no scalar address chain per row
+               * (gathers 1,520 -> 1,435 cycles at 4 streams; neutral at 1) */
+              const int4 v = *(const int4 *)(ix + s * 4);
+              uint32_t o1 = (uint32_t)tid * 4u + (uint32_t)(v.x & 0xFF) * (GA_ROWS * 4u);
+              uint32_t o2 = (uint32_t)tid * 4u + (uint32_t)(v.y & 0xFF) * (GA_ROWS * 4u);
+              uint32_t o3 = (uint32_t)tid * 4u + (uint32_t)(v.z & 0xFF) * (GA_ROWS * 4u);
+              asm volatile("" : "+v"(o1), "+v"(o2), "+v"(o3));
+              const char *b1 = (const char *)A.mf_emb[0], *b2 = (const char *)A.mf_emb[1], *b3 = (const char *)A.mf_emb[2];
 #pragma unroll
-            for (uint32_t g = 0; g < 3; g++) {
-              e[s][g] = *(const float *)(b1 + ub + g * NA * 4u);
-              e[s][3 + g] = *(const float *)(b2 + ub + g * NA * 4u);
-              e[s][6 + g] = *(const float *)(b3 + ub + g * NA * 4u);
+              for (uint32_t g = 0; g < 3; g++) {
+                e[s][g] = *(const float *)(b1 + o1 + g * NA * 4u);
+                e[s][3 + g] = *(const float *)(b2 + o2 + g * NA * 4u);
+                e[s][6 + g] = *(const float *)(b3 + o3 + g * NA * 4u);
+              }
+            }
+          } else {
+            for (int s = 0; s < S; s++) {
+              /* the indices are the same in every lane: scalar row addresses */
+              const int4 v = *(const int4 *)(ix + s * 4);
+              const float *e1 = A.mf_emb[0] + (__builtin_amdgcn_readfirstlane(v.x) & 0xFF) * GA_ROWS;
+              const float *e2 = A.mf_emb[1] + (__builtin_amdgcn_readfirstlane(v.y) & 0xFF) * GA_ROWS;
+              const float *e3 = A.mf_emb[2] + (__builtin_amdgcn_readfirstlane(v.z) & 0xFF) * GA_ROWS;
+              /* scalar row base + unsigned 32-bit lane offset + immediate: the
+               * global_load saddr form, no vector address arithmetic per row */
+              uint32_t ub = (uint32_t)tid * 4u;
+              asm volatile("" : "+v"(ub)); /* opaque per row: not reassociated into table + lane pairs */
+              const char *b1 = (const char *)e1, *b2 = (const char *)e2, *b3 = (const char *)e3;
+#pragma unroll
+              for (uint32_t g = 0; g < 3; g++) {
+                e[s][g] = *(const float *)(b1 + ub + g * NA * 4u);
+                e[s][3 + g] = *(const float *)(b2 + ub + g * NA * 4u);
+                e[s][6 + g] = *(const float *)(b3 + ub + g * NA * 4u);
+              }
             }
           }
           if (stamping) {
