@@ -341,9 +341,9 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
                * global_load saddr form with no scalar address chain per row
                * (gathers 1,520 -> 1,435 cycles at 4 streams; neutral at 1) */
               const int4 v = *(const int4 *)(ix + s * 4);
-              uint32_t o1 = (uint32_t)tid * 4u + (uint32_t)(v.x & 0xFF) * (GA_ROWS * 4u);
-              uint32_t o2 = (uint32_t)tid * 4u + (uint32_t)(v.y & 0xFF) * (GA_ROWS * 4u);
-              uint32_t o3 = (uint32_t)tid * 4u + (uint32_t)(v.z & 0xFF) * (GA_ROWS * 4u);
+              uint32_t o1 = (uint32_t)tid * 4u + (uint32_t)v.x;
+              uint32_t o2 = (uint32_t)tid * 4u + (uint32_t)v.y;
+              uint32_t o3 = (uint32_t)tid * 4u + (uint32_t)v.z;
               asm volatile("" : "+v"(o1), "+v"(o2), "+v"(o3));
               const char *b1 = (const char *)A.mf_emb[0], *b2 = (const char *)A.mf_emb[1], *b3 = (const char *)A.mf_emb[2];
 #pragma unroll
@@ -463,13 +463,19 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     FcLane F;
     F.init(img, lane);
     put_xb();
+    /* the sig/pred/exc indices as the GRU_A waves consume them: at S > 1
+     * the byte offsets of the three embedding rows (the gathers add the lane
+     * offset only), at S = 1 the indices */
+    auto ix_word = [](int su, int pu, int exc) {
+      return S > 1 ? make_int4(su * (GA_ROWS * 4), pu * (GA_ROWS * 4), exc * (GA_ROWS * 4), 0) : make_int4(su, pu, exc, 0);
+    };
     if (samp) {
       /* pred and the u-law indices of the first sample (lpcnet.c:252-254) */
       float p2 = 0.f;
 #pragma unroll
       for (int j = 0; j < NLPC; j++) p2 = p2 - lsr[j] * lpr[j];
       pred = p2;
-      if (samp_w && hl == 0) *(int4 *)(ix + ms * 4) = make_int4(lin2ulaw_x86(lsr[0]), lin2ulaw_x86(pred), last_exc, 0);
+      if (samp_w && hl == 0) *(int4 *)(ix + ms * 4) = ix_word(lin2ulaw_x86(lsr[0]), lin2ulaw_x86(pred), last_exc);
     }
     __syncthreads(); /* initial q(h_A), q(h_B), ix, seeds */
     stamp_start();
@@ -579,7 +585,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
                                               deemph);
 #endif
         stamp(11);
-        if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + ms * 4) = make_int4(R.su, R.pu, R.exc, 0);
+        if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + ms * 4) = ix_word(R.su, R.pu, R.exc);
         if (tracing && samp_w && hl < 8 && my_active) {
           float v = R.lg[0];
 #pragma unroll
@@ -611,7 +617,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
 #pragma unroll
         for (int j = 0; j < NLPC; j++) p2 = p2 - lsr[j] * lpr[j];
         pred = p2;
-        if (samp_w && hl == 0) *(int4 *)(ix + ms * 4) = make_int4(lin2ulaw_x86(lsr[0]), lin2ulaw_x86(pred), last_exc, 0);
+        if (samp_w && hl == 0) *(int4 *)(ix + ms * 4) = ix_word(lin2ulaw_x86(lsr[0]), lin2ulaw_x86(pred), last_exc);
       }
     }
     if (samp) finish();
