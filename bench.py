@@ -286,23 +286,26 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(seconds):
+def cpu_baseline(seconds, variant=0):
     """The reference's own AVX2 kernels (oracle/_ref, compiled from the
     reference sources) driven by the oracle's lpcnet.c/nnet.c restatement,
     one stream per worker thread, one worker pinned per host core this
     process may use.  On the GPU box that is the harness's CPU share for one
     GPU (OMP_NUM_THREADS = 16 there; the affinity mask shows the whole
-    machine), so `per_core` is the number to scale to a node."""
+    machine), so `per_core` is the number to scale to a node.  variant 1:
+    the reference's --disable-dot-product build (fp32 GRU weights,
+    vec_avx.h:861-904 compiled with DISABLE_DOT_PROD), beside configs[1]'s
+    batch1_fp32 line."""
     import lpcnet_amd as L
     import oracle_lib as O
     kind = "reference" if O.have_ref() else "port"
     kernels = O.ref_kernels() if O.have_ref() else None
-    blob = L.synthetic_model(1, 0)
+    blob = L.synthetic_model(1, variant)
     cpus = sorted(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     threads = max(1, min(len(cpus), share) if share > 0 else len(cpus))
     # warm the lazily built tables on one thread first
-    O.Oracle(blob, 0, kernels).synthesize(L.synthetic_features(0, 1)[0])
+    O.Oracle(blob, variant, kernels).synthesize(L.synthetic_features(0, 1)[0])
     frames_done = [0] * threads
     stop = [False]
 
@@ -311,7 +314,7 @@ def cpu_baseline(seconds):
             os.sched_setaffinity(threading.get_native_id(), {cpus[t % len(cpus)]})
         except OSError:
             pass
-        o = O.Oracle(blob, 0, kernels)
+        o = O.Oracle(blob, variant, kernels)
         f = L.synthetic_features(1000 + t, 64)
         k = 0
         while not stop[0]:
@@ -333,7 +336,8 @@ def cpu_baseline(seconds):
     return {"value": value, "unit": "samples/s", "cores": threads, "kind": kind,
             "per_core": value / threads, "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "affinity_cpus": len(cpus),
-            "sample": f"{threads} pinned threads x 1 stream each (one per core of this process's CPU share), int8 "
+            "sample": f"{threads} pinned threads x 1 stream each (one per core of this process's CPU share), "
+                      f"{'fp32 (--disable-dot-product)' if variant else 'int8'} "
                       f"synthetic model, {frames} frames in {dt:.1f}s "
                       f"({'reference vec_avx.h/kiss99/freq.c kernels compiled from /root/reference/src' if kind == 'reference' else 'portable oracle'}"
                       f" + oracle restatement of lpcnet.c/nnet.c; restatement/reference speed ratio: BASELINE.md section 3)"}
@@ -411,6 +415,8 @@ def main():
         out["batch256"] = side_line(L, blob, 256, args, "b256", "int8")
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        # beside batch1_fp32 (configs[1]): the reference's fp32 build on the same cores
+        out["cpu_baseline_fp32"] = cpu_baseline(args.cpu_seconds, 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

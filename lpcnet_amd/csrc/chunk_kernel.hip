@@ -287,14 +287,8 @@ template <int NFR, int SC>
 static int launch_chunk_t(const FrameArgs &a, void *stream)
 {
   using G = CkGeom<NFR, SC>;
-  static bool attr = false;
   const int bytes = G::FLOATS * 4;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void *)chunk_kernel<NFR, SC>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) !=
-        hipSuccess)
-      return -1;
-    attr = true;
-  }
+  if (ensure_dyn_lds((const void *)chunk_kernel<NFR, SC>, bytes)) return -1;
   const int grid = (a.nstreams + G::SC - 1) / G::SC;
   hipLaunchKernelGGL((chunk_kernel<NFR, SC>), dim3(grid), dim3(CK_THREADS), bytes, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -307,13 +301,7 @@ int launch_chunk(const FrameArgs &a, void *stream)
    * rounds of one workgroup per CU: 17..24 frames as 20 or 24 frames x 4
    * streams (5 or 6 column tiles) when that turns two rounds of 32 x 2 into
    * one (at 1024 streams: 20 frames 247 -> ~155 us) */
-  static int cus = 0; /* the node's GPUs are all alike */
-  if (cus <= 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      cus = 256;
-  }
+  const int cus = current_device_cus();
   /* estimated time: rounds of workgroups x column tiles per workgroup */
   auto cost = [&](int sc, int nct) { return ((a.nstreams + sc - 1) / sc + cus - 1) / cus * nct; };
   if (a.nframes <= 8) return launch_chunk_t<8, 8>(a, stream);

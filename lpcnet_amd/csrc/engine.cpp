@@ -25,7 +25,9 @@
 #include <cstddef>
 #include <atomic>
 #include <functional>
+#include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -244,6 +246,40 @@ void build_lpc_tables(LpcTables &T)
 }
 
 }  // namespace
+
+/* ---- launcher helpers (lpcnet_engine.h), keyed by the current device ---- */
+namespace lpcnet_mi355x {
+
+int ensure_dyn_lds(const void *kernel, int bytes)
+{
+  static std::mutex mu;
+  static std::map<std::pair<const void *, int>, int> done; /* (kernel, device) -> bytes set */
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  std::lock_guard<std::mutex> lk(mu);
+  int &have = done[{kernel, dev}];
+  if (have >= bytes) return 0;
+  if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) return -1;
+  have = bytes;
+  return 0;
+}
+
+int current_device_cus()
+{
+  static std::mutex mu;
+  static std::map<int, int> cus;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cus.find(dev);
+  if (it != cus.end()) return it->second;
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  cus[dev] = n;
+  return n;
+}
+
+}  // namespace lpcnet_mi355x
 
 /* ------------------------------------------------------------------------ */
 struct LPCNetBatch {
@@ -1360,9 +1396,8 @@ LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
   if (ok) *b->h_status = 0;
   ok = ok && hipMalloc(&b->d_lpc, sizeof(float) * NLPC * (size_t)nb_streams * LPC_CHUNK) == hipSuccess;
   ok = ok && hipMalloc(&b->d_lpc_tab, sizeof(LpcTables)) == hipSuccess;
-  /* frame-network outputs of a chunk of frames (chunk_kernel -> multi-frame
-   * sample launches): allocated here, not inside the first synthesize call */
-  ok = ok && hipMalloc(&b->d_chunk, sizeof(FrameCond) * (size_t)LPC_CHUNK * nb_streams) == hipSuccess;
+  /* d_chunk (the chunked path's frame outputs, LPC_CHUNK x 4.9 KB per
+   * stream) is allocated by the first call that takes that path */
   if (ok) {
     LpcTables T;
     build_lpc_tables(T);
@@ -1518,6 +1553,12 @@ LPCNET_EXPORT int lpcnet_batch_restore_state(LPCNetBatch *b, int stream, const v
       set_err("snapshot GRU state outside [-2, 2]: not a state this engine produced");
       return -1;
     }
+    /* last_exc indexes the 256-row embedding tables (lpcnet.c:264: an
+     * excitation is a u-law byte) */
+    if (tmp.last_exc < 0 || tmp.last_exc > 255) {
+      set_err("snapshot last_exc outside [0, 255]: not a state this engine produced");
+      return -1;
+    }
   }
   HIPCHK(hipStreamSynchronize(b->stream));
   HIPCHK(hipMemcpy(&b->d_state[stream], buf, sizeof(StreamState), hipMemcpyHostToDevice));
@@ -1556,6 +1597,16 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
    * ones reading FrameCond) */
   const bool chunked = mfm || (!ovl && b->chunking && (b->mf || b->fp) && b->B > OVERLAP_MAX_STREAMS && !b->d_stamps &&
                                !getenv("LPCNET_NO_CHUNK"));
+  if (chunked && !b->d_chunk) {
+    /* frame-network outputs of a chunk of frames (chunk_kernel -> sample
+     * launches): sizeof(FrameCond) = 4.9 KB x LPC_CHUNK per stream (160 MB
+     * at 1024 streams), only for batches that take this path */
+    if (hipMalloc(&b->d_chunk, sizeof(FrameCond) * (size_t)LPC_CHUNK * b->B) != hipSuccess) {
+      b->d_chunk = nullptr;
+      set_err("device allocation of the chunked frame-network buffer failed");
+      return -1;
+    }
+  }
   hipStream_t fs = ovl ? b->fstream : b->stream;
   for (int c0 = 0; c0 < nframes; c0 += LPC_CHUNK) {
     /* lpc_from_cepstrum depends only on the features: one launch for up to
@@ -1602,7 +1653,8 @@ LPCNET_EXPORT int lpcnet_batch_set_frame_chunking(LPCNetBatch *b, int enable)
 LPCNET_EXPORT int lpcnet_batch_set_spin_limit(LPCNetBatch *b, int polls)
 {
   if (!b || polls < 0) return -1;
-  b->spin_limit = polls == 0 ? FLAG_SPIN_LIMIT_DEFAULT : polls;
+  /* clamped: the kernels' poll counter must be able to exceed the limit */
+  b->spin_limit = polls == 0 ? FLAG_SPIN_LIMIT_DEFAULT : std::min(polls, FLAG_SPIN_LIMIT_MAX);
   return 0;
 }
 
@@ -1761,14 +1813,26 @@ static const uint32_t kMagic = 0x4c50434eu; /* "LPCN" */
 
 LPCNET_EXPORT int lpcnet_get_size(void) { return (int)sizeof(LPCNetState); }
 
+/* Handles initialised by lpcnet_init and not yet destroyed.  lpcnet_init is
+ * called on raw caller memory (lpcnet_get_size + malloc, as the reference's
+ * decoder does), so its contents are never trusted to tell a live handle
+ * from garbage: only this registry does. */
+static std::mutex g_live_mu;
+static std::set<LPCNetState *> g_live;
+
 LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
 {
+  if (!st) return -1;
   /* src/lpcnet.c:184-200 ends with lpcnet_reset(): re-initialising a live
    * handle (from lpcnet_create / an earlier lpcnet_init) resets its streams
    * and keeps its device binding and model; anything else is a fresh handle */
-  if (st->magic == kMagic && st->batch) {
-    lpcnet_batch_reset(st->batch);
-    return 0;
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    if (g_live.count(st)) {
+      if (st->batch) lpcnet_batch_reset(st->batch);
+      return 0;
+    }
+    g_live.insert(st);
   }
   st->magic = kMagic;
   const char *d = getenv("LPCNET_DEVICE");
@@ -1787,7 +1851,15 @@ LPCNET_EXPORT LPCNetState *lpcnet_create(void)
 LPCNET_EXPORT void lpcnet_destroy(LPCNetState *st)
 {
   if (!st) return;
-  if (st->magic == kMagic && st->batch) lpcnet_batch_destroy(st->batch);
+  bool live;
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    live = g_live.erase(st) > 0;
+  }
+  if (live && st->batch) lpcnet_batch_destroy(st->batch);
+  /* a later malloc may hand this block out again: leave nothing that looks live */
+  st->magic = 0;
+  st->batch = nullptr;
   free(st);
 }
 

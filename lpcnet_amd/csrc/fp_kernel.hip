@@ -359,7 +359,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
       lpr[j] = lpc_of(A, sid)[j];
     }
     float deemph = ps->deemph_mem, pred = 0.f;
-    int last_exc = ps->last_exc;
+    int last_exc = ps->last_exc & 0xFF;
     uint32_t rz = ps->rng[0], rw = ps->rng[1], rj = ps->rng[2], rc = ps->rng[3];
     float xv[NB]; /* GRU_B state, every lane */
 #pragma unroll
@@ -528,13 +528,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
 template <bool TRACE>
 static int launch_fp_t(const SampleArgs &a, hipStream_t stream)
 {
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)fp_kernel<TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - IMG_VAR) !=
-        hipSuccess)
-      return -1;
-    attr_set = true;
-  }
+  if (ensure_dyn_lds((const void *)fp_kernel<TRACE>, 160 * 1024 - IMG_VAR)) return -1;
   hipLaunchKernelGGL((fp_kernel<TRACE>), dim3(warm_grid(a.nstreams, a.nstreams)), dim3(FP_THREADS), fp_lds_bytes() - IMG_VAR, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

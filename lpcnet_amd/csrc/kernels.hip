@@ -249,7 +249,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
     sbv = p->gru_b_state[lane & (NB - 1)];
     for (int k = lane; k < GB_ROWS; k += 64) condb[my_s * GB_ROWS + k] = p->gru_b_cond[k];
     deemph = p->deemph_mem;
-    last_exc = p->last_exc;
+    last_exc = p->last_exc & 0xFF;
     rz = p->rng[0]; rw = p->rng[1]; rj = p->rng[2]; rc = p->rng[3];
   }
   __syncthreads(); /* image in LDS */
@@ -640,13 +640,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
 template <int S, int V, bool SAT, bool REG>
 static int launch_sample_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
 {
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)sample_kernel<S, V, SAT, REG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return -1;
-    attr_set = true;
-  }
+  if (ensure_dyn_lds((const void *)sample_kernel<S, V, SAT, REG>, 160 * 1024)) return -1;
   int grid = (a.nstreams + S - 1) / S;
   hipLaunchKernelGGL((sample_kernel<S, V, SAT, REG>), dim3(grid), dim3(SAMPLE_THREADS), lds_bytes, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;

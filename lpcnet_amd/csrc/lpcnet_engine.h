@@ -194,6 +194,7 @@ struct SampleArgs {
 };
 
 constexpr int FLAG_SPIN_LIMIT_DEFAULT = 1 << 20; /* lpcnet_batch_set_spin_limit */
+constexpr int FLAG_SPIN_LIMIT_MAX = 1 << 30;     /* larger requests are clamped (int poll counters) */
 /* Status bits a sample kernel reports to the host (SampleArgs::status). */
 constexpr int STATUS_FLAG_TIMEOUT = 1; /* an LDS flag wait exceeded spin_limit: output invalid */
 constexpr int STATUS_ACTIVITY = 2;     /* a multi-frame launch saw a stream become active mid-launch */
@@ -235,6 +236,12 @@ __device__ __forceinline__ const float *lpc_of(const SampleArgs &A, int sid)
   return A.cond ? A.cond[sid].lpc : A.st[sid].lpc;
 }
 #endif
+
+/* Host helpers shared by the launchers (engine.cpp), thread-safe and keyed
+ * by the current HIP device: raise a kernel's dynamic-LDS limit to `bytes`
+ * once per (kernel, device); the CU count of the current device. */
+int ensure_dyn_lds(const void *kernel, int bytes);
+int current_device_cus();
 
 /* Kernel launchers (kernels.hip).  variant: 0 int8, 1 fp32. sat: int8 pairs
  * may saturate. lds_bytes from sample_lds_bytes(). */

@@ -436,7 +436,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         lpr[j] = lpc_of(A, min(s0 + ms, A.nstreams - 1))[j];
       }
       deemph = p->deemph_mem;
-      last_exc = p->last_exc;
+      last_exc = p->last_exc & 0xFF; /* the gathers index 256-row tables: never out of bounds (restore_state also rejects such snapshots) */
       rz = p->rng[0]; rw = p->rng[1]; rj = p->rng[2]; rc = p->rng[3];
     }
     float sbv = A.st[min(s0 + sl, A.nstreams - 1)].gru_b_state[gu];
@@ -649,13 +649,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
 template <int S, bool TRACE>
 static int launch_mf_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
 {
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)mf_kernel<S, TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - IMG_VAR) !=
-        hipSuccess)
-      return -1;
-    attr_set = true;
-  }
+  if (ensure_dyn_lds((const void *)mf_kernel<S, TRACE>, 160 * 1024 - IMG_VAR)) return -1;
   const int grid = warm_grid((a.nstreams + S - 1) / S, a.nstreams);
   /* lds_bytes counts the static image too (mf_lds_bytes) */
   hipLaunchKernelGGL((mf_kernel<S, TRACE>), dim3(grid), dim3(MF_THREADS), lds_bytes - IMG_VAR, stream, a);

@@ -102,10 +102,15 @@ def _engine_worker(rank, world, port, out, per_rank, frames):
 
 
 @pytest.mark.gpu
-def test_two_rank_engine_shard_invariance(require_gpu):
+@pytest.mark.parametrize("per_rank,frames", [(96, 6), (1024, 10)])
+def test_two_rank_engine_shard_invariance(require_gpu, per_rank, frames):
+    """per_rank 96: mf_kernel<1> with the overlapped per-frame frame kernel
+    (<= 128 streams); per_rank 1024 is BASELINE configs[4]'s own per-GPU
+    size: each rank runs mf_kernel<4>, the chunked frame network and the
+    multi-frame sample launches, exactly as `bench.py --gpus N` does."""
     import bench
     import lpcnet_amd as L
-    per_rank, frames, world = 96, 6, 2
+    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -117,7 +122,17 @@ def test_two_rank_engine_shard_invariance(require_gpu):
         p.join(timeout=60)
         assert p.exitcode == 0
     blob = L.synthetic_model(1, 0)
-    _, _, _, single = bench.run_batch(L, blob, world * per_rank, 0, 2, frames - 2, None, 1)
+    _, (_, kn, kf, _, _), info, single = bench.run_batch(L, blob, world * per_rank, 0, 2, frames - 2, None, 1)
     assert sharded.shape == single.shape == (frames, world * per_rank, 160)
     assert np.array_equal(sharded, single.astype(np.int32))
     assert np.abs(single[2:].astype(np.float64)).mean() > 100
+    if per_rank >= 1024:
+        # the single-process run took the configs[4] path too: one
+        # multi-frame launch of the timed frames on 4 streams per workgroup
+        assert info.quad_path == 4 and info.streams_per_workgroup == 4
+        assert kn == 1 and kf == frames - 2, (kn, kf)
+        # and both agree with the CPU oracle on streams from each shard
+        import oracle_lib as O
+        for sid in (0, per_rank - 1, per_rank, 2 * per_rank - 1, per_rank + 517):
+            ref = O.synth_stream(blob, L.synthetic_features(sid, frames)[:, :20], 0)
+            assert np.array_equal(single[:, sid], ref), sid

@@ -363,6 +363,69 @@ def test_restore_refuses_out_of_range_gru_state(require_gpu, blobs):
     assert np.array_equal(b.synthesize(allf[4]), ref.synthesize(allf[4]))
 
 
+def test_restore_refuses_out_of_range_last_exc(require_gpu, blobs):
+    """last_exc indexes the 256-row embedding tables: a snapshot with
+    last_exc outside [0, 255] is refused (at 512 streams mf_kernel<2> turns
+    it into a byte offset of the gather); the spin-limit setter clamps huge
+    bounds instead of letting the poll counter overflow."""
+    import struct
+    blob = blobs["streams_int8"]
+    B, F = 512, 4
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    b = L.LPCNetBatch(B, 0, blob)
+    assert b.info().streams_per_workgroup == 2
+    for f in range(3):
+        b.synthesize(allf[f])
+    snap = bytes(b.save_state(7))
+    # StreamState ends ..., deemph_mem, last_exc, frame_count (= 3 now), rng[4], pad
+    i32 = lambda o: struct.unpack_from("<i", snap, o)[0]  # noqa: E731
+    offs = [o for o in range(len(snap) - 64, len(snap) - 8, 4) if i32(o + 4) == 3 and 0 <= i32(o) <= 255]
+    assert len(offs) == 1, offs
+    off = offs[0]
+    for v in (256, -1, 1 << 20):
+        bad = bytearray(snap)
+        struct.pack_into("<i", bad, off, v)
+        with pytest.raises(L.LPCNetError, match="last_exc"):
+            b.restore_state(7, bytes(bad))
+    b.restore_state(7, snap)
+    b.set_spin_limit(2 ** 31 - 1)
+    ref = L.LPCNetBatch(B, 0, blob)
+    for f in range(3):
+        ref.synthesize(allf[f])
+    assert np.array_equal(b.synthesize(allf[3]), ref.synthesize(allf[3]))
+
+
+def test_8192_streams_one_gpu_match_oracle(require_gpu, blobs):
+    """BASELINE configs[4]'s total stream count on one GPU: LPCNetBatch(8192)
+    through the device-resident multi-frame path (mf_kernel<4>: 2048
+    workgroups in 8 rounds over the CUs, chunked frame network), against the
+    CPU oracle on two streams of every 1024-stream shard (PCM and final GRU
+    states bit for bit), and shard 3 run alone as a 1024-stream batch gives
+    the same PCM for its streams."""
+    B, F = 8192, 8
+    blob = blobs["streams_int8"]
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    b = L.LPCNetBatch(B, 0, blob)
+    assert b.info().quad_path == 4 and b.info().streams_per_workgroup == 4
+    b.reset_timers(1)
+    got = np.concatenate([_frames(b, allf, 0, 2), _frames(b, allf, 2, F)], 0)
+    assert b.kernel_frames(0) == F and b.kernel_ms(0)[1] == 3  # 2 single-frame launches + one of 6
+    assert np.abs(got[2:].astype(np.float64)).mean() > 100
+    for shard in range(8):
+        for sid in (1024 * shard + (37 * shard) % 1024, 1024 * shard + 1023 - shard):
+            o = O.Oracle(blob, 0)
+            exp = np.stack([o.synthesize(allf[f, sid]) for f in range(F)])
+            assert np.array_equal(got[:, sid], exp), sid
+            a, g = o.state()
+            st = b.get_state(sid)
+            assert np.array_equal(bits(st["gru_a_state"]), bits(a)), sid
+            assert np.array_equal(bits(st["gru_b_state"]), bits(g)), sid
+    b.close()
+    c = L.LPCNetBatch(1024, 0, blob)
+    alone = np.concatenate([_frames(c, allf[:, 3072:4096], 0, 2), _frames(c, allf[:, 3072:4096], 2, F)], 0)
+    assert np.array_equal(alone, got[:, 3072:4096])
+
+
 CHECK256 = (0, 1, 128, 254, 255)
 
 

@@ -85,6 +85,27 @@ def test_kernel_float_identities_exhaustive(tmp_path):
     assert r.returncode == 0, r.stdout
 
 
+def test_lpcnet_init_never_trusts_raw_memory():
+    """lpcnet_init runs on caller memory (lpcnet_get_size + malloc, as the
+    reference's decoder does): bytes that look like a live handle (the magic
+    word and a stray batch pointer, e.g. a block a scrub-free allocator
+    reused after lpcnet_destroy) must give a fresh handle, never a reset of
+    that pointer.  Re-init of a live handle and destroy stay well-defined.
+    No device work: the batch is bound lazily by lpcnet_load_model."""
+    import ctypes as C
+    n = L.lib.lpcnet_get_size()
+    raw = (C.c_ubyte * n)()
+    C.memmove(raw, (0x4c50434e).to_bytes(4, "little") + b"\0" * 4 + (0xdeadbeef000).to_bytes(8, "little"), 16)
+    assert L.lib.lpcnet_init(C.cast(raw, C.c_void_p)) == 0
+    assert L.lib.lpcnet_init(C.cast(raw, C.c_void_p)) == 0  # now live: re-init resets (nothing bound)
+    st = L.lib.lpcnet_create()
+    assert st
+    L.lib.lpcnet_destroy(st)
+    st2 = L.lib.lpcnet_create()  # may reuse the freed block
+    assert st2 and L.lib.lpcnet_init(st2) == 0
+    L.lib.lpcnet_destroy(st2)
+
+
 def test_device_numerics_rejects_bad_arguments():
     """Argument checks happen before any HIP call (no GPU needed)."""
     assert L.lib.lpcnet_mi355x_device_numerics(0, 99, None, None, 1) == -1
