@@ -41,6 +41,10 @@ typedef struct {
   int lds_bytes;                  /* dynamic LDS of the sample kernel */
   double mfma_ops_per_group_sample; /* int8 matrix-core ops issued per workgroup per sample
                                        (mf_kernel; padding included), 0 otherwise */
+  /* model constants (see lpcnet_batch_set_model_constants) */
+  float lpc_gamma;
+  int features_delay;
+  int end2end;
 } LPCNetModelInfo;
 
 /* Create a batch of nb_streams streams on HIP device `device`.
@@ -59,6 +63,20 @@ LPCNET_EXPORT int lpcnet_batch_model_info(const LPCNetBatch *b, LPCNetModelInfo 
  * a forced mode the model cannot run falls back to 1.  Results are
  * identical; only speed differs.  Returns -1 for any other mode. */
 LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode);
+/* The model constants the reference compiles in from the generated
+ * nnet_data.h (training_tf2/dump_lpcnet.py:423-446): LPC_GAMMA
+ * (lpc_weighting of the frame's LPC, lpcnet.c:116-118), FEATURES_DELAY (the
+ * lookahead: depth of the lpc_from_cepstrum ring, conv2 clear and silent
+ * first frames, lpcnet.c:101,109-114,239; 0..4) and END2END (LPC from the
+ * frame network's rc outputs via rc2lpc, lpcnet.c:56-80,107-108).
+ * lpcnet_batch_load_model / lpcnet_load_model take them from optional blob
+ * records named LPC_GAMMA (one float), FEATURES_DELAY and END2END (one int
+ * each) -- the reference's parser skips records it does not bind -- else
+ * the dump defaults (1.0, 2, 0); the environment variables LPCNET_LPC_GAMMA,
+ * LPCNET_FEATURES_DELAY and LPCNET_END2END override both at load time.  This
+ * setter changes them for the loaded model (until the next load).  Returns
+ * -1 without a model or for an unsupported value. */
+LPCNET_EXPORT int lpcnet_batch_set_model_constants(LPCNetBatch *b, float lpc_gamma, int features_delay, int end2end);
 /* lpcnet_reset() on every stream / on one stream. */
 LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b);
 LPCNET_EXPORT int lpcnet_batch_reset_stream(LPCNetBatch *b, int stream);
@@ -152,7 +170,10 @@ LPCNET_EXPORT int lpcnet_batch_get_state(LPCNetBatch *b, int stream, float *gru_
 
 /* ---- tooling (host only, no GPU needed) -------------------------------- */
 /* Deterministic synthetic default-size model in the reference blob format.
- * flags: bit0 = make some int8 pairs able to saturate maddubs.
+ * flags: bit0 = make some int8 pairs able to saturate maddubs; bit1 = GRU_A
+ * block masks chosen as training_tf2/lpcnet.py:140-160 (Sparsify) does --
+ * a global per-gate energy threshold -- over skewed row energies, so block
+ * rows run far above the mean length, as in trained models.
  * Returns the blob size; writes it if buf != NULL and cap is large enough. */
 LPCNET_EXPORT int lpcnet_mi355x_synthetic_model(unsigned seed, int variant, int flags, unsigned char *buf, int cap);
 /* Synthetic feature frames (NB_TOTAL_FEATURES floats each) for stream `stream`. */

@@ -57,6 +57,7 @@ def _load():
         "lpcnet_batch_load_model": (i, [vp, C.c_char_p, i]),
         "lpcnet_batch_model_info": (i, [vp, vp]),
         "lpcnet_batch_set_kernel": (i, [vp, i]),
+        "lpcnet_batch_set_model_constants": (i, [vp, f, i, i]),
         "lpcnet_batch_reset": (None, [vp]),
         "lpcnet_batch_reset_stream": (i, [vp, i]),
         "lpcnet_batch_nb_streams": (i, [vp]),
@@ -106,7 +107,8 @@ class ModelInfo(C.Structure):
                 ("may_saturate", C.c_int), ("bytes_shared_per_frame", C.c_double),
                 ("bytes_shared_per_sample", C.c_double), ("bytes_per_stream_sample", C.c_double),
                 ("ops_per_sample", C.c_double), ("streams_per_workgroup", C.c_int), ("quad_path", C.c_int),
-                ("lds_bytes", C.c_int), ("mfma_ops_per_group_sample", C.c_double)]
+                ("lds_bytes", C.c_int), ("mfma_ops_per_group_sample", C.c_double),
+                ("lpc_gamma", C.c_float), ("features_delay", C.c_int), ("end2end", C.c_int)]
 
     @property
     def kernel_name(self) -> str:
@@ -146,13 +148,37 @@ def device_count() -> int:
     return lib.lpcnet_mi355x_device_count()
 
 
-def synthetic_model(seed: int = 1, variant: int = VARIANT_INT8, saturating: bool = False) -> bytes:
-    """Deterministic synthetic default-size model in the reference blob format."""
-    flags = 1 if saturating else 0
+def synthetic_model(seed: int = 1, variant: int = VARIANT_INT8, saturating: bool = False, skewed: bool = False) -> bytes:
+    """Deterministic synthetic default-size model in the reference blob format.
+    skewed: GRU_A masks by a global per-gate threshold over skewed block
+    energies (Sparsify, training_tf2/lpcnet.py:140-160): long block rows."""
+    flags = (1 if saturating else 0) | (2 if skewed else 0)
     n = lib.lpcnet_mi355x_synthetic_model(seed, variant, flags, None, 0)
     buf = C.create_string_buffer(n)
     lib.lpcnet_mi355x_synthetic_model(seed, variant, flags, buf, n)
     return buf.raw
+
+
+def with_model_constants(blob: bytes, lpc_gamma: float | None = None, features_delay: int | None = None,
+                         end2end: bool | None = None) -> bytes:
+    """``blob`` plus the side records LPC_GAMMA / FEATURES_DELAY / END2END
+    (64-byte WeightHead records, nnet.h:54-61) that carry the constants
+    dump_lpcnet.py writes into nnet_data.h; the reference's parser skips
+    records it does not bind."""
+    out = bytearray(blob)
+    for name, val in (("LPC_GAMMA", None if lpc_gamma is None else np.float32(lpc_gamma).tobytes()),
+                      ("FEATURES_DELAY", None if features_delay is None else np.int32(features_delay).tobytes()),
+                      ("END2END", None if end2end is None else np.int32(1 if end2end else 0).tobytes())):
+        if val is None:
+            continue
+        head = bytearray(64)
+        head[0:4] = b"DNNw"
+        head[8:12] = np.int32(0 if name == "LPC_GAMMA" else 1).tobytes()  # WEIGHT_TYPE_float / _int
+        head[12:16] = np.int32(4).tobytes()
+        head[16:20] = np.int32(64).tobytes()
+        head[20:20 + len(name)] = name.encode()
+        out += head + val + bytes(60)
+    return bytes(out)
 
 
 def synthetic_features(stream: int, nframes: int) -> np.ndarray:
@@ -230,6 +256,12 @@ class LPCNetBatch:
         """0 automatic, 1 lockstep sample kernel, 4 mf_kernel (matrix cores), 5 fp_kernel (fp32);
         a mode the model cannot run falls back to 1."""
         if lib.lpcnet_batch_set_kernel(self._b, mode) != 0:
+            raise LPCNetError(last_error())
+
+    def set_model_constants(self, lpc_gamma: float = 1.0, features_delay: int = 2, end2end: bool = False) -> None:
+        """LPC_GAMMA / FEATURES_DELAY / END2END of the loaded model (the reference's
+        nnet_data.h constants); see lpcnet_batch_set_model_constants."""
+        if lib.lpcnet_batch_set_model_constants(self._b, lpc_gamma, features_delay, 1 if end2end else 0) != 0:
             raise LPCNetError(last_error())
 
     def set_spin_limit(self, polls: int) -> None:

@@ -119,11 +119,13 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   float *c1 = lds + G::R0;   /* [SC][C1_SS]: conv1 outputs, row f + 2 = frame f (stride CK_RS) */
   float *ya = c1 + G::R1;    /* [64][CK_RS]: conv2, then dense2 outputs */
   __shared__ int fcs[G::SC];
-  __shared__ float olpc[G::SC][FEATURES_DELAY][NLPC];
+  __shared__ float olpc[G::SC][MAX_FEATURES_DELAY][NLPC];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, g = l >> 4, r = l & 15;
   const int s0 = blockIdx.x * G::SC;
   const int n = A.nframes, B = A.nstreams;
   const uint32_t *rcp = A.rcp;
+  const int D = A.mc.delay;
+  const float gamma = A.mc.lpc_gamma;
 
   /* inputs (lpcnet.c:91-99): frames -2, -1 from the conv1 memory, then
    * features | pitch embedding of each frame of the chunk */
@@ -153,8 +155,8 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
     const int s = e / (2 * COND), j = e % (2 * COND), sid = s0 + s;
     c1[s * G::C1_SS + (j / COND) * CK_RS + j % COND] = sid < B ? A.st[sid].conv2_mem[j] : 0.f;
   }
-  if (tid < G::SC * FEATURES_DELAY * NLPC) {
-    const int s = tid / (FEATURES_DELAY * NLPC), q = tid % (FEATURES_DELAY * NLPC), sid = s0 + s;
+  if (tid < G::SC * D * NLPC) {
+    const int s = tid / (D * NLPC), q = tid % (D * NLPC), sid = s0 + s;
     olpc[s][q / NLPC][q % NLPC] = sid < B ? A.st[sid].old_lpc[q / NLPC][q % NLPC] : 0.f;
   }
   if (tid < G::SC) fcs[tid] = s0 + tid < B ? A.st[s0 + tid].frame_count : 1000;
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   ck_tile<3 * COND, COND, COND, CK_RS>(A.conv2_w, A.conv2_b, wave, c1, xb, acc);
 #pragma unroll
   for (int j = 0; j < NCT; j++) {
-    const bool clr = ck_fc(fcs[cs[j]], cf[j]) < FEATURES_DELAY;
+    const bool clr = ck_fc(fcs[cs[j]], cf[j]) < D;
     float4 t;
     t.x = clr ? 0.f : tanh_x86<true>(acc[j][0], rcp);
     t.y = clr ? 0.f : tanh_x86<true>(acc[j][1], rcp);
@@ -225,6 +227,31 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
                     tanh_x86<true>(acc[j][3], rcp));
   __syncthreads();
 
+  /* END2END models (lpcnet.c:104,107-108): each frame's LPC = rc2lpc of the
+   * first LPC_ORDER conditioning values, weighted by LPC_GAMMA; one lane per
+   * (stream, frame) column */
+  if (A.mc.end2end && tid < G::COLS) {
+    const int s = tid / NFR, f = tid % NFR, sid = s0 + s;
+    if (sid < B && f < n) {
+      float rc[NLPC], lp[NLPC];
+#pragma unroll
+      for (int k = 0; k < NLPC; k++) rc[k] = ya[tid * CK_RS + k];
+      rc2lpc_dev(lp, rc);
+      float gi = gamma;
+#pragma unroll
+      for (int k = 0; k < NLPC; k++) {
+        lp[k] = lp[k] * gi;
+        gi *= gamma;
+      }
+      FrameCond *q = &A.cond[(size_t)f * B + sid];
+#pragma unroll
+      for (int k = 0; k < NLPC; k++) q->lpc[k] = lp[k];
+      if (f == n - 1)
+#pragma unroll
+        for (int k = 0; k < NLPC; k++) A.st[sid].lpc[k] = lp[k];
+    }
+  }
+
   /* conditioning projections (lpcnet.c:106-107), linear: gadf | gbdf as one
    * [128][1200] matrix, 75 row tiles over the 8 waves; frame f's outputs go
    * to cond[f], the last frame's also to the stream state */
@@ -249,8 +276,8 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   }
 
   /* per frame: the LPC it synthesises with (lpcnet.c:110-118: the ring's
-   * older slot, i.e. lpc_from_cepstrum of frame f - 2; LPC_GAMMA = 1) and
-   * frame_count after its update */
+   * oldest slot, i.e. lpc_from_cepstrum of frame f - FEATURES_DELAY, then
+   * lpc_weighting; END2END: written above) and frame_count after its update */
   for (int e = tid; e < G::SC * NFR * (NLPC + 1); e += CK_THREADS) {
     const int s = e / (NFR * (NLPC + 1)), rem = e % (NFR * (NLPC + 1));
     const int f = rem / (NLPC + 1), k = rem % (NLPC + 1), sid = s0 + s;
@@ -259,9 +286,9 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
     if (k == NLPC) {
       const int fc = ck_fc(fcs[s], f);
       q->frame_count = fc < 1000 ? fc + 1 : fc;
-    } else {
-      const int t = f - 2;
-      q->lpc[k] = (t >= 0 ? A.lpc_new[((size_t)t * B + sid) * NLPC + k] : olpc[s][-1 - t][k]) * 1.0f;
+    } else if (!A.mc.end2end) {
+      const int t = f - D;
+      q->lpc[k] = lpc_weight(t >= 0 ? A.lpc_new[((size_t)t * B + sid) * NLPC + k] : olpc[s][-1 - t][k], k, gamma);
     }
   }
   /* the stream state after the chunk: conv2 memory = conv1 outputs of frames
@@ -270,14 +297,13 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
     const int s = e / (2 * COND), j = e % (2 * COND), sid = s0 + s;
     if (sid < B) A.st[sid].conv2_mem[j] = c1[s * G::C1_SS + (n + j / COND) * CK_RS + j % COND];
   }
-  if (tid < G::SC * NLPC) {
+  if (!A.mc.end2end && tid < G::SC * NLPC) {
     const int s = tid / NLPC, k = tid % NLPC, sid = s0 + s;
     if (sid < B) {
       auto L = [&](int t) { return t >= 0 ? A.lpc_new[((size_t)t * B + sid) * NLPC + k] : olpc[s][-1 - t][k]; };
       StreamState *p = &A.st[sid];
-      p->lpc[k] = L(n - 3) * 1.0f;
-      p->old_lpc[0][k] = L(n - 1);
-      p->old_lpc[1][k] = L(n - 2);
+      p->lpc[k] = lpc_weight(L(n - 1 - D), k, gamma);
+      for (int j = 0; j < D; j++) p->old_lpc[j][k] = L(n - 1 - j);
     }
   }
   if (tid < G::SC && s0 + tid < B) A.st[s0 + tid].frame_count = ck_fc(fcs[tid], n);

@@ -353,6 +353,37 @@ __device__ __forceinline__ int dot4(uint32_t w, uint32_t xs, int acc)
   else return __builtin_amdgcn_sdot4((int)w, (int)xs, acc, false);
 }
 
+/* rc2lpc (lpcnet.c:56-80, END2END models): the reference's recursion as
+ * written, one thread, float products and sums separately rounded (this TU
+ * is compiled with -ffp-contract=off). */
+__device__ __forceinline__ void rc2lpc_dev(float (&lpc)[NLPC], const float (&rc)[NLPC])
+{
+  float tmp[NLPC], ntmp[NLPC];
+#pragma unroll
+  for (int k = 0; k < NLPC; k++) {
+    tmp[k] = rc[k];
+    ntmp[k] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < NLPC; i++) {
+#pragma unroll
+    for (int j = 0; j < i; j++) ntmp[j] = tmp[j] + tmp[i] * tmp[i - j - 1];
+#pragma unroll
+    for (int k = 0; k < i; k++) tmp[k] = ntmp[k];
+  }
+#pragma unroll
+  for (int k = 0; k < NLPC; k++) lpc[k] = tmp[k];
+}
+
+/* lpc_weighting (freq.c:299-308) of coefficient k: lpc[k] * gamma^(k+1),
+ * the power built as the reference's running float product */
+__device__ __forceinline__ float lpc_weight(float v, int k, float gamma)
+{
+  float gi = gamma;
+  for (int m = 0; m < k; m++) gi *= gamma;
+  return v * gi;
+}
+
 }  // namespace lpcnet_mi355x
 
 #endif

@@ -122,6 +122,17 @@ struct Kiss {
 };
 
 /* ---- blob parsing (parse_lpcnet_weights.c:36-113) ---------------------- */
+int check_constants(const ModelConst &mc)
+{
+  if (!std::isfinite(mc.lpc_gamma)) { set_err("LPC_GAMMA must be finite"); return -1; }
+  if (mc.delay < 0 || mc.delay > MAX_FEATURES_DELAY) {
+    set_err("FEATURES_DELAY must lie in [0, " + std::to_string(MAX_FEATURES_DELAY) + "]");
+    return -1;
+  }
+  if (mc.end2end != 0 && mc.end2end != 1) { set_err("END2END must be 0 or 1"); return -1; }
+  return 0;
+}
+
 struct Arr {
   std::string name;
   int size;
@@ -293,6 +304,7 @@ struct LPCNetBatch {
   bool sat = false;
   bool reg = false;
   int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 4 matrix-core mf_kernel, 5 fp32 fp_kernel */
+  ModelConst mc{1.0f, DEFAULT_FEATURES_DELAY, 0}; /* FEATURES_DELAY / LPC_GAMMA / END2END of the model */
   bool mf_ok = false;    /* model fits the matrix-core register tables */
   bool mf = false;       /* mf_kernel (mode 4) */
   double mf_ga_ops = 0;  /* int8 matrix-core ops per workgroup per sample: the GRU_A recurrent pass */
@@ -344,7 +356,7 @@ struct LPCNetBatch {
   std::vector<hipEvent_t> ev_free;
   /* lower bound of every stream's frame_count (lpcnet.c:119) before the next
    * frame: the multi-frame sample launches start where no stream can still
-   * be inside its first FEATURES_DELAY frames */
+   * be inside its first `delay` (FEATURES_DELAY) frames */
   int min_fc = 0;
   void frames_done(int n) { min_fc = min_fc >= 1000 ? min_fc : std::min(min_fc + n, 1000); }
   int set_device() { return hipSetDevice(device) == hipSuccess ? 0 : -1; }
@@ -416,11 +428,11 @@ void choose_kernel(LPCNetBatch *b)
     b->info.quad_path = 5;
     return;
   }
-  if (mode == 4 && b->mf_ok && mf_lds_bytes(b->S) <= 160 * 1024) {
+  if (mode == 4 && b->mf_ok && mf_lds_bytes(b->S, b->sa.mf_split) <= 160 * 1024) {
     b->mf = true;
     b->info.mfma_ops_per_group_sample = b->mf_ga_ops + b->mf_gb_ops;
     b->info.streams_per_workgroup = b->S;
-    b->info.lds_bytes = mf_lds_bytes(b->S);
+    b->info.lds_bytes = mf_lds_bytes(b->S, b->sa.mf_split);
     b->info.quad_path = 4;
     return;
   }
@@ -562,6 +574,142 @@ static void mf_bank_slots(const std::vector<int> *const rows4[4], int nslot, int
   }
 }
 
+/* mf_kernel work plan of the GRU_A recurrent product.
+ *
+ * Each GRU_A lane group (8 lanes) owns one unit block (8 units, one 8-row
+ * block row per gate) and runs, per gate, `own` slots of its row's blocks.
+ * A trained model's block rows can be far longer than the mean -- Sparsify
+ * keeps blocks by a global per-gate energy threshold (training_tf2/
+ * lpcnet.py:140-160) -- so a row longer than the own cap is split: its first
+ * own[g] blocks stay with the owner, the rest go in pieces of at most
+ * piece[g] blocks to other lane groups' hosted region (at most one piece per
+ * lane group and gate), whose int32 partial sums the kernel adds into the
+ * owner's accumulator through LDS.  Integer sums are exact in any order, so
+ * the result is bit-identical to the unsplit product. */
+struct MfPiece {
+  int unit, t0, t1; /* blocks [t0, t1) of unit block `unit`'s row of the gate */
+};
+struct MfPlan {
+  bool split = false;
+  std::vector<int> perm;               /* lane group -> own unit block */
+  int own[3] = {MF_ZMAX, MF_ZMAX, MF_HMAX};
+  std::vector<MfPiece> pieces[3];
+  std::vector<int> host[3];            /* lane group -> piece index (-1 none) */
+  int nzr[SAMPLE_WAVES] = {}, nh[SAMPLE_WAVES] = {}, nfzr[SAMPLE_WAVES] = {}, nfh[SAMPLE_WAVES] = {};
+};
+
+bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P)
+{
+  constexpr int NUB = NA / 8, NLG = SAMPLE_WAVES * 8;
+  int kmax[3] = {0, 0, 0};
+  for (int g = 0; g < 3; g++)
+    for (int u = 0; u < NUB; u++) kmax[g] = std::max(kmax[g], (int)ga[g * NUB + u].size());
+  auto pieces_needed = [&](int g, int T, int F) {
+    long n = 0;
+    for (int u = 0; u < NUB; u++) {
+      const int K = (int)ga[g * NUB + u].size();
+      if (K > T) n += F > 0 ? (K - T + F - 1) / F : 1000000;
+    }
+    return n;
+  };
+  if (std::max(kmax[0], kmax[1]) <= MF_ZMAX && kmax[2] <= MF_HMAX && !getenv("LPCNET_MF_FORCE_SPLIT")) {
+    P.split = false;
+  } else {
+    /* smallest per-sample MFMA count 2 (Tzr + Fzr) + (Th + Fh) whose pieces
+     * fit one per lane group (LPCNET_MF_FORCE_SPLIT: split even a model that
+     * fits, with the smallest own cap, for tests) */
+    const bool force = getenv("LPCNET_MF_FORCE_SPLIT") != nullptr;
+    long best = -1;
+    int bz[2] = {0, 0}, bh[2] = {0, 0};
+    for (int Tz = 4; Tz <= MF_ZMAX; Tz += 4)
+      for (int Fz = 0; Tz + Fz <= MF_ZMAX; Fz += 4) {
+        const long pz = std::max(pieces_needed(0, Tz, Fz), pieces_needed(1, Tz, Fz));
+        if (pz > NLG || (Fz > 0 && pz == 0)) continue;
+        for (int Th = 4; Th <= MF_HMAX; Th += 4)
+          for (int Fh = 0; Th + Fh <= MF_HMAX; Fh += 4) {
+            const long ph = pieces_needed(2, Th, Fh);
+            if (ph > NLG || (Fh > 0 && ph == 0)) continue;
+            if (force && pz + ph == 0) continue;
+            const long cost = 2 * (Tz + Fz) + Th + Fh;
+            if (best < 0 || cost < best || (force && cost == best && Tz < bz[0])) {
+              best = cost;
+              bz[0] = Tz; bz[1] = Fz; bh[0] = Th; bh[1] = Fh;
+            }
+          }
+      }
+    if (best < 0) return false; /* does not fit even split: the lockstep kernel runs it */
+    P.split = true;
+    P.own[0] = P.own[1] = bz[0];
+    P.own[2] = bh[0];
+    const int F[3] = {bz[1], bz[1], bh[1]};
+    for (int g = 0; g < 3; g++) {
+      P.pieces[g].clear();
+      for (int u = 0; u < NUB; u++) {
+        const int K = (int)ga[g * NUB + u].size();
+        for (int t0 = P.own[g]; t0 < K; t0 += F[g]) P.pieces[g].push_back(MfPiece{u, t0, std::min(K, t0 + F[g])});
+      }
+    }
+  }
+  /* own parts -> unit-block assignment (balance, see mf_assign_unit_blocks) */
+  std::vector<std::vector<int>> own(ga.size());
+  for (int g = 0; g < 3; g++)
+    for (int u = 0; u < NUB; u++) {
+      const std::vector<int> &v = ga[g * NUB + u];
+      own[g * NUB + u].assign(v.begin(), v.begin() + std::min((int)v.size(), P.own[g]));
+    }
+  P.perm = mf_assign_unit_blocks(own);
+  /* pieces -> lane groups, spread over the waves (lane group 8w + j in the
+   * order j-major, w-minor) */
+  for (int g = 0; g < 3; g++) {
+    P.host[g].assign(NLG, -1);
+    for (int p = 0; p < (int)P.pieces[g].size(); p++) {
+      const int lg = 8 * (p % SAMPLE_WAVES) + p / SAMPLE_WAVES;
+      P.host[g][lg] = p;
+    }
+  }
+  for (int w = 0; w < SAMPLE_WAVES; w++) {
+    int kz = 0, kh = 0, fz = 0, fh = 0;
+    for (int j = 0; j < 8; j++) {
+      const int lg = 8 * w + j, ub = P.perm[lg];
+      kz = std::max(kz, (int)std::max(own[ub].size(), own[NUB + ub].size()));
+      kh = std::max(kh, (int)own[2 * NUB + ub].size());
+      for (int g = 0; g < 3; g++)
+        if (P.host[g][lg] >= 0) {
+          const MfPiece &pc = P.pieces[g][P.host[g][lg]];
+          (g < 2 ? fz : fh) = std::max(g < 2 ? fz : fh, pc.t1 - pc.t0);
+        }
+    }
+    P.nzr[w] = (kz + 3) / 4;
+    P.nh[w] = (kh + 3) / 4;
+    P.nfzr[w] = (fz + 3) / 4;
+    P.nfh[w] = (fh + 3) / 4;
+    if (4 * (P.nzr[w] + P.nfzr[w]) > MF_ZMAX || 4 * (P.nh[w] + P.nfh[w]) > MF_HMAX) return false;
+  }
+  return true;
+}
+
+/* The model constants of a blob (see load_model); -1 on a malformed record
+ * or an unsupported value. */
+int model_constants(const std::vector<Arr> &L, ModelConst &mc)
+{
+  if (const Arr *a = find(L, "LPC_GAMMA")) {
+    if (a->size != 4) { set_err("LPC_GAMMA record must hold one float"); return -1; }
+    memcpy(&mc.lpc_gamma, a->data, 4);
+  }
+  if (const Arr *a = find(L, "FEATURES_DELAY")) {
+    if (a->size != 4) { set_err("FEATURES_DELAY record must hold one int"); return -1; }
+    memcpy(&mc.delay, a->data, 4);
+  }
+  if (const Arr *a = find(L, "END2END")) {
+    if (a->size != 4) { set_err("END2END record must hold one int"); return -1; }
+    memcpy(&mc.end2end, a->data, 4);
+  }
+  if (const char *v = getenv("LPCNET_LPC_GAMMA")) mc.lpc_gamma = strtof(v, nullptr);
+  if (const char *v = getenv("LPCNET_FEATURES_DELAY")) mc.delay = atoi(v);
+  if (const char *v = getenv("LPCNET_END2END")) mc.end2end = atoi(v);
+  return check_constants(mc);
+}
+
 int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload = true)
 {
   std::vector<Arr> L;
@@ -609,7 +757,15 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   F(fc_f, "dual_fc_factor", 512);
 #undef F
   (void)embed_sig;
+  /* model constants: optional side records named like the #defines
+   * dump_lpcnet.py:423-446 writes into nnet_data.h (LPC_GAMMA float,
+   * FEATURES_DELAY int, END2END int; the reference's parser ignores unknown
+   * records), else the dump defaults; LPCNET_LPC_GAMMA /
+   * LPCNET_FEATURES_DELAY / LPCNET_END2END override both (drop-in callers) */
+  ModelConst mc{1.0f, DEFAULT_FEATURES_DELAY, 0};
+  if (model_constants(L, mc)) return -1;
   const void *gbw = find_check(L, "gru_b_weights", 32 * nbb * q);
+
   const void *gbrec = find_check(L, "gru_b_recurrent_weights", 3 * NB * NB * q);
   if (!gbw || !gbrec) return -1;
 
@@ -798,49 +954,77 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   /* ---- matrix-core tables (non-saturating int8 models, mf_kernel) ---- */
   std::vector<uint32_t> mft, mfgb;
   bool mf_ok = int8 && !sat && !getenv("LPCNET_NO_MFMA");
-  for (int w = 0; w < SAMPLE_WAVES && mf_ok; w++)
-    for (int j = 0; j < 8; j++) {
-      if ((int)ga_blocks[w * 8 + j].size() > MF_ZMAX || (int)ga_blocks[NA / 8 + w * 8 + j].size() > MF_ZMAX ||
-          (int)ga_blocks[2 * (NA / 8) + w * 8 + j].size() > MF_HMAX)
-        mf_ok = false;
+  MfPlan plan;
+  if (mf_ok) mf_ok = mf_plan(ga_blocks, plan);
+  if (getenv("LPCNET_VERBOSE")) {
+    fprintf(stderr, "lpcnet: mf_kernel plan: %s", !mf_ok ? "not applicable" : plan.split ? "split" : "unsplit");
+    if (mf_ok) {
+      fprintf(stderr, " own caps z/r %d h %d, pieces z %zu r %zu h %zu; groups per wave (own zr, hosted zr, own h, hosted h):",
+              plan.own[0], plan.own[2], plan.pieces[0].size(), plan.pieces[1].size(), plan.pieces[2].size());
+      for (int w = 0; w < SAMPLE_WAVES; w++) fprintf(stderr, " (%d %d %d %d)", plan.nzr[w], plan.nfzr[w], plan.nh[w], plan.nfh[w]);
     }
-  std::vector<int> mf_units;
+    fprintf(stderr, "\n");
+  }
+  std::vector<int> mf_units, mf_frow;
   if (mf_ok) {
     const int8_t *wa = (const int8_t *)gaw->data, *wb = (const int8_t *)gbw, *wr = (const int8_t *)gbrec;
     /* GRU_A: lane l of wave w = row l%8 of unit block perm[8w + l/8] of each
-     * gate (units 8 perm[.] .. +7); D row of that lane = that unit */
-    const std::vector<int> perm = mf_assign_unit_blocks(ga_blocks);
+     * gate (units 8 perm[.] .. +7); D row of that lane = that unit.  Its
+     * own region holds the first own[g] blocks of that row block; a split
+     * model's hosted region [own, own + hosted) the piece of another
+     * (long) row block, whose partial sums go to that row's owner */
+    const std::vector<int> &perm = plan.perm;
     mft.assign((size_t)SAMPLE_WAVES * MF_LANE_U32 * 64, 0);
     mf_units.assign((size_t)SAMPLE_WAVES * 64, 0);
+    mf_frow.assign((size_t)3 * SAMPLE_WAVES * 64, NA); /* NA: no hosted piece (a dummy row) */
+    sa.mf_split = plan.split ? 1 : 0;
     for (int w = 0; w < SAMPLE_WAVES; w++) {
       auto word = [&](int k, int l) -> uint32_t & { return mft[((size_t)w * MF_LANE_U32 + k) * 64 + l]; };
-      int kz = 0, kh = 0;
-      for (int j = 0; j < 8; j++) {
-        const int ub = perm[w * 8 + j];
-        kz = std::max(kz, (int)std::max(ga_blocks[ub].size(), ga_blocks[NA / 8 + ub].size()));
-        kh = std::max(kh, (int)ga_blocks[2 * (NA / 8) + ub].size());
-      }
-      sa.mf_nzr[w] = (kz + 3) / 4;
-      sa.mf_nh[w] = (kh + 3) / 4;
+      sa.mf_nzr[w] = plan.nzr[w];
+      sa.mf_nh[w] = plan.nh[w];
+      sa.mf_nfzr[w] = plan.nfzr[w];
+      sa.mf_nfh[w] = plan.nfh[w];
       for (int l = 0; l < 64; l++) mf_units[w * 64 + l] = 8 * perm[w * 8 + (l >> 3)] + (l & 7);
       for (int g = 0; g < 3; g++) {
         const int base = g == 0 ? 0 : (g == 1 ? MF_ZMAX : 2 * MF_ZMAX);
-        const int nslot = 4 * (g < 2 ? sa.mf_nzr[w] : sa.mf_nh[w]);
-        for (int half = 0; half < 2; half++) {
-          /* the 4 block rows read by one 32-lane LDS group: slot order
-           * chosen so their x words fall in distinct banks (mf_bank_slots) */
-          const std::vector<int> *rows4[4];
-          for (int k = 0; k < 4; k++) rows4[k] = &ga_blocks[g * (NA / 8) + perm[w * 8 + 4 * half + k]];
-          int slot_of[4][MF_HMAX], cb_at[4][MF_HMAX];
-          mf_bank_slots(rows4, nslot, slot_of, cb_at);
-          for (int k = 0; k < 4; k++) {
-            const int j = 4 * half + k, ub = perm[w * 8 + j], rb = g * (NA / 8) + ub;
-            for (int r = 0; r < 8; r++) {
-              const int l = 8 * j + r;
-              for (int t = 0; t < (int)ga_blocks[rb].size(); t++)
-                memcpy(&word(base + slot_of[k][t], l), wa + 32 * (ga_first[rb] + t) + 4 * r, 4);
-              for (int t = 0; t < nslot; t++)
-                word(MF_GA + (base + t) / 4, l) |= (uint32_t)cb_at[k][t] << (8 * ((base + t) & 3));
+        const int nown = 4 * (g < 2 ? plan.nzr[w] : plan.nh[w]), nfor = 4 * (g < 2 ? plan.nfzr[w] : plan.nfh[w]);
+        for (int region = 0; region < 2; region++) {
+          const int nslot = region ? nfor : nown, off = region ? nown : 0;
+          if (!nslot) continue;
+          for (int half = 0; half < 2; half++) {
+            /* the 4 block rows read by one 32-lane LDS group: slot order
+             * chosen so their x words fall in distinct banks (mf_bank_slots) */
+            std::vector<int> lists[4];
+            int rbk[4], t0k[4];
+            for (int k = 0; k < 4; k++) {
+              const int lg = w * 8 + 4 * half + k;
+              rbk[k] = -1;
+              t0k[k] = 0;
+              int t1 = 0;
+              if (!region) {
+                rbk[k] = g * (NA / 8) + perm[lg];
+                t1 = std::min((int)ga_blocks[rbk[k]].size(), plan.own[g]);
+              } else if (plan.host[g][lg] >= 0) {
+                const MfPiece &pc = plan.pieces[g][plan.host[g][lg]];
+                rbk[k] = g * (NA / 8) + pc.unit;
+                t0k[k] = pc.t0;
+                t1 = pc.t1;
+                for (int r = 0; r < 8; r++) mf_frow[((size_t)g * SAMPLE_WAVES + w) * 64 + 8 * (4 * half + k) + r] = 8 * pc.unit + r;
+              }
+              if (rbk[k] >= 0) lists[k].assign(ga_blocks[rbk[k]].begin() + t0k[k], ga_blocks[rbk[k]].begin() + t1);
+            }
+            const std::vector<int> *rows4[4] = {&lists[0], &lists[1], &lists[2], &lists[3]};
+            int slot_of[4][MF_HMAX], cb_at[4][MF_HMAX];
+            mf_bank_slots(rows4, nslot, slot_of, cb_at);
+            for (int k = 0; k < 4; k++) {
+              const int j = 4 * half + k;
+              for (int r = 0; r < 8; r++) {
+                const int l = 8 * j + r;
+                for (int t = 0; t < (int)lists[k].size(); t++)
+                  memcpy(&word(base + off + slot_of[k][t], l), wa + 32 * (ga_first[rbk[k]] + t0k[k] + t) + 4 * r, 4);
+                for (int t = 0; t < nslot; t++)
+                  word(MF_GA + (base + off + t) / 4, l) |= (uint32_t)cb_at[k][t] << (8 * ((base + off + t) & 3));
+              }
             }
           }
         }
@@ -935,12 +1119,24 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     }
   }
 
-  /* choose streams per workgroup and check the LDS budget */
+  /* choose streams per workgroup and check the LDS budget of the lockstep
+   * kernel: the whole image in LDS, or -- models with long block rows -- only
+   * its fixed tables, the weight sections read from global memory */
   int S = b->B >= 1024 ? 4 : (b->B >= 512 ? 2 : 1);
-  int lds = sample_lds_bytes(S, variant, (int)img.size());
+  int image_lds = (int)img.size();
+  int lds = sample_lds_bytes(S, variant, image_lds);
   while (lds > 160 * 1024 && S > 1) {
     S /= 2;
-    lds = sample_lds_bytes(S, variant, (int)img.size());
+    lds = sample_lds_bytes(S, variant, image_lds);
+  }
+  if (lds > 160 * 1024) {
+    image_lds = IMG_VAR;
+    S = b->B >= 1024 ? 4 : (b->B >= 512 ? 2 : 1);
+    lds = sample_lds_bytes(S, variant, image_lds);
+    while (lds > 160 * 1024 && S > 1) {
+      S /= 2;
+      lds = sample_lds_bytes(S, variant, image_lds);
+    }
   }
   if (lds > 160 * 1024) {
     set_err("model does not fit the 160 KiB LDS budget");
@@ -999,6 +1195,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   if (mf_ok) {
     UP(sa.mf, mft.data(), mft.size() * 4);
     UP(sa.mf_unit, mf_units.data(), mf_units.size() * 4);
+    UP(sa.mf_frow, mf_frow.data(), mf_frow.size() * 4);
     {
       /* Range of the GRU_A gates' inputs for the elementwise fast path:
        * z/r: cvt_rne((bias + diag st + ((cond + Esig) + Epred) + Eexc) * 16256)
@@ -1067,8 +1264,10 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   }
 #undef UP
   sa.image_bytes = (int)img.size();
+  sa.image_lds_bytes = image_lds;
   b->sa = sa;
   b->fa = fa;
+  b->mc = mc;
   b->variant = variant;
   b->sat = sat;
   b->reg = reg;
@@ -1102,10 +1301,13 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   b->mf_ga_ops = b->mf_gb_ops = 0;
   if (mf_ok) {
     double n4 = 0;
-    for (int w = 0; w < SAMPLE_WAVES; w++) n4 += 8.0 * sa.mf_nzr[w] + 4.0 * sa.mf_nh[w];
+    for (int w = 0; w < SAMPLE_WAVES; w++) n4 += 8.0 * (sa.mf_nzr[w] + sa.mf_nfzr[w]) + 4.0 * (sa.mf_nh[w] + sa.mf_nfh[w]);
     b->mf_ga_ops = 2.0 * n4 * 1024.0;
     b->mf_gb_ops = 2.0 * 2.0 * MF_GB_TILES * 16384.0;
   }
+  in.lpc_gamma = mc.lpc_gamma;
+  in.features_delay = mc.delay;
+  in.end2end = mc.end2end;
   in.ops_per_sample = 2.0 * (32.0 * nba + 32.0 * nbb + 3 * NB * NB + 8 * 2 * NB + NLPC) +
                       2.0 * (3.0 * FIN * COND + 3.0 * COND * COND + 2.0 * COND * COND + COND * GA_ROWS + COND * GB_ROWS) / FRAME;
   choose_kernel(b); /* also sets mfma_ops_per_group_sample for the chosen kernel */
@@ -1156,11 +1358,13 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
   hipStream_t fs = ovl >= 0 ? b->fstream : b->stream;
   FrameArgs fa = b->fa;
   fa.st = b->d_state;
+  fa.mc = b->mc;
   fa.nstreams = b->B;
   fa.features = d_features;
   fa.lpc_new = d_lpc_frame;
   SampleArgs sa = b->sa;
   sa.st = b->d_state;
+  sa.delay = b->mc.delay;
   sa.nstreams = b->B;
   sa.N = N;
   sa.pcm = d_pcm;
@@ -1185,7 +1389,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
   if (e[0]) HIPCHK(hipEventRecord(e[0], fs));
   /* lpc_from_cepstrum of this frame's features: the frame kernel pushes it
    * into the two-frame LPC ring (lpcnet.c:110-112) */
-  if (run_lpc && launch_lpc(d_features, d_lpc_frame, b->B, b->d_lpc_tab, fs)) {
+  if (run_lpc && !b->mc.end2end && launch_lpc(d_features, d_lpc_frame, b->B, b->d_lpc_tab, fs)) {
     set_err("lpc kernel launch failed");
     return -1;
   }
@@ -1248,11 +1452,12 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
  * (chunk_kernel, outputs in d_chunk[f]); launch the sample kernel of frames
  * f .. f + nfr - 1 on b->stream, reading their conditioning from d_chunk[f..]
  * and writing d_pcm [nfr][B][N].  nfr > 1: matrix-core kernel only, every
- * stream past its first FEATURES_DELAY frames (SampleArgs::nframes). */
+ * stream past its first `delay` frames (SampleArgs::nframes). */
 int launch_chunk_samples(LPCNetBatch *b, int f, short *d_pcm, int N, int nfr = 1)
 {
   SampleArgs sa = b->sa;
   sa.st = b->d_state;
+  sa.delay = b->mc.delay;
   sa.cond = b->d_chunk + (size_t)f * b->B;
   sa.nstreams = b->B;
   sa.N = N;
@@ -1290,6 +1495,7 @@ int launch_chunk_frames(LPCNetBatch *b, const float *d_features, int n)
 {
   FrameArgs fa = b->fa;
   fa.st = b->d_state;
+  fa.mc = b->mc;
   fa.nstreams = b->B;
   fa.features = d_features;
   fa.lpc_new = b->d_lpc;
@@ -1471,6 +1677,20 @@ LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode)
   return 0;
 }
 
+LPCNET_EXPORT int lpcnet_batch_set_model_constants(LPCNetBatch *b, float lpc_gamma, int features_delay, int end2end)
+{
+  if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
+  const ModelConst mc{lpc_gamma, features_delay, end2end};
+  if (check_constants(mc)) return -1;
+  if (b->set_device()) return -1;
+  (void)hipStreamSynchronize(b->stream); /* queued frames keep the constants they were enqueued with */
+  b->mc = mc;
+  b->info.lpc_gamma = mc.lpc_gamma;
+  b->info.features_delay = mc.delay;
+  b->info.end2end = mc.end2end;
+  return 0;
+}
+
 LPCNET_EXPORT int lpcnet_batch_model_info(const LPCNetBatch *b, LPCNetModelInfo *info)
 {
   if (!b || !b->have_model || !info) return -1;
@@ -1614,7 +1834,7 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
      * one-wave streams is latency-bound); queued on the frame kernels' queue,
      * after the frame kernels of the previous chunk that read d_lpc */
     const int n = std::min(LPC_CHUNK, nframes - c0);
-    if (launch_lpc(d_features + c0 * fstride, b->d_lpc, n * b->B, b->d_lpc_tab, fs)) {
+    if (!b->mc.end2end && launch_lpc(d_features + c0 * fstride, b->d_lpc, n * b->B, b->d_lpc_tab, fs)) {
       set_err("lpc kernel launch failed");
       return -1;
     }
@@ -1622,7 +1842,7 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_frames(LPCNetBatch *b, const float *h_
       const int fc0 = b->min_fc;
       if (launch_chunk_frames(b, d_features + c0 * fstride, n)) return -1;
       /* frames in which a stream may still turn active: one launch each */
-      const int k = mfm ? std::min(n, std::max(0, FEATURES_DELAY - fc0)) : n;
+      const int k = mfm ? std::min(n, std::max(0, b->mc.delay - fc0)) : n;
       for (int f = c0; f < c0 + k; f++)
         if (launch_chunk_samples(b, f - c0, d_pcm + (size_t)f * b->B * N, N)) return -1;
       if (k < n && launch_chunk_samples(b, k, d_pcm + (size_t)(c0 + k) * b->B * N, N, n - k)) return -1;

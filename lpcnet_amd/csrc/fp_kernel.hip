@@ -183,7 +183,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int sid = blockIdx.x;
   const uint32_t *rcp = (const uint32_t *)(img + IMG_RCP);
-  const bool active = frame_count_of(A, sid) > FEATURES_DELAY;
+  const bool active = frame_count_of(A, sid) > A.delay;
   if (!active) {
     for (int n = tid; n < A.N; n += FP_THREADS) A.pcm[(size_t)sid * A.N + n] = 0;
     return;

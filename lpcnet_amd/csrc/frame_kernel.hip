@@ -154,7 +154,8 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
   /* this frame's new LPC (host-computed; possibly pinned host memory read
    * over PCIe): fetched first, used in the epilogue */
   float lpc_in = 0.f;
-  if (tid < NS * NLPC && s0 + tid / NLPC < A.nstreams) lpc_in = A.lpc_new[(s0 + tid / NLPC) * NLPC + tid % NLPC];
+  if (!A.mc.end2end && tid < NS * NLPC && s0 + tid / NLPC < A.nstreams)
+    lpc_in = A.lpc_new[(s0 + tid / NLPC) * NLPC + tid % NLPC];
   /* inputs (lpcnet.c:91-99): conv1 window = conv1 memory | features | pitch
    * embedding; conv2 memory.  All loads of a thread in flight, then stores. */
   {
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
 #pragma unroll
     for (int q = 0; q < NS; q++) {
       const float t = tanh_x86(a[q], rcp);
-      ya[q][i] = fc[q] < FEATURES_DELAY ? 0.f : t;
+      ya[q][i] = fc[q] < A.mc.delay ? 0.f : t;
     }
   }
   __syncthreads();
@@ -290,18 +291,33 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
     const int q = e / (2 * COND), j = e % (2 * COND);
     if (s0 + q < A.nstreams) A.st[s0 + q].conv2_mem[j] = x2[q][COND + j];
   }
-  /* LPC ring (lpcnet.c:110-118; LPC_GAMMA = 1 -> lpc_weighting multiplies by 1.0f) */
-  if (tid < NS * NLPC) {
+  /* the frame's LPC (lpcnet.c:107-118): END2END -> rc2lpc of the first
+   * LPC_ORDER conditioning values (dense2's outputs, still in ya); else the
+   * lpc_from_cepstrum ring of FEATURES_DELAY frames (none at delay 0); then
+   * lpc_weighting by LPC_GAMMA */
+  if (A.mc.end2end) {
+    if (tid < NS && s0 + tid < A.nstreams) {
+      float rc[NLPC], l[NLPC];
+#pragma unroll
+      for (int k = 0; k < NLPC; k++) rc[k] = ya[tid][k];
+      rc2lpc_dev(l, rc);
+      StreamState *p = &A.st[s0 + tid];
+      float gi = A.mc.lpc_gamma;
+#pragma unroll
+      for (int k = 0; k < NLPC; k++) {
+        p->lpc[k] = l[k] * gi;
+        gi *= A.mc.lpc_gamma;
+      }
+    }
+  } else if (tid < NS * NLPC) {
     const int q = tid / NLPC, k = tid % NLPC, sid = s0 + q;
     if (sid < A.nstreams) {
       StreamState *p = &A.st[sid];
-      const float cur = p->old_lpc[FEATURES_DELAY - 1][k];
-      const float nxt = p->old_lpc[0][k];
-      float g = 1.0f, gi = g;
-      for (int m = 0; m < k; m++) gi *= g;
-      p->lpc[k] = cur * gi;
-      p->old_lpc[1][k] = nxt;
-      p->old_lpc[0][k] = lpc_in;
+      const int D = A.mc.delay;
+      const float cur = D > 0 ? p->old_lpc[D - 1][k] : lpc_in;
+      for (int j = D - 1; j > 0; j--) p->old_lpc[j][k] = p->old_lpc[j - 1][k];
+      if (D > 0) p->old_lpc[0][k] = lpc_in;
+      p->lpc[k] = lpc_weight(cur, k, A.mc.lpc_gamma);
     }
   }
   __syncthreads();

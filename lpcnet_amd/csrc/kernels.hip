@@ -175,7 +175,11 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
   extern __shared__ uint4 lds4[];
   unsigned char *lds = (unsigned char *)lds4;
   using L = SampleLds<S, V>;
-  unsigned char *xa_base = lds + A.image_bytes;
+  /* the image is copied to LDS whole, or -- models whose weight sections
+   * do not fit (long block rows) -- only its fixed tables, the weights being
+   * read from the global copy (same offsets) */
+  const unsigned char *wimg = A.image_lds_bytes < A.image_bytes ? (const unsigned char *)A.image : lds;
+  unsigned char *xa_base = lds + A.image_lds_bytes;
   unsigned char *xb = xa_base + L::xa;
   float *sbuf = (float *)(xb + L::xb);
   float *zr = sbuf + S * NB;
@@ -197,7 +201,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
   bool any = false;
   for (int s = 0; s < S; s++) {
     int sid = s0 + s;
-    active[s] = sid < A.nstreams && A.st[sid].frame_count > FEATURES_DELAY;
+    active[s] = sid < A.nstreams && A.st[sid].frame_count > A.delay;
     any |= active[s];
   }
   if (!any) {
@@ -209,11 +213,11 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
   }
 
   /* weights and tables -> LDS */
-  for (int o = tid; o < A.image_bytes / 16; o += SAMPLE_THREADS) lds4[o] = A.image[o];
+  for (int o = tid; o < A.image_lds_bytes / 16; o += SAMPLE_THREADS) lds4[o] = A.image[o];
 
   const int K4z = REG ? A.ga_K4[wv][0] : 0, K4r = REG ? A.ga_K4[wv][1] : 0, K4h = REG ? A.ga_K4[wv][2] : 0;
-  const uint4 *wq = (const uint4 *)lds;
-  const uint32_t *cq = (const uint32_t *)lds;
+  const uint4 *wq = (const uint4 *)wimg;
+  const uint32_t *cq = (const uint32_t *)wimg;
 
   /* GRU_A unit state and constants: thread tid owns unit i = tid */
   const int i = tid;
@@ -289,8 +293,8 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
   if (stream_wave) pre_sample();
   __syncthreads();
 
-  const uint32_t *lds32 = (const uint32_t *)lds;
-  const uint16_t *lds16 = (const uint16_t *)lds;
+  const uint32_t *lds32 = (const uint32_t *)wimg;
+  const uint16_t *lds16 = (const uint16_t *)wimg;
   const int j8 = lane >> 3;
   /* dual_fc nodes 1..15 (tree levels 0..3) never change lane: node qq+1,
    * channel lane&1 -> weights, bias and factor held in registers */
@@ -447,7 +451,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
           for (int k = ks; k < nb; k += 8) dot_streams<S, SAT>(xa, cp[k] * (S * 4), wp[k * 8 + r], acc);
         }
         if (ks < NB / 4) {
-          uint32_t w = ((const uint32_t *)(lds + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r];
+          uint32_t w = ((const uint32_t *)(wimg + A.gb_rec_off))[(rb * (NB / 4) + ks) * 8 + r];
           dot_streams<S, SAT>(xb, ks * S * 4, w, accr);
         }
         for (int s = 0; s < S; s++) {
@@ -465,7 +469,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs A)
         const int s = lane >> 3;
         if (s < S) {
           const float4 *xf = (const float4 *)(xa_base + nxt * (NA / 4) * S * 16);
-          const float4 *wp = (const float4 *)(lds + A.gb_woff[rb] * 4);
+          const float4 *wp = (const float4 *)(wimg + A.gb_woff[rb] * 4);
           const uint16_t *cp = lds16 + A.gb_coff[rb];
           const int nb = A.gb_nb[rb];
           float y = A.gb_par[row] + condb[s * GB_ROWS + row];

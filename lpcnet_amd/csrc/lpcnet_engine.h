@@ -22,7 +22,11 @@ constexpr int NLPC = 16;       /* LPC_ORDER */
 constexpr int FRAME = 160;     /* samples per frame */
 constexpr int GA_ROWS = 3 * NA;
 constexpr int GB_ROWS = 3 * NB;
-constexpr int FEATURES_DELAY = 2;
+/* Model constants the reference bakes into the generated nnet_data.h
+ * (dump_lpcnet.py:423-446, from train_lpcnet.py --lookahead / --lpc-gamma /
+ * --end2end); here load-time parameters of a model (ModelConst). */
+constexpr int DEFAULT_FEATURES_DELAY = 2; /* dump_lpcnet.py:441 default lookahead */
+constexpr int MAX_FEATURES_DELAY = 4;     /* train_lpcnet.py:273 trims (4 - lookahead) frames: lookahead <= 4 */
 constexpr int SAMPLE_THREADS = 384; /* one thread per GRU_A unit */
 constexpr int SAMPLE_WAVES = SAMPLE_THREADS / 64;
 constexpr int STAMP_WAVES = 8;      /* stamps are [workgroup][STAMP_WAVES][16] */
@@ -78,7 +82,7 @@ struct alignas(16) StreamState {
   float gru_b_state[NB];
   float last_sig[NLPC];
   float lpc[NLPC];
-  float old_lpc[FEATURES_DELAY][NLPC];
+  float old_lpc[MAX_FEATURES_DELAY][NLPC]; /* lpc_from_cepstrum ring, first `delay` rows used */
   float conv1_mem[FIN * 2];
   float conv2_mem[COND * 2];
   float deemph_mem;
@@ -114,8 +118,19 @@ struct alignas(16) FrameCond {
   int pad[3];
 };
 
+/* FEATURES_DELAY (lookahead frames: the LPC ring depth, the conv2 clear and
+ * the silent first frames, lpcnet.c:101,109-112,239), LPC_GAMMA
+ * (lpc_weighting, lpcnet.c:116-118) and END2END (LPC from the frame
+ * network's rc outputs, lpcnet.c:56-80,107-108) of a model. */
+struct ModelConst {
+  float lpc_gamma;
+  int delay;
+  int end2end;
+};
+
 struct FrameArgs {
   StreamState *st;
+  ModelConst mc;
   int nstreams;
   const float *features; /* [B][NF] for this frame */
   const float *lpc_new;  /* [B][NLPC] lpc_from_cepstrum(features) (lpc_kernel) */
@@ -134,13 +149,14 @@ struct FrameArgs {
 
 struct SampleArgs {
   StreamState *st;
+  int delay;             /* FEATURES_DELAY: a stream synthesises once frame_count > delay (lpcnet.c:239) */
   const FrameCond *cond; /* optional [B]: read the frame's outputs here instead of st */
   int nstreams;
   int N;                 /* samples to produce (<= FRAME) */
   int nframes;           /* mf_kernel: frames per launch (0 = 1).  Frame f reads cond + f B and
                             writes pcm + f B N; needs cond, preload 0, no trace, and every
                             stream active in all or none of the frames (the host splits a run
-                            at the FEATURES_DELAY transition, STATUS_ACTIVITY otherwise) */
+                            at the `delay` transition, STATUS_ACTIVITY otherwise) */
   short *pcm;            /* [B][N] */
   int preload;           /* samples 0..preload-1 are teacher-forced from pcm (lpcnet.c:256-259) */
   const float *emb_sig, *emb_pred, *emb_exc; /* [256][GA_ROWS] */
@@ -150,6 +166,8 @@ struct SampleArgs {
   const int *gb_wsum;    /* [2][GB_ROWS] */
   const uint4 *image;    /* LDS image */
   int image_bytes;
+  int image_lds_bytes;   /* lockstep kernel: bytes of the image copied to LDS (image_bytes, or IMG_VAR
+                            when the weight sections stay in global memory) */
   int ga_K[SAMPLE_WAVES][3];   /* blocks per lane for wave w, gate g (padded) */
   int ga_woff[SAMPLE_WAVES][3];/* weight chunk offset (u32 units in image / float4 units in ga_wf) */
   int ga_coff[SAMPLE_WAVES][3];/* column-block index chunk offset (u16 units in image) */
@@ -174,8 +192,15 @@ struct SampleArgs {
   float mf_h_bound;                  /* the same for the h gate's conditioning (tanh range) */
   const float *mf_emb[3];            /* sig/pred/exc tables with columns in lane order:
                                         [256][3][SAMPLE_WAVES * 64], column p = unit mf_unit[p] */
-  int mf_nzr[SAMPLE_WAVES];
-  int mf_nh[SAMPLE_WAVES];
+  int mf_nzr[SAMPLE_WAVES];          /* own 4-slot groups per GRU_A wave: z and r */
+  int mf_nh[SAMPLE_WAVES];           /* h */
+  /* split models (rows longer than the own cap, engine.cpp mf_plan): hosted
+   * 4-slot groups after the own ones, the row each lane's hosted partial
+   * sums belong to [3 gates][SAMPLE_WAVES * 64] (NA: none) */
+  int mf_split;
+  int mf_nfzr[SAMPLE_WAVES];
+  int mf_nfh[SAMPLE_WAVES];
+  const int *mf_frow;
   const uint4 *mf_gb;
   const float4 *fp_zr, *fp_h, *fp_gb; /* fp_kernel tables (see FP_ZF) */
   const uint32_t *fp_off;
@@ -261,7 +286,7 @@ constexpr int CHUNK_MIN_FRAMES = 4; /* shorter runs use the per-frame kernel */
  * GRU_A recurrent product on v_mfma_i32_4x4x4_16b_i8 in the GRU_A waves,
  * GRU_B products on v_mfma_i32_16x16x64_i8 in the sampler waves, two
  * workgroup barriers per sample. */
-int mf_lds_bytes(int S);
+int mf_lds_bytes(int S, int split);
 int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream);
 /* fp32 latency kernel: one stream per workgroup, LDS flags instead of
  * workgroup barriers (fp32 models within the FP_* limits, dense GRU_B). */

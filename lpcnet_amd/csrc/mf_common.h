@@ -106,6 +106,86 @@ __device__ __forceinline__ void mf_run(const unsigned char *lds, const uint32_t 
   }
 }
 
+/* Split models (engine.cpp mf_plan): the z and r products over the own
+ * groups [0, no) into az / ar and over the hosted piece's groups [no, no +
+ * nf) into fz / fr (another row's partial sums); x words of the next group
+ * read while the current group's MFMAs run.  Runtime group counts: this
+ * work hides behind the sampler chain. */
+__device__ __forceinline__ void mf_zr_split(const unsigned char *lds, const uint32_t (&wz)[MF_ZMAX],
+                                            const uint32_t (&wr)[MF_ZMAX], const uint32_t (&oz)[MF_ZMAX / 2],
+                                            const uint32_t (&orr)[MF_ZMAX / 2], int no, int nf, v4i &az, v4i &ar,
+                                            v4i &fz, v4i &fr)
+{
+  const int ng = no + nf;
+  uint32_t xz[4], xr[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    xz[k] = mf_x(lds, oz, k);
+    xr[k] = mf_x(lds, orr, k);
+  }
+#pragma unroll
+  for (int g = 0; g < MF_ZMAX / 4; g++) {
+    if (g < ng) {
+      uint32_t nz[4], nr[4];
+      if (g + 1 < MF_ZMAX / 4 && g + 1 < ng) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          nz[k] = mf_x(lds, oz, 4 * (g + 1) + k);
+          nr[k] = mf_x(lds, orr, 4 * (g + 1) + k);
+        }
+      }
+      if (g < no) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          az = mfma4(xz[k], wz[4 * g + k], az);
+          ar = mfma4(xr[k], wr[4 * g + k], ar);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          fz = mfma4(xz[k], wz[4 * g + k], fz);
+          fr = mfma4(xr[k], wr[4 * g + k], fr);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        xz[k] = nz[k];
+        xr[k] = nr[k];
+      }
+    }
+  }
+}
+
+/* the same for one gate of NS slots (h) */
+template <int NS>
+__device__ __forceinline__ void mf_run_split(const unsigned char *lds, const uint32_t (&w)[NS], const uint32_t (&o)[NS / 2],
+                                             int no, int nf, v4i &a, v4i &f)
+{
+  const int ng = no + nf;
+  uint32_t x[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) x[k] = mf_x(lds, o, k);
+#pragma unroll
+  for (int g = 0; g < NS / 4; g++) {
+    if (g < ng) {
+      uint32_t n[4];
+      if (g + 1 < NS / 4 && g + 1 < ng) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) n[k] = mf_x(lds, o, 4 * (g + 1) + k);
+      }
+      if (g < no) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) a = mfma4(x[k], w[4 * g + k], a);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) f = mfma4(x[k], w[4 * g + k], f);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) x[k] = n[k];
+    }
+  }
+}
+
 /* v_mfma_i32_16x16x64_i8: A (src0) lane l = row l%16, B (src1) lane l =
  * column l%16, the 16 bytes of both = k 16(l/16) + 0..15 (any k permutation
  * common to A and B is the same product); D lane l register i = row

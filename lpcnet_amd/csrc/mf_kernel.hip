@@ -49,11 +49,14 @@ struct MfLds {
   static constexpr int okw = 8 * 4;           /* per-GRU_A-wave "inputs in range" words */
   static constexpr int gbw = 3 * 64 * 16;     /* GRU_B recurrent A tiles [3][64 lanes] (LDS, not registers) */
   static constexpr int total = x + xb + sb + ix + pcm + cnd + gbs + gbr + okw + gbw;
+  static constexpr int part = 3 * (NA + 1) * S * 4; /* split models: hosted partial sums [3][NA + 1][S] (row NA: none) */
 };
 
-int mf_lds_bytes(int S)
+int mf_lds_bytes(int S, int split)
 {
-  return IMG_VAR + (S == 4 ? MfLds<4>::total : (S == 2 ? MfLds<2>::total : MfLds<1>::total));
+  const int base = S == 4 ? MfLds<4>::total : (S == 2 ? MfLds<2>::total : MfLds<1>::total);
+  const int part = S == 4 ? MfLds<4>::part : (S == 2 ? MfLds<2>::part : MfLds<1>::part);
+  return IMG_VAR + base + (split ? part : 0);
 }
 
 /* compute_sparse_gru elementwise (nnet.c:431-447) of one GRU_A unit for S
@@ -105,7 +108,7 @@ __device__ __forceinline__ void ga_elementwise(float (&st)[S], const float (&e)[
   for (int s = 0; s < S; s++) xa_i[s * MF_XSTR] = (unsigned char)quant_s8_state(st[s]);
 }
 
-template <int S, bool TRACE>
+template <int S, bool TRACE, bool SPLIT>
 __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
 {
   extern __shared__ uint4 lds4[];
@@ -121,6 +124,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   int *gbr = gbs + S * GB_ROWS;
   int *okw = gbr + GB_ROWS;
   v4i *gbw = (v4i *)(okw + 8);
+  int *part = (int *)(gbw + 3 * 64); /* SPLIT: [3][NA + 1][S] */
   /* fixed image sections (rcpps / u-law / logit tables, dual_fc) in static
    * LDS: addresses into dynamic LDS carry an extra add of its base per
    * access, on the activation and walk chains */
@@ -140,7 +144,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   bool any = false;
   for (int s = 0; s < S; s++) {
     const int sid = s0 + s;
-    active[s] = sid < A.nstreams && frame_count_of(A, sid) > FEATURES_DELAY;
+    active[s] = sid < A.nstreams && frame_count_of(A, sid) > A.delay;
     any |= active[s];
   }
   /* multi-frame launches (A.nframes > 1): frame f reads cond + f B and
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
    * the GRU_A waves stage the next frame's inputs (GRU_A conditioning, GRU_B
    * seeds, range words) after the last sample's barrier Y, and one extra
    * barrier separates the frames.  Activity (lpcnet.c:265-268: the first
-   * FEATURES_DELAY frames of a stream give zeros and leave its state alone)
+   * `delay` (FEATURES_DELAY) frames of a stream give zeros and leave its state alone)
    * must be the same in every frame of the launch: the host splits runs at
    * that transition; a launch that sees one anyway reports STATUS_ACTIVITY. */
   const int nfr = A.nframes > 1 ? A.nframes : 1;
@@ -158,7 +162,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     const FrameCond *cl = A.cond + (size_t)(nfr - 1) * A.nstreams;
     for (int s = 0; s < S; s++) {
       const int sid = s0 + s;
-      bad |= sid < A.nstreams && (frame_count_of(A, cl, sid) > FEATURES_DELAY) != active[s];
+      bad |= sid < A.nstreams && (frame_count_of(A, cl, sid) > A.delay) != active[s];
     }
     if (bad && tid == 0 && A.status) A.status[0] = STATUS_ACTIVITY; /* plain vector store to the pinned host word */
   }
@@ -254,9 +258,16 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
       for (int t = 0; t < MF_HMAX / 2; t++) oh[t] = off(2 * MF_ZMAX + 2 * t) | (off(2 * MF_ZMAX + 2 * t + 1) << 16);
     }
     const int nzr = A.mf_nzr[wv], nh = A.mf_nh[wv];
+    /* split models: this lane's hosted groups and the rows their partial
+     * sums belong to (NA: none) */
+    const int nfzr = SPLIT ? A.mf_nfzr[wv] : 0, nfh = SPLIT ? A.mf_nfh[wv] : 0;
+    const int frz = SPLIT ? A.mf_frow[tid] : NA, frr = SPLIT ? A.mf_frow[SAMPLE_THREADS + tid] : NA,
+              frh = SPLIT ? A.mf_frow[2 * SAMPLE_THREADS + tid] : NA;
     __syncthreads(); /* image in LDS */
     bool fast = true;
     for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8_state(st[s]);
+    if constexpr (SPLIT)
+      for (int e = tid; e < 3 * (NA + 1) * S; e += SAMPLE_THREADS) part[e] = 0;
     __syncthreads(); /* initial q(h_A), q(h_B), ix, seeds */
     stamp_start();
 #ifdef MF_PRIO45
@@ -269,14 +280,26 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
      * computed right after the recurrent product (off the X->Y critical path):
      * az/ar, the (subias + diag*state) terms of z and r, and the whole
      * recurrent h-gate value (nnet.c:431-440) */
-    int az[S], ar[S], ah[S];
+    int az[S], ar[S], ah[S], hseed[S];
     float tz[S], tr[S], hpre[S];
     auto recurrent = [&]() {
       v4i vz[1] = {{wsz, wsz, wsz, wsz}}, vr[1] = {{wsr, wsr, wsr, wsr}}, vh[2] = {{wsh, wsh, wsh, wsh}, {0, 0, 0, 0}};
       mf_opaque(oz);
       mf_opaque(orr);
       mf_opaque(oh);
-      if (TRACE) {
+      if constexpr (SPLIT) {
+        /* own groups into v*, the hosted piece into f*, whose partial sums
+         * go to their row's owner through LDS (exact int32 adds, any order);
+         * the owners add them after barrier X */
+        v4i fz = {0, 0, 0, 0}, fr = {0, 0, 0, 0}, fh = {0, 0, 0, 0};
+        mf_zr_split(lds, wz, wr, oz, orr, nzr, nfzr, vz[0], vr[0], fz, fr);
+        mf_run_split<MF_HMAX>(lds, wh, oh, nh, nfh, vh[0], fh);
+        for (int s = 0; s < S; s++) {
+          atomicAdd(&part[(0 * (NA + 1) + frz) * S + s], fz[s]);
+          atomicAdd(&part[(1 * (NA + 1) + frr) * S + s], fr[s]);
+          atomicAdd(&part[(2 * (NA + 1) + frh) * S + s], fh[s]);
+        }
+      } else if (TRACE) {
         mf_zr<1>(lds, wz, wr, oz, orr, nzr, vz, vr);
         mf_run<MF_HMAX, 2>(lds, wh, oh, nh, vh);
       } else {
@@ -310,7 +333,10 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         ah[s] = vh[0][s] + vh[1][s];
         tz[s] = bz + dz * st[s];
         tr[s] = br + dr * st[s];
-        hpre[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
+        if constexpr (SPLIT)
+          hseed[s] = cvt_rne((bh + dh * st[s]) * kScale);
+        else
+          hpre[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
       }
     };
     recurrent();
@@ -373,6 +399,20 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
               }
             }
           }
+          if constexpr (SPLIT) {
+            /* the hosted pieces' partial sums of this lane's rows (written
+             * between barriers Y and X), then cleared for the next sample */
+            for (int s = 0; s < S; s++) {
+              int *pz = &part[(0 * (NA + 1) + i) * S + s], *pr = &part[(1 * (NA + 1) + i) * S + s],
+                  *ph = &part[(2 * (NA + 1) + i) * S + s];
+              az[s] += *pz;
+              ar[s] += *pr;
+              hpre[s] = (float)((ah[s] + *ph) + hseed[s]) * kScale1;
+              *pz = 0;
+              *pr = 0;
+              *ph = 0;
+            }
+          }
           if (stamping) {
             /* diagnostic only: wait for every gather before the stamp */
             float g = 0.f;
@@ -416,13 +456,13 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     const bool samp = my_s < S;                         /* wave-uniform */
     const bool samp_w = samp && (S == 4 || half == 0);  /* lanes owning the stream's outputs */
     const int ms = samp ? my_s : 0;
-    const bool my_active = samp && s0 + ms < A.nstreams && frame_count_of(A, s0 + ms) > FEATURES_DELAY;
+    const bool my_active = samp && s0 + ms < A.nstreams && frame_count_of(A, s0 + ms) > A.delay;
     /* GRU_B: lane = (unit quad gq, stream gs, gi): unit gu = 4gq + gi of
      * stream gs; the MFMA columns are (gs, gi), so D register gi of this lane
      * holds row 4gq + gi.  gown: stream gs is one of this wave's. */
     const int gq = lane >> 4, gs = (lane & 15) >> 2, gi = lane & 3, gu = 4 * gq + gi, sl = min(gs, S - 1);
     const bool gown = gs < S && (S == 4 ? (gs >> 1) : gs) == sw;
-    const bool gact = gown && s0 + gs < A.nstreams && frame_count_of(A, s0 + gs) > FEATURES_DELAY;
+    const bool gact = gown && s0 + gs < A.nstreams && frame_count_of(A, s0 + gs) > A.delay;
 
     float lsr[NLPC], lpr[NLPC];
     float pred = 0.f, deemph = 0.f;
@@ -646,20 +686,22 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   }
 }
 
-template <int S, bool TRACE>
+template <int S, bool TRACE, bool SPLIT>
 static int launch_mf_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
 {
-  if (ensure_dyn_lds((const void *)mf_kernel<S, TRACE>, 160 * 1024 - IMG_VAR)) return -1;
+  if (ensure_dyn_lds((const void *)mf_kernel<S, TRACE, SPLIT>, 160 * 1024 - IMG_VAR)) return -1;
   const int grid = warm_grid((a.nstreams + S - 1) / S, a.nstreams);
   /* lds_bytes counts the static image too (mf_lds_bytes) */
-  hipLaunchKernelGGL((mf_kernel<S, TRACE>), dim3(grid), dim3(MF_THREADS), lds_bytes - IMG_VAR, stream, a);
+  hipLaunchKernelGGL((mf_kernel<S, TRACE, SPLIT>), dim3(grid), dim3(MF_THREADS), lds_bytes - IMG_VAR, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 template <int S>
 static int launch_mf_s(const SampleArgs &a, int lds_bytes, hipStream_t st)
 {
-  return a.trace_logits ? launch_mf_t<S, true>(a, lds_bytes, st) : launch_mf_t<S, false>(a, lds_bytes, st);
+  if (a.mf_split)
+    return a.trace_logits ? launch_mf_t<S, true, true>(a, lds_bytes, st) : launch_mf_t<S, false, true>(a, lds_bytes, st);
+  return a.trace_logits ? launch_mf_t<S, true, false>(a, lds_bytes, st) : launch_mf_t<S, false, false>(a, lds_bytes, st);
 }
 
 int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream)

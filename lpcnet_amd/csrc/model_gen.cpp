@@ -21,6 +21,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -100,7 +101,30 @@ struct Sparse {
   std::vector<std::vector<std::vector<float>>> w; /* per block: 32 floats [r][c] */
 };
 
-Sparse make_sparse(Rng &r, int nout, int nin, const float density[3], float amp, bool saturate)
+/* Block mask of one gate as training_tf2/lpcnet.py:140-160 (Sparsify)
+ * chooses it: the blocks whose energy reaches a GLOBAL per-gate threshold
+ * (the (1 - density) quantile).  With skew, output rows (and input columns)
+ * carry heterogeneous energy -- log-normal row / column scales -- so the
+ * kept blocks pile up on the strong rows: block rows far above the mean
+ * length, as a trained model's can be. */
+std::vector<char> sparsify_mask(Rng &r, int rows, int cols, int want, float row_sigma, float col_sigma)
+{
+  std::vector<float> rs(rows), cs(cols), e((size_t)rows * cols);
+  for (auto &v : rs) v = expf(row_sigma * r.gauss());
+  for (auto &v : cs) v = expf(col_sigma * r.gauss());
+  for (int i = 0; i < rows; i++)
+    for (int j = 0; j < cols; j++) e[(size_t)i * cols + j] = rs[i] * cs[j] * (0.5f + r.uni());
+  std::vector<float> sorted(e);
+  std::sort(sorted.begin(), sorted.end());
+  const float thresh = sorted[sorted.size() - (size_t)want];
+  std::vector<char> mask(e.size(), 0);
+  int have = 0;
+  for (size_t k = 0; k < e.size(); k++)
+    if (e[k] >= thresh && have < want) { mask[k] = 1; have++; }
+  return mask;
+}
+
+Sparse make_sparse(Rng &r, int nout, int nin, const float density[3], float amp, bool saturate, float skew = 0.f)
 {
   Sparse s;
   s.nout = nout;
@@ -113,11 +137,15 @@ Sparse make_sparse(Rng &r, int nout, int nin, const float density[3], float amp,
     int total = gate_rows * nib;
     int want = (int)lrint(density[g] * total);
     std::vector<char> mask(total, 0);
-    int have = 0;
-    for (int i = 0; i < total && have < want; i++) {
-      /* selection sampling: pick with probability (want-have)/(total-i) */
-      uint32_t u = r.next() % (uint32_t)(total - i);
-      if ((int)u < want - have) { mask[i] = 1; have++; }
+    if (skew > 0.f) {
+      mask = sparsify_mask(r, gate_rows, nib, want, skew, 0.5f * skew);
+    } else {
+      int have = 0;
+      for (int i = 0; i < total && have < want; i++) {
+        /* selection sampling: pick with probability (want-have)/(total-i) */
+        uint32_t u = r.next() % (uint32_t)(total - i);
+        if ((int)u < want - have) { mask[i] = 1; have++; }
+      }
     }
     for (int ob = 0; ob < gate_rows; ob++)
       for (int ib = 0; ib < nib; ib++)
@@ -181,6 +209,9 @@ extern "C" LPCNET_EXPORT int lpcnet_mi355x_synthetic_model(unsigned seed, int va
   Rng r;
   r.seed("lpcnet-mi355x-synthetic-model", seed);
   bool sat = (flags & 1) != 0;
+  /* flags bit 1: GRU_A masks chosen like Sparsify with skewed row energy
+   * (trained-model-like block rows: tens of blocks on the strongest rows) */
+  const float skew = (flags & 2) ? 1.0f : 0.f;
   Blob blob;
   /* frame network (lpcnet.py:333-358) */
   blob.addf("embed_pitch_weights", uvec(r, 256 * EP, 0.5f));
@@ -247,7 +278,7 @@ extern "C" LPCNET_EXPORT int lpcnet_mi355x_synthetic_model(unsigned seed, int va
   /* sparse GRU_A (dump_lpcnet.py:124-170) */
   {
     const float dens[3] = {0.05f, 0.05f, 0.2f};
-    Sparse sa = make_sparse(r, 3 * NA, NA, dens, 0.6f, sat);
+    Sparse sa = make_sparse(r, 3 * NA, NA, dens, 0.6f, sat, skew);
     std::vector<double> colsum;
     blob.addf("sparse_gru_a_recurrent_weights_diag", uvec(r, 3 * NA, 0.5f));
     emit_sparse(blob, sa, "sparse_gru_a_recurrent_weights", "sparse_gru_a_recurrent_weights_idx", variant, &colsum);

@@ -24,8 +24,8 @@
 #define NB 16
 #define CONV_K 3
 #define FEATURES_DELAY 2 /* dump_lpcnet.py:442 default lookahead */
+#define MAX_FEATURES_DELAY 4 /* train_lpcnet.py:273: lookahead <= 4 */
 #define CONV1_DELAY 1    /* dump_lpcnet.py:306 (k-1)//2 */
-#define LPC_GAMMA 1.0f   /* dump_lpcnet.py:431 default */
 #define LPC_ORDER 16
 #define FRAME_SIZE 160
 #define PREEMPH 0.85f /* lpcnet.c:40 */
@@ -570,6 +570,9 @@ struct OracleState {
   const int *gb_idx;
   const float *fc_w, *fc_b, *fc_factor;
   float logit_table[256];
+  /* model constants (nnet_data.h #defines, dump_lpcnet.py:423-446) */
+  float lpc_gamma;
+  int delay, end2end;
   oracle_rng rng;
   /* dynamic state (cleared by reset) */
   float conv1_mem[FRAME_INPUT * (CONV_K - 1)];
@@ -578,7 +581,7 @@ struct OracleState {
   float gru_b_state[NB];
   int last_exc;
   float last_sig[LPC_ORDER];
-  float old_lpc[FEATURES_DELAY][LPC_ORDER];
+  float old_lpc[MAX_FEATURES_DELAY][LPC_ORDER];
   float gru_a_cond[3 * NA];
   float gru_b_cond[3 * NB];
   int frame_count;
@@ -635,6 +638,9 @@ OracleState *oracle_create(const unsigned char *blob, int len, int variant, cons
   F(st->fc_w, "dual_fc_weights", NB * 2 * NLEVELS);
   F(st->fc_factor, "dual_fc_factor", 2 * NLEVELS);
 #undef F
+  st->lpc_gamma = 1.f;
+  st->delay = FEATURES_DELAY;
+  st->end2end = 0;
   /* lpcnet.c:188-191 */
   for (int i = 0; i < 256; i++) {
     float prob = .025f + .95f * i / 255.f;
@@ -661,6 +667,15 @@ void oracle_reset(OracleState *st)
   memset(st->conv1_mem, 0, (char *)&st->t_logits - (char *)st->conv1_mem);
   st->last_exc = st->k->lin2ulaw(0.f);
   st->k->rng_srand(&st->rng, (const unsigned char *)"LPCNet", 6);
+}
+
+int oracle_set_constants(OracleState *st, float lpc_gamma, int features_delay, int end2end)
+{
+  if (features_delay < 0 || features_delay > MAX_FEATURES_DELAY || (end2end != 0 && end2end != 1)) return -1;
+  st->lpc_gamma = lpc_gamma;
+  st->delay = features_delay;
+  st->end2end = end2end;
+  return 0;
 }
 
 void oracle_set_trace(OracleState *st, float *logits8, int *exc, uint32_t *rng_words2)
@@ -705,6 +720,18 @@ static void conv1d(const OracleState *st, float *out, float *mem, const float *w
   memcpy(mem, &tmp[nin], nin * (CONV_K - 1) * sizeof(float));
 }
 
+/* lpcnet.c:56-80 rc2lpc (END2END models), as written */
+static void rc2lpc(float *lpc, const float *rc)
+{
+  float tmp[LPC_ORDER], ntmp[LPC_ORDER] = {0};
+  memcpy(tmp, rc, sizeof(tmp));
+  for (int i = 0; i < LPC_ORDER; i++) {
+    for (int j = 0; j <= i - 1; j++) ntmp[j] = tmp[j] + tmp[i] * tmp[i - j - 1];
+    for (int k = 0; k <= i - 1; k++) tmp[k] = ntmp[k];
+  }
+  for (int i = 0; i < LPC_ORDER; i++) lpc[i] = tmp[i];
+}
+
 /* lpcnet.c:82-120 run_frame_network */
 static void run_frame_network(OracleState *st, const float *features)
 {
@@ -716,15 +743,21 @@ static void run_frame_network(OracleState *st, const float *features)
   conv1d(st, conv1_out, st->conv1_mem, st->conv1_w, st->conv1_b, FRAME_INPUT, in);
   if (st->frame_count < CONV1_DELAY) memset(conv1_out, 0, sizeof(conv1_out));
   conv1d(st, conv2_out, st->conv2_mem, st->conv2_w, st->conv2_b, COND, conv1_out);
-  if (st->frame_count < FEATURES_DELAY) memset(conv2_out, 0, sizeof(conv2_out));
+  if (st->frame_count < st->delay) memset(conv2_out, 0, sizeof(conv2_out));
   dense(st, dense1_out, st->dense1_w, st->dense1_b, COND, COND, 1, conv2_out);
   dense(st, condition, st->dense2_w, st->dense2_b, COND, COND, 1, dense1_out);
   dense(st, st->gru_a_cond, st->gadf_w, st->gadf_b, COND, 3 * NA, 0, condition);
   dense(st, st->gru_b_cond, st->gbdf_w, st->gbdf_b, COND, 3 * NB, 0, condition);
-  memcpy(st->lpc, st->old_lpc[FEATURES_DELAY - 1], sizeof(st->lpc));
-  memmove(st->old_lpc[1], st->old_lpc[0], (FEATURES_DELAY - 1) * LPC_ORDER * sizeof(float));
-  st->k->lpc_from_cepstrum(st->old_lpc[0], features);
-  st->k->lpc_weighting(st->lpc, LPC_GAMMA);
+  if (st->end2end) {
+    rc2lpc(st->lpc, condition); /* lpcnet.c:104,107-108: rc = condition[0..LPC_ORDER) */
+  } else if (st->delay > 0) {   /* lpcnet.c:109-112 */
+    memcpy(st->lpc, st->old_lpc[st->delay - 1], sizeof(st->lpc));
+    memmove(st->old_lpc[1], st->old_lpc[0], (st->delay - 1) * LPC_ORDER * sizeof(float));
+    st->k->lpc_from_cepstrum(st->old_lpc[0], features);
+  } else {                      /* lpcnet.c:113-114 */
+    st->k->lpc_from_cepstrum(st->lpc, features);
+  }
+  st->k->lpc_weighting(st->lpc, st->lpc_gamma); /* lpcnet.c:116-118 */
   if (st->frame_count < 1000) st->frame_count++;
 }
 
@@ -816,7 +849,7 @@ static int run_sample_network(OracleState *st, int last_exc, int last_sig, int p
 /* lpcnet.c:235-271 lpcnet_synthesize_tail_impl */
 static void synthesize_tail(OracleState *st, short *output, int N, int preload)
 {
-  if (st->frame_count <= FEATURES_DELAY) {
+  if (st->frame_count <= st->delay) {
     memset(output, 0, N * sizeof(short));
     return;
   }

@@ -88,6 +88,11 @@ void oracle_reset(OracleState *st);
 /* lpcnet.c:273-277 lpcnet_synthesize_impl(st, features, output, N, preload) */
 void oracle_synthesize(OracleState *st, const float *features, short *output, int N, int preload);
 
+/* Model constants the reference compiles in from nnet_data.h
+ * (dump_lpcnet.py:423-446): LPC_GAMMA, FEATURES_DELAY (0..4), END2END.
+ * Defaults 1.0, 2, 0.  Returns -1 for an unsupported value. */
+int oracle_set_constants(OracleState *st, float lpc_gamma, int features_delay, int end2end);
+
 /* Optional per-sample trace (pointers may be NULL); each call to
  * oracle_synthesize writes up to N entries from index 0. */
 void oracle_set_trace(OracleState *st, float *logits8, int *exc, uint32_t *rng_words2);

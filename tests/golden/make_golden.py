@@ -132,16 +132,20 @@ STREAMS = (0, 1, 7)
 NFRAMES = 40
 
 
-def stream_fixture(name, variant, saturating):
+def stream_fixture(name, variant, saturating, constants=None, STREAMS=STREAMS, NFRAMES=NFRAMES):
+    """constants: (LPC_GAMMA, FEATURES_DELAY, END2END) of a trained model's
+    nnet_data.h (dump_lpcnet.py:423-446); None = the dump defaults."""
     blob = L.synthetic_model(1, variant, saturating)
     d = {"blob_sha256": np.frombuffer(hashlib.sha256(blob).digest(), np.uint8), "variant": np.int32(variant),
          "streams": np.array(STREAMS, np.int32)}
+    if constants is not None:
+        d["constants"] = np.array(constants, np.float64)
     pcm = np.zeros((len(STREAMS), NFRAMES, 160), np.int16)
     feats = np.zeros((len(STREAMS), NFRAMES, 36), np.float32)
     for si, s in enumerate(STREAMS):
         f = L.synthetic_features(s, NFRAMES)
         feats[si] = f
-        o = O.Oracle(blob, variant, O.ref_kernels())
+        o = O.Oracle(blob, variant, O.ref_kernels(), constants)
         logits = np.zeros((4, 160, 8), np.float32)
         exc = np.zeros((4, 160), np.int32)
         rngw = np.zeros((4, 160, 2), np.uint32)
@@ -161,14 +165,27 @@ def stream_fixture(name, variant, saturating):
     d["pcm"], d["features"] = pcm, feats
     # self-check: the portable kernels reproduce the reference kernels end to end
     for si, s in enumerate(STREAMS):
-        port = O.synth_stream(blob, feats[si], variant)
+        port = O.synth_stream(blob, feats[si], variant, constants=constants)
         assert np.array_equal(port, pcm[si]), f"{name}: port kernels diverge from reference kernels (stream {s})"
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
     print(name, "rms", float(np.sqrt(np.mean(pcm.astype(np.float64) ** 2))))
 
 
+# trained-model constants other than the dump defaults (round 3): the
+# reference's compiled lpc_weighting (freq.c:299-308) and lpc_from_cepstrum
+# drive the LPC ring of each depth; rc2lpc (lpcnet.c:56-80, END2END) is the
+# oracle's restatement (lpcnet.c is not compilable here)
+CONST_FIXTURES = [("streams_int8_g092_d3", 0, (0.92, 3, 0)), ("streams_int8_g095_d0", 0, (0.95, 0, 0)),
+                  ("streams_int8_e2e_g09_d1", 0, (0.9, 1, 1)), ("streams_fp32_g092_d4", 1, (0.92, 4, 0))]
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["constants"]:
+        for name, variant, c in CONST_FIXTURES:
+            stream_fixture(name, variant, False, c, STREAMS=(0, 5), NFRAMES=12)
+        sys.exit(0)
     kernels_fixture()
     stream_fixture("streams_int8", 0, False)
     stream_fixture("streams_fp32", 1, False)
     stream_fixture("streams_int8_sat", 0, True)
+    for name, variant, c in CONST_FIXTURES:
+        stream_fixture(name, variant, False, c, STREAMS=(0, 5), NFRAMES=12)

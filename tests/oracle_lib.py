@@ -34,6 +34,7 @@ for name, res, args in [
     ("oracle_reset", None, [_vp]),
     ("oracle_synthesize", None, [_vp, _vp, _vp, _i, _i]),
     ("oracle_set_trace", None, [_vp, _vp, _vp, _vp]),
+    ("oracle_set_constants", _i, [_vp, C.c_float, _i, _i]),
     ("oracle_get_frame", None, [_vp, _vp, _vp, _vp]),
     ("oracle_frame_count", _i, [_vp]),
     ("oracle_get_state", None, [_vp, _vp, _vp]),
@@ -100,10 +101,16 @@ def kernel_table(k: C.c_void_p):
 class Oracle:
     """One reference-semantics synthesis stream on the CPU."""
 
-    def __init__(self, blob: bytes, variant: int = 0, kernels=None):
+    def __init__(self, blob: bytes, variant: int = 0, kernels=None, constants=None):
+        """constants: (LPC_GAMMA, FEATURES_DELAY, END2END) of the model, the
+        #defines the reference compiles in from nnet_data.h; default (1.0, 2, 0)."""
         self._st = _ora.oracle_create(blob, len(blob), variant, kernels or port_kernels())
         if not self._st:
             raise ValueError("oracle_create: blob rejected")
+        if constants is not None:
+            g, d, e = constants
+            if _ora.oracle_set_constants(self._st, g, int(d), int(e)) != 0:
+                raise ValueError("oracle_set_constants: unsupported value")
 
     def synthesize(self, features: np.ndarray, n: int = 160, preload: np.ndarray | None = None,
                    trace: bool = False):
@@ -150,8 +157,9 @@ class Oracle:
             pass
 
 
-def synth_stream(blob: bytes, feats: np.ndarray, variant: int = 0, kernels=None, n: int = 160) -> np.ndarray:
-    o = Oracle(blob, variant, kernels)
+def synth_stream(blob: bytes, feats: np.ndarray, variant: int = 0, kernels=None, n: int = 160,
+                 constants=None) -> np.ndarray:
+    o = Oracle(blob, variant, kernels, constants)
     return np.stack([o.synthesize(feats[f], n) for f in range(len(feats))])
 
 

@@ -123,6 +123,56 @@ def test_oracle_stream_golden(name, variant):
             assert np.array_equal(bits(np.concatenate([a, b, lpc])), bits(G["frame_cond"][fr]))
 
 
+CONST_FIXTURES = ["streams_int8_g092_d3", "streams_int8_g095_d0", "streams_int8_e2e_g09_d1", "streams_fp32_g092_d4"]
+
+
+@pytest.mark.parametrize("name", CONST_FIXTURES)
+def test_oracle_model_constants_golden(name):
+    """Trained-model constants (LPC_GAMMA, FEATURES_DELAY, END2END;
+    dump_lpcnet.py:423-446): the portable oracle reproduces the fixtures made
+    with the reference's compiled lpc_weighting / lpc_from_cepstrum, both
+    fixture streams, every frame, and the silent first FEATURES_DELAY frames."""
+    import lpcnet_amd as L
+    G = np.load(os.path.join(O.GOLDEN, name + ".npz"))
+    g, d, e = G["constants"]
+    variant = int(G["variant"])
+    blob = L.synthetic_model(1, variant)
+    for si in range(len(G["streams"])):
+        o = O.Oracle(blob, variant, constants=(float(g), int(d), int(e)))
+        for fr in range(G["pcm"].shape[1]):
+            pcm = o.synthesize(G["features"][si, fr])
+            assert np.array_equal(pcm, G["pcm"][si, fr]), (si, fr)
+            if si == 0 and fr < 6:
+                a, b, lpc = o.frame()
+                assert np.array_equal(bits(np.concatenate([a, b, lpc])), bits(G["frame_cond"][fr])), fr
+        assert np.all(G["pcm"][si, :int(d)] == 0) and np.any(G["pcm"][si, int(d)] != 0)
+
+
+def test_oracle_rejects_bad_constants():
+    import lpcnet_amd as L
+    blob = L.synthetic_model(1, 0)
+    for c in ((1.0, 5, 0), (1.0, -1, 0), (1.0, 2, 2)):
+        with pytest.raises(ValueError):
+            O.Oracle(blob, 0, constants=c)
+
+
+def test_engine_reads_and_validates_constant_records():
+    """The engine takes the constants from optional blob records named like
+    nnet_data.h's #defines (validated host-side, no GPU), rejects malformed
+    or unsupported ones; the records do not disturb any other array."""
+    import lpcnet_amd as L
+    blob = L.synthetic_model(1, 0)
+    L.validate_model(L.with_model_constants(blob, 0.92, 3, True))
+    L.validate_model(L.with_model_constants(blob, 1.0, 0, False))
+    for kw in ({"features_delay": 5}, {"features_delay": -1}, {"lpc_gamma": float("inf")}):
+        with pytest.raises(L.LPCNetError):
+            L.validate_model(L.with_model_constants(blob, **kw))
+    bad = bytearray(L.with_model_constants(blob, end2end=True))
+    bad[-64 + 0] = 7  # END2END = 7
+    with pytest.raises(L.LPCNetError, match="END2END"):
+        L.validate_model(bytes(bad))
+
+
 def test_oracle_rejects_bad_blob():
     import lpcnet_amd as L
     blob = bytearray(L.synthetic_model(1, 0))
