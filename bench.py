@@ -77,6 +77,7 @@ def parse():
     p.add_argument("--no-batch1", action="store_true", help="skip the batch1 / batch1_fp32 / batch256 lines")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-latency", action="store_true", help="skip the stamped latency run")
+    p.add_argument("--no-capacity", action="store_true", help="skip the measured real-time capacity ladder")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--preheat-ms", type=float, default=100.0,
                    help="untimed load before the warmup (DPM clock ramp), then every stream is reset")
@@ -360,6 +361,60 @@ def side_line(L, blob, B, args, config, variant_name):
     return out
 
 
+def capacity(L, blob, args, ladder=(1024, 1025, 1536, 2048, 4096, 8192, 16384, 24576, 28672, 32768)):
+    """Measured real-time capacity of one GPU: the whole frame step (LPC,
+    frame network, 160 samples of every stream; device-resident I/O) timed
+    at each batch size of the ladder, including the non-multiples 1025 and
+    1536 of the 4-streams-per-workgroup, 1024-streams-per-round layout; a
+    batch is real-time while its frame step stays <= 10 ms.  The largest
+    real-time batch is then bracketed by bisection (multiples of 256)."""
+    steps = 6
+    rows = {}
+
+    def run(B):
+        dt, _, info, _ = run_batch(L, blob, B, 0, 2, steps, None, 0, 0.0)
+        ms = dt / steps * 1e3
+        rows[B] = {"frame_step_ms": ms, "samples_per_s": B * 160 * steps / dt, "realtime": ms <= 10.0,
+                   "streams_per_workgroup": info.streams_per_workgroup}
+        return ms
+
+    ok, bad = 0, None
+    for B in ladder:
+        if run(B) <= 10.0:
+            ok = max(ok, B)
+        else:
+            bad = B
+            break
+    if bad is not None:
+        lo, hi = ok, bad
+        while hi - lo > 256:
+            mid = (lo + hi) // 2 // 256 * 256
+            if mid <= lo:
+                break
+            if run(mid) <= 10.0:
+                lo = mid
+            else:
+                hi = mid
+        ok = lo
+    return {"max_realtime_streams": ok, "criterion": "frame step (10 ms of audio for every stream) <= 10 ms, measured",
+            "steps_per_point": steps, "ladder": {str(k): v for k, v in sorted(rows.items())}}
+
+
+def skewed_lines(L, args):
+    """A trained-model-like sparsity pattern (Sparsify's global per-gate
+    threshold over skewed block energies, training_tf2/lpcnet.py:140-160:
+    block rows of up to 76 (z/r) and 96 (h) blocks): which kernel runs it and
+    its throughput at the three batch sizes of the default-model lines."""
+    blob = L.synthetic_model(1, L.VARIANT_INT8, skewed=True)
+    out = {}
+    for B in (1, 256, 1024):
+        nf = max(args.steps, 20)
+        dt, (k, n, kf, _, _), info, _ = run_batch(L, blob, B, 0, args.warmup, nf, None, args.timers, args.preheat_ms)
+        out[f"b{B}"] = {"samples_per_s": B * nf * 160 / dt, "sample_kernel_ms_per_frame": k / max(kf, 1),
+                        "kernel": info.kernel_name, "quad_path": info.quad_path}
+    return out
+
+
 def main():
     args = parse()
     world, rank, local, dist = dist_setup(args)
@@ -413,6 +468,10 @@ def main():
         out["batch1_fp32"] = side_line(L, L.synthetic_model(1, L.VARIANT_FP32), 1, args, "b1_fp32", "fp32")
         # BASELINE configs[2]: 256 streams on one GPU (int8 products on the matrix cores)
         out["batch256"] = side_line(L, blob, 256, args, "b256", "int8")
+    if rank == 0 and world == 1 and not args.no_batch1:
+        out["skewed_int8"] = skewed_lines(L, args)
+    if rank == 0 and world == 1 and not args.no_capacity:
+        out["capacity"] = capacity(L, blob, args)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         # beside batch1_fp32 (configs[1]): the reference's fp32 build on the same cores

@@ -37,7 +37,10 @@ typedef struct {
   double ops_per_sample;          /* 2*MAC per stream per sample */
   int streams_per_workgroup;      /* streams per sample-kernel workgroup */
   int quad_path;                  /* sample kernel: 0 lockstep (per-slot LDS layout), 1 lockstep (quad
-                                     LDS layout), 4 mf_kernel (matrix cores), 5 fp_kernel (fp32) */
+                                     LDS layout), 4 mf_kernel (matrix cores), 5 fp_kernel (fp32),
+                                     6 mf2_kernel (matrix cores, two staggered 4-stream groups per
+                                     workgroup; batches >= 2048; launches with preload or trace
+                                     take mf_kernel) */
   int lds_bytes;                  /* dynamic LDS of the sample kernel */
   double mfma_ops_per_group_sample; /* int8 matrix-core ops issued per workgroup per sample
                                        (mf_kernel; padding included), 0 otherwise */
@@ -204,6 +207,12 @@ LPCNET_EXPORT int lpcnet_mi355x_device_numerics(int device, int op, const void *
 LPCNET_EXPORT int lpcnet_mi355x_validate_model(const unsigned char *data, int len);
 /* Number of visible HIP devices (0 on a machine without GPU). */
 LPCNET_EXPORT int lpcnet_mi355x_device_count(void);
+/* The drop-in handles (include/lpcnet.h) bound to the same model on the
+ * same device share one device copy of it and one work batch; concurrent
+ * lpcnet_synthesize calls on them coalesce into one launch.  Statistics of
+ * the pool `st` belongs to: coalesced launches, handled requests, handles
+ * bound.  -1 if st is not bound. */
+LPCNET_EXPORT int lpcnet_mi355x_pool_stats(const LPCNetState *st, long *launches, long *requests, int *streams);
 /* Last error string of this thread. */
 LPCNET_EXPORT const char *lpcnet_mi355x_last_error(void);
 

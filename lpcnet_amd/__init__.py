@@ -116,7 +116,9 @@ class ModelInfo(C.Structure):
         (as rocprofv3 names it)."""
         sat = "true" if self.may_saturate else "false"
         if self.quad_path == 4:
-            return f"mf_kernel<{self.streams_per_workgroup}, false>"
+            return f"mf_kernel<{self.streams_per_workgroup}, false, false>"
+        if self.quad_path == 6:
+            return "mf2_kernel<4>"
         if self.quad_path == 5:
             return "fp_kernel<false>"
         quad = "true" if self.quad_path == 1 else "false"

@@ -24,6 +24,7 @@
 #include <cmath>
 #include <cstddef>
 #include <atomic>
+#include <condition_variable>
 #include <functional>
 #include <map>
 #include <mutex>
@@ -307,6 +308,8 @@ struct LPCNetBatch {
   ModelConst mc{1.0f, DEFAULT_FEATURES_DELAY, 0}; /* FEATURES_DELAY / LPC_GAMMA / END2END of the model */
   bool mf_ok = false;    /* model fits the matrix-core register tables */
   bool mf = false;       /* mf_kernel (mode 4) */
+  bool mf2 = false;      /* large batches: mf2_kernel (two staggered 4-stream groups per workgroup) for
+                            launches without preload / trace / stamps */
   double mf_ga_ops = 0;  /* int8 matrix-core ops per workgroup per sample: the GRU_A recurrent pass */
   double mf_gb_ops = 0;  /* the GRU_B tiles of both sampler waves */
   bool fp_ok = false;    /* fp32 model fits the fp_kernel tables */
@@ -417,6 +420,7 @@ bool block_may_saturate(const int8_t *w)
 void choose_kernel(LPCNetBatch *b)
 {
   b->mf = false;
+  b->mf2 = false;
   b->fp = false;
   b->info.mfma_ops_per_group_sample = 0;
   int mode = b->kernel_mode;
@@ -434,6 +438,17 @@ void choose_kernel(LPCNetBatch *b)
     b->info.streams_per_workgroup = b->S;
     b->info.lds_bytes = mf_lds_bytes(b->S, b->sa.mf_split);
     b->info.quad_path = 4;
+    /* two staggered 4-stream groups per workgroup from MF2_MIN_STREAMS on
+     * (LPCNET_MF2=0 off, =1 at any batch size) */
+    const char *e2 = getenv("LPCNET_MF2");
+    const bool want2 = e2 ? atoi(e2) != 0 : b->B >= MF2_MIN_STREAMS;
+    if (want2 && !b->sa.mf_split && mf2_lds_bytes(4) <= 160 * 1024) {
+      b->mf2 = true;
+      b->info.mfma_ops_per_group_sample = 2 * (b->mf_ga_ops + b->mf_gb_ops);
+      b->info.streams_per_workgroup = 8;
+      b->info.lds_bytes = mf2_lds_bytes(4);
+      b->info.quad_path = 6;
+    }
     return;
   }
   b->info.streams_per_workgroup = b->S;
@@ -1352,20 +1367,23 @@ int ensure_trace(LPCNetBatch *b, int N)
  * computed earlier on the same queue (lpcnet_batch_synthesize_frames
  * batches it over many frames). */
 int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_frame, bool run_lpc, short *d_pcm, int N,
-                      int preload = 0, int ovl = -1)
+                      int preload = 0, int ovl = -1, int nB = -1)
 {
+  /* nB: run the first nB streams of the batch only (the drop-in pool's work
+   * batch); the overlapped form always runs all of them */
+  if (nB < 0 || ovl >= 0) nB = b->B;
   const int c = ovl & 1;
   hipStream_t fs = ovl >= 0 ? b->fstream : b->stream;
   FrameArgs fa = b->fa;
   fa.st = b->d_state;
   fa.mc = b->mc;
-  fa.nstreams = b->B;
+  fa.nstreams = nB;
   fa.features = d_features;
   fa.lpc_new = d_lpc_frame;
   SampleArgs sa = b->sa;
   sa.st = b->d_state;
   sa.delay = b->mc.delay;
-  sa.nstreams = b->B;
+  sa.nstreams = nB;
   sa.N = N;
   sa.pcm = d_pcm;
   sa.preload = std::max(0, std::min(preload, N));
@@ -1389,7 +1407,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
   if (e[0]) HIPCHK(hipEventRecord(e[0], fs));
   /* lpc_from_cepstrum of this frame's features: the frame kernel pushes it
    * into the two-frame LPC ring (lpcnet.c:110-112) */
-  if (run_lpc && !b->mc.end2end && launch_lpc(d_features, d_lpc_frame, b->B, b->d_lpc_tab, fs)) {
+  if (run_lpc && !b->mc.end2end && launch_lpc(d_features, d_lpc_frame, nB, b->d_lpc_tab, fs)) {
     set_err("lpc kernel launch failed");
     return -1;
   }
@@ -1413,7 +1431,8 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   const int lrc = N <= 0 ? 0
                 : b->fp    ? launch_fp(sa, b->stream)
-                : b->mf    ? launch_mf(sa, b->S, b->info.lds_bytes, b->stream)
+                : b->mf2 && !sa.preload && !sa.trace_logits && !sa.stamps ? launch_mf2(sa, 4, b->stream)
+                : b->mf    ? launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream)
                              : launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream);
   if (lrc) {
     set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -1473,7 +1492,10 @@ int launch_chunk_samples(LPCNetBatch *b, int f, short *d_pcm, int N, int nfr = 1
     e2 = get_event(b);
     HIPCHK(hipEventRecord(e1, b->stream));
   }
-  const int lrc = N <= 0 ? 0 : b->fp ? launch_fp(sa, b->stream) : launch_mf(sa, b->S, b->info.lds_bytes, b->stream);
+  const int lrc = N <= 0                                  ? 0
+                  : b->fp                                 ? launch_fp(sa, b->stream)
+                  : b->mf2 && !sa.trace_logits && !sa.stamps ? launch_mf2(sa, 4, b->stream)
+                                                          : launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream);
   if (lrc) {
     set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     return -1;
@@ -1723,20 +1745,27 @@ LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b)
   b->min_fc = v[0].frame_count;
 }
 
-LPCNET_EXPORT int lpcnet_batch_synthesize_impl(LPCNetBatch *b, const float *features, short *pcm, int N, int preload)
+/* one frame for the first nB streams of a batch, host I/O ([nB][NF] in,
+ * [nB][N] out) */
+static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm, int N, int preload)
 {
   if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
   if (N < 0 || N > FRAME || !features || (N > 0 && !pcm) || preload < 0) { set_err("bad arguments"); return -1; }
   if (b->set_device()) return -1;
   if (ensure_trace(b, N)) return -1;
   /* everything below is ordered after work already queued on b->stream */
-  HIPCHK(hipMemcpyAsync(b->d_feat, features, sizeof(float) * NF * b->B, hipMemcpyHostToDevice, b->stream));
+  HIPCHK(hipMemcpyAsync(b->d_feat, features, sizeof(float) * NF * nB, hipMemcpyHostToDevice, b->stream));
   if (preload > 0 && N > 0)
-    HIPCHK(hipMemcpyAsync(b->d_pcm, pcm, sizeof(short) * N * b->B, hipMemcpyHostToDevice, b->stream));
-  if (launch_frame_step(b, b->d_feat, b->d_lpc, true, b->d_pcm, N, preload)) return -1;
-  if (N > 0) HIPCHK(hipMemcpyAsync(pcm, b->d_pcm, sizeof(short) * N * b->B, hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(hipMemcpyAsync(b->d_pcm, pcm, sizeof(short) * N * nB, hipMemcpyHostToDevice, b->stream));
+  if (launch_frame_step(b, b->d_feat, b->d_lpc, true, b->d_pcm, N, preload, -1, nB)) return -1;
+  if (N > 0) HIPCHK(hipMemcpyAsync(pcm, b->d_pcm, sizeof(short) * N * nB, hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
   return check_status(b);
+}
+
+LPCNET_EXPORT int lpcnet_batch_synthesize_impl(LPCNetBatch *b, const float *features, short *pcm, int N, int preload)
+{
+  return synth_first(b, b ? b->B : 0, features, pcm, N, preload);
 }
 
 LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features, short *pcm, int N)
@@ -2024,10 +2053,236 @@ LPCNET_EXPORT int lpcnet_batch_get_state(LPCNetBatch *b, int stream, float *gru_
 /* ======================================================================== */
 /* drop-in single-stream API (include/lpcnet.h)                              */
 
+/* The drop-in handles share the GPU.  Every LPCNetState bound to the same
+ * model (blob bytes, resolved model constants) on the same device is a slot
+ * of one StatePool: one device copy of the model, the slots' stream states
+ * in one device array, and one work batch.  Concurrent lpcnet_synthesize
+ * calls on different handles coalesce into one launch (flat combining: the
+ * first caller to find the pool idle runs every request pending at that
+ * moment -- the slots' states are gathered into the work batch, one frame
+ * step runs, the states are scattered back), so K reference-style callers
+ * on K threads get batch-K launches instead of K batch-1 engines.  Each
+ * handle's results are those of its own stream alone (streams of a batch
+ * are independent), i.e. the reference's. */
+struct StatePool {
+  struct Req {
+    int slot;
+    const float *feat;
+    short *out;
+    int N;
+    bool done;
+    int rc;
+    std::string err;
+  };
+  uint64_t key = 0;
+  int device = 0;
+  std::vector<unsigned char> blob;
+  LPCNetBatch *work = nullptr; /* work->B >= the largest coalesced call */
+  StreamState *d_slots = nullptr;
+  int cap = 0;
+  std::vector<int> free_slots;
+  int refs = 0;
+  int *d_map = nullptr;
+  int map_cap = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  bool busy = false;
+  std::vector<Req *> pending;
+  /* statistics (tests / diagnostics) */
+  long launches = 0, requests = 0;
+};
+
+static std::mutex g_pools_mu;
+static std::map<std::pair<uint64_t, int>, StatePool *> g_pools;
+
+static uint64_t pool_key(const unsigned char *data, int len)
+{
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](const void *p, size_t n) {
+    for (size_t k = 0; k < n; k++) h = (h ^ ((const unsigned char *)p)[k]) * 1099511628211ull;
+  };
+  mix(data, (size_t)len);
+  mix(&len, sizeof(len));
+  /* load-time overrides change the model bound to the same bytes */
+  for (const char *e : {"LPCNET_LPC_GAMMA", "LPCNET_FEATURES_DELAY", "LPCNET_END2END", "LPCNET_KERNEL"}) {
+    const char *v = getenv(e);
+    mix(e, strlen(e));
+    if (v) mix(v, strlen(v));
+  }
+  return h;
+}
+
+/* the pool of (blob, device), created with its model on first use; refs+1 */
+static StatePool *pool_acquire(const unsigned char *data, int len, int device)
+{
+  const uint64_t key = pool_key(data, len);
+  std::lock_guard<std::mutex> lk(g_pools_mu);
+  auto it = g_pools.find({key, device});
+  if (it != g_pools.end() && it->second->blob.size() == (size_t)len && !memcmp(it->second->blob.data(), data, len)) {
+    it->second->refs++;
+    return it->second;
+  }
+  if (it != g_pools.end()) return nullptr; /* hash collision between different blobs: refuse rather than mix */
+  LPCNetBatch *w = lpcnet_batch_create(1, device);
+  if (!w) return nullptr;
+  if (lpcnet_batch_load_model(w, data, len)) {
+    const std::string e = g_err;
+    lpcnet_batch_destroy(w);
+    set_err(e);
+    return nullptr;
+  }
+  StatePool *p = new StatePool();
+  p->key = key;
+  p->device = device;
+  p->blob.assign(data, data + len);
+  p->work = w;
+  p->refs = 1;
+  g_pools[{key, device}] = p;
+  return p;
+}
+
+static void pool_release(StatePool *p, int slot)
+{
+  bool last = false;
+  {
+    std::unique_lock<std::mutex> lk(p->mu);
+    p->cv.wait(lk, [&] { return !p->busy; });
+    if (slot >= 0) p->free_slots.push_back(slot);
+    last = --p->refs == 0;
+  }
+  if (!last) return;
+  std::lock_guard<std::mutex> lk(g_pools_mu);
+  if (p->refs != 0) return; /* re-acquired meanwhile */
+  g_pools.erase({p->key, p->device});
+  if (hipSetDevice(p->device) == hipSuccess) {
+    (void)hipFree(p->d_slots);
+    (void)hipFree(p->d_map);
+  }
+  lpcnet_batch_destroy(p->work);
+  delete p;
+}
+
+/* a free slot holding `init` (a reset state when null); -1 on failure */
+static int pool_alloc_slot(StatePool *p, const StreamState *init)
+{
+  std::unique_lock<std::mutex> lk(p->mu);
+  p->cv.wait(lk, [&] { return !p->busy; });
+  if (hipSetDevice(p->device) != hipSuccess) { set_err("hipSetDevice failed"); return -1; }
+  if (p->free_slots.empty()) {
+    const int ncap = std::max(4, 2 * p->cap);
+    StreamState *d = nullptr;
+    if (hipMalloc(&d, sizeof(StreamState) * (size_t)ncap) != hipSuccess) { set_err("device allocation failed"); return -1; }
+    if (p->cap && hipMemcpy(d, p->d_slots, sizeof(StreamState) * (size_t)p->cap, hipMemcpyDeviceToDevice) != hipSuccess) {
+      (void)hipFree(d);
+      set_err("device copy failed");
+      return -1;
+    }
+    (void)hipFree(p->d_slots);
+    p->d_slots = d;
+    for (int k = ncap - 1; k >= p->cap; k--) p->free_slots.push_back(k);
+    p->cap = ncap;
+  }
+  const int slot = p->free_slots.back();
+  StreamState s;
+  if (init) s = *init;
+  else host_reset_state(s);
+  if (hipMemcpy(&p->d_slots[slot], &s, sizeof(s), hipMemcpyHostToDevice) != hipSuccess) { set_err("device copy failed"); return -1; }
+  p->free_slots.pop_back();
+  return slot;
+}
+
+static int pool_slot_io(StatePool *p, int slot, StreamState *get, const StreamState *put)
+{
+  std::unique_lock<std::mutex> lk(p->mu);
+  p->cv.wait(lk, [&] { return !p->busy; });
+  if (hipSetDevice(p->device) != hipSuccess) return -1;
+  if (get && hipMemcpy(get, &p->d_slots[slot], sizeof(*get), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (put && hipMemcpy(&p->d_slots[slot], put, sizeof(*put), hipMemcpyHostToDevice) != hipSuccess) return -1;
+  return 0;
+}
+
+/* one coalesced frame step for requests rq (all the same N) */
+static int pool_run(StatePool *p, const std::vector<StatePool::Req *> &rq)
+{
+  const int n = (int)rq.size(), N = rq[0]->N;
+  if (p->work->B < n) {
+    int nb = 1;
+    while (nb < n) nb *= 2;
+    LPCNetBatch *w = lpcnet_batch_create(nb, p->device);
+    if (!w) return -1;
+    if (lpcnet_batch_load_model(w, p->blob.data(), (int)p->blob.size())) {
+      lpcnet_batch_destroy(w);
+      return -1;
+    }
+    lpcnet_batch_destroy(p->work);
+    p->work = w;
+  }
+  LPCNetBatch *w = p->work;
+  if (w->set_device()) return -1;
+  if (p->map_cap < n) {
+    (void)hipFree(p->d_map);
+    p->d_map = nullptr;
+    HIPCHK(hipMalloc(&p->d_map, sizeof(int) * (size_t)w->B));
+    p->map_cap = w->B;
+  }
+  std::vector<int> map(n);
+  std::vector<float> feat((size_t)n * NF);
+  std::vector<short> pcm((size_t)n * std::max(N, 1));
+  for (int k = 0; k < n; k++) {
+    map[k] = rq[k]->slot;
+    memcpy(&feat[(size_t)k * NF], rq[k]->feat, sizeof(float) * NF);
+  }
+  HIPCHK(hipMemcpyAsync(p->d_map, map.data(), sizeof(int) * n, hipMemcpyHostToDevice, w->stream));
+  if (launch_state_copy(w->d_state, p->d_slots, nullptr, p->d_map, n, w->stream)) { set_err("state gather failed"); return -1; }
+  const int rc = synth_first(w, n, feat.data(), pcm.data(), N, 0);
+  if (rc == 0) {
+    if (launch_state_copy(p->d_slots, w->d_state, p->d_map, nullptr, n, w->stream)) { set_err("state scatter failed"); return -1; }
+    HIPCHK(hipStreamSynchronize(w->stream));
+    for (int k = 0; k < n; k++)
+      if (N > 0) memcpy(rq[k]->out, &pcm[(size_t)k * N], sizeof(short) * N);
+  }
+  p->launches++;
+  p->requests += n;
+  return rc;
+}
+
+static int pool_synthesize(StatePool *p, int slot, const float *features, short *out, int N)
+{
+  if (N < 0 || N > FRAME || !features || (N > 0 && !out)) { set_err("bad arguments"); return -1; }
+  StatePool::Req r{slot, features, out, N, false, 0, std::string()};
+  std::unique_lock<std::mutex> lk(p->mu);
+  p->pending.push_back(&r);
+  while (!r.done) {
+    if (p->busy) {
+      p->cv.wait(lk);
+      continue;
+    }
+    /* combine: every pending request with the first one's N */
+    p->busy = true;
+    std::vector<StatePool::Req *> mine, rest;
+    for (StatePool::Req *q : p->pending) (q->N == p->pending[0]->N ? mine : rest).push_back(q);
+    p->pending.swap(rest);
+    lk.unlock();
+    const int rc = pool_run(p, mine);
+    const std::string e = rc ? g_err : std::string();
+    lk.lock();
+    for (StatePool::Req *q : mine) {
+      q->rc = rc;
+      q->err = e;
+      q->done = true;
+    }
+    p->busy = false;
+    p->cv.notify_all();
+  }
+  if (r.rc) set_err(r.err);
+  return r.rc;
+}
+
 struct LPCNetState {
   uint32_t magic;
   int device;
-  LPCNetBatch *batch;
+  StatePool *pool; /* bound model (nullptr: none) */
+  int slot;
 };
 static const uint32_t kMagic = 0x4c50434eu; /* "LPCN" */
 
@@ -2040,16 +2295,26 @@ LPCNET_EXPORT int lpcnet_get_size(void) { return (int)sizeof(LPCNetState); }
 static std::mutex g_live_mu;
 static std::set<LPCNetState *> g_live;
 
+static bool is_live(LPCNetState *st)
+{
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  return st && g_live.count(st);
+}
+
 LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
 {
   if (!st) return -1;
   /* src/lpcnet.c:184-200 ends with lpcnet_reset(): re-initialising a live
-   * handle (from lpcnet_create / an earlier lpcnet_init) resets its streams
+   * handle (from lpcnet_create / an earlier lpcnet_init) resets its stream
    * and keeps its device binding and model; anything else is a fresh handle */
   {
     std::lock_guard<std::mutex> lk(g_live_mu);
     if (g_live.count(st)) {
-      if (st->batch) lpcnet_batch_reset(st->batch);
+      if (st->pool) {
+        StreamState s;
+        host_reset_state(s);
+        pool_slot_io(st->pool, st->slot, nullptr, &s);
+      }
       return 0;
     }
     g_live.insert(st);
@@ -2057,7 +2322,8 @@ LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
   st->magic = kMagic;
   const char *d = getenv("LPCNET_DEVICE");
   st->device = d ? atoi(d) : 0;
-  st->batch = nullptr;
+  st->pool = nullptr;
+  st->slot = -1;
   return 0;
 }
 
@@ -2076,26 +2342,42 @@ LPCNET_EXPORT void lpcnet_destroy(LPCNetState *st)
     std::lock_guard<std::mutex> lk(g_live_mu);
     live = g_live.erase(st) > 0;
   }
-  if (live && st->batch) lpcnet_batch_destroy(st->batch);
+  if (live && st->pool) pool_release(st->pool, st->slot);
   /* a later malloc may hand this block out again: leave nothing that looks live */
   st->magic = 0;
-  st->batch = nullptr;
+  st->pool = nullptr;
   free(st);
 }
 
 LPCNET_EXPORT void lpcnet_reset(LPCNetState *st)
 {
-  if (st && st->batch) lpcnet_batch_reset(st->batch);
+  if (!is_live(st) || !st->pool) return;
+  StreamState s;
+  host_reset_state(s);
+  pool_slot_io(st->pool, st->slot, nullptr, &s);
 }
 
 LPCNET_EXPORT int lpcnet_load_model(LPCNetState *st, const unsigned char *data, int len)
 {
-  if (!st) return -1;
-  if (!st->batch) {
-    st->batch = lpcnet_batch_create(1, st->device);
-    if (!st->batch) return -1;
+  if (!is_live(st)) return -1;
+  StatePool *p = pool_acquire(data, len, st->device);
+  if (!p) return -1;
+  if (p == st->pool) {
+    pool_release(p, -1); /* same model: keep the binding */
+    return 0;
   }
-  return lpcnet_batch_load_model(st->batch, data, len) == 0 ? 0 : -1;
+  /* the model changes, the stream state stays (lpcnet.c:202-210 only binds arrays) */
+  StreamState s;
+  bool have = st->pool && pool_slot_io(st->pool, st->slot, &s, nullptr) == 0;
+  const int slot = pool_alloc_slot(p, have ? &s : nullptr);
+  if (slot < 0) {
+    pool_release(p, -1);
+    return -1;
+  }
+  if (st->pool) pool_release(st->pool, st->slot);
+  st->pool = p;
+  st->slot = slot;
+  return 0;
 }
 
 LPCNET_EXPORT void lpcnet_synthesize(LPCNetState *st, const float *features, short *output, int N)
@@ -2106,16 +2388,27 @@ LPCNET_EXPORT void lpcnet_synthesize(LPCNetState *st, const float *features, sho
    * on stderr */
   static std::atomic<bool> warned{false};
   int rc;
-  if (!st || !st->batch) {
+  if (!is_live(st) || !st->pool) {
     set_err("lpcnet_synthesize: no model bound (call lpcnet_load_model first; liblpcnet_mi355x has no compiled-in model)");
     rc = -1;
   } else {
-    rc = lpcnet_batch_synthesize(st->batch, features, output, N);
+    rc = pool_synthesize(st->pool, st->slot, features, output, N);
   }
   if (rc != 0) {
     if (output && N > 0) memset(output, 0, sizeof(short) * N);
     if (!warned.exchange(true)) fprintf(stderr, "liblpcnet_mi355x: %s\n", g_err.c_str());
   }
+}
+
+LPCNET_EXPORT int lpcnet_mi355x_pool_stats(const LPCNetState *st, long *launches, long *requests, int *streams)
+{
+  LPCNetState *s = const_cast<LPCNetState *>(st);
+  if (!is_live(s) || !s->pool) return -1;
+  std::lock_guard<std::mutex> lk(s->pool->mu);
+  if (launches) *launches = s->pool->launches;
+  if (requests) *requests = s->pool->requests;
+  if (streams) *streams = s->pool->refs;
+  return 0;
 }
 
 /* Host-only check of a weight blob against every rule lpcnet_load_model

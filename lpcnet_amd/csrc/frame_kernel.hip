@@ -357,6 +357,26 @@ int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, void 
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+/* Stream-state moves of the shared drop-in pool (engine.cpp StatePool):
+ * dst[dmap ? dmap[k] : k] = src[smap ? smap[k] : k] for k < n, one
+ * workgroup per state, 16 bytes per thread. */
+__global__ __launch_bounds__(256) void state_copy_kernel(StreamState *dst, const StreamState *src, const int *dmap,
+                                                       const int *smap, int n)
+{
+  const int k = blockIdx.x;
+  if (k >= n) return;
+  uint4 *d = (uint4 *)&dst[dmap ? dmap[k] : k];
+  const uint4 *s = (const uint4 *)&src[smap ? smap[k] : k];
+  for (int e = threadIdx.x; e < (int)(sizeof(StreamState) / 16); e += blockDim.x) d[e] = s[e];
+}
+
+int launch_state_copy(StreamState *dst, const StreamState *src, const int *dmap, const int *smap, int n, void *stream)
+{
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(state_copy_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, dst, src, dmap, smap, n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 constexpr int FK_B1_GRID = 2;
 
 /* Up to one stream per CU the single-stream kernel runs every stream in its

@@ -276,6 +276,8 @@ constexpr int FK_ONE_STREAM_MAX = 256; /* frame kernel: one stream per workgroup
 int frame_groups(int nstreams);        /* frame kernel workgroups (stamp rows) for a batch */
 /* copy the frame step's outputs of every stream into cond[B] */
 int launch_cond_copy(const StreamState *st, FrameCond *cond, int nstreams, void *stream);
+/* dst[dmap ? dmap[k] : k] = src[smap ? smap[k] : k], k < n (device index maps) */
+int launch_state_copy(StreamState *dst, const StreamState *src, const int *dmap, const int *smap, int n, void *stream);
 int launch_sample(const SampleArgs &a, int S, int variant, int sat, int reg, int lds_bytes, void *stream);
 
 /* Frame network of up to LPC_CHUNK frames in one launch (chunk_kernel.hip):
@@ -288,6 +290,11 @@ constexpr int CHUNK_MIN_FRAMES = 4; /* shorter runs use the per-frame kernel */
  * workgroup barriers per sample. */
 int mf_lds_bytes(int S, int split);
 int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream);
+/* Large batches: two groups of S streams per workgroup, half a sample
+ * apart (mf2_kernel.hip); no preload / trace / stamps / split models. */
+constexpr int MF2_MIN_STREAMS = 2048; /* automatic choice of mf2_kernel from this batch size */
+int mf2_lds_bytes(int S);
+int launch_mf2(const SampleArgs &a, int S, void *stream);
 /* fp32 latency kernel: one stream per workgroup, LDS flags instead of
  * workgroup barriers (fp32 models within the FP_* limits, dense GRU_B). */
 int fp_lds_bytes();

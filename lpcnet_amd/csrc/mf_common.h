@@ -9,6 +9,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "device_math.h"
 #include "lpcnet_engine.h"
 
 namespace lpcnet_mi355x {
@@ -184,6 +185,55 @@ __device__ __forceinline__ void mf_run_split(const unsigned char *lds, const uin
       for (int k = 0; k < 4; k++) x[k] = n[k];
     }
   }
+}
+
+/* compute_sparse_gru elementwise (nnet.c:431-447) of one GRU_A unit for S
+ * streams, from the gathered rows e (nnet.c:484-491 sums in the reference's
+ * order), the recurrent sums az/ar, the state terms tz/tr and the recurrent
+ * h-gate value hpre; FAST: the range-guarded select-free forms.  Scalar
+ * float ops only: packed v_pk_add/mul_f32 (explicit or SLP-formed -- this
+ * file is built with -fno-slp-vectorize) cost more SIMD issue cycles than
+ * the scalar pairs, and waves 0/4 and 1/5 share one SIMD's VALU here
+ * (measured: 7,450 -> 7,240 cycles per sample at 1024 streams). */
+template <int S, bool FAST, bool HW, typename Stamp>
+__device__ __forceinline__ void ga_elementwise(float (&st)[S], const float (&e)[S][9], const float *cnd, int tid,
+                                               const int (&az)[S], const int (&ar)[S], const float (&tz)[S],
+                                               const float (&tr)[S], const float (&hpre)[S], const uint32_t *rcp,
+                                               unsigned char *xa_i, bool stamping, Stamp &stamp)
+{
+  (void)stamping;
+  (void)stamp;
+  float zrv[2 * S], hv[S], inh[S];
+  for (int s = 0; s < S; s++) {
+    const float inz = ((cnd[tid * S + s] + e[s][0]) + e[s][3]) + e[s][6];
+    const float inr = ((cnd[(NA + tid) * S + s] + e[s][1]) + e[s][4]) + e[s][7];
+    inh[s] = ((cnd[(2 * NA + tid) * S + s] + e[s][2]) + e[s][5]) + e[s][8];
+    if (FAST) {
+      zrv[s] = (float)(az[s] + cvt_rne_fin((tz[s] + inz) * kScale)) * kScale1;
+      zrv[S + s] = (float)(ar[s] + cvt_rne_fin((tr[s] + inr) * kScale)) * kScale1;
+    } else {
+      zrv[s] = (float)(az[s] + cvt_rne((tz[s] + inz) * kScale)) * kScale1;
+      zrv[S + s] = (float)(ar[s] + cvt_rne((tr[s] + inr) * kScale)) * kScale1;
+    }
+    hv[s] = hpre[s];
+  }
+#ifdef MF_FINE
+  if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(11); }
+#endif
+  sigmoid_x86_fin_n<2 * S, HW>(zrv, rcp);
+#ifdef MF_FINE
+  if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(12); }
+#endif
+  for (int s = 0; s < S; s++) hv[s] = hv[s] * zrv[S + s] + inh[s];
+  if (FAST)
+    tanh_x86_fin_n<S, HW>(hv, rcp);
+  else
+    tanh_x86_n<S, HW>(hv, rcp);
+  for (int s = 0; s < S; s++) st[s] = zrv[s] * st[s] + (1.f - zrv[s]) * hv[s];
+#ifdef MF_FINE
+  if (stamping) { float g = 0.f; for (int k = 0; k < S; k++) g += st[k]; asm volatile("" ::"v"(g)); stamp(13); }
+#endif
+  for (int s = 0; s < S; s++) xa_i[s * MF_XSTR] = (unsigned char)quant_s8_state(st[s]);
 }
 
 /* v_mfma_i32_16x16x64_i8: A (src0) lane l = row l%16, B (src1) lane l =

@@ -69,6 +69,19 @@ int ref_rcp_table(uint32_t *tab)
   return bad;
 }
 
+/* This CPU's rcpps of every float in [1, 2): tab[m] = rcpps(1.m), 2^23
+ * entries (the full mantissa table, for hosts whose rcpps is not a function
+ * of the top 11 mantissa bits). */
+void ref_rcp_full(uint32_t *tab)
+{
+  for (uint32_t m = 0; m < (1u << 23); m += 8) {
+    uint32_t u[8];
+    for (int k = 0; k < 8; k++) u[k] = 0x3f800000u | (m + k);
+    __m256 v = _mm256_rcp_ps(_mm256_loadu_ps((const float *)u));
+    _mm256_storeu_ps((float *)&tab[m], v);
+  }
+}
+
 /* Single rcpps on this CPU (for spot checks of the emulation). */
 float ref_rcp(float x)
 {

@@ -127,9 +127,11 @@ def test_two_rank_engine_shard_invariance(require_gpu, per_rank, frames):
     assert np.array_equal(sharded, single.astype(np.int32))
     assert np.abs(single[2:].astype(np.float64)).mean() > 100
     if per_rank >= 1024:
-        # the single-process run took the configs[4] path too: one
-        # multi-frame launch of the timed frames on 4 streams per workgroup
-        assert info.quad_path == 4 and info.streams_per_workgroup == 4
+        # the single-process 2048-stream run takes mf2_kernel (two staggered
+        # 4-stream groups per workgroup), each rank's 1024 streams mf_kernel<4>:
+        # two different kernels agree on every stream; one multi-frame launch
+        # of the timed frames
+        assert info.quad_path == 6 and info.streams_per_workgroup == 8
         assert kn == 1 and kf == frames - 2, (kn, kf)
         # and both agree with the CPU oracle on streams from each shard
         import oracle_lib as O

@@ -144,7 +144,8 @@ def test_matrix_core_kernel_edge_cases_at_bench_size(require_gpu, blobs):
 
 @pytest.mark.parametrize("env", ["LPCNET_MF_EXACT", "LPCNET_MF_ZR_BOUND=0.05", "LPCNET_MF_ZR_BOUND=1.5"])
 @pytest.mark.parametrize("B,check", [(1030, (0, 1, 2, 3, 517, 1029)), (70, (0, 37, 69))])
-def test_matrix_core_range_paths_match_oracle(require_gpu, blobs, monkeypatch, env, B, check):
+@pytest.mark.parametrize("mf2", ["0", "1"])
+def test_matrix_core_range_paths_match_oracle(require_gpu, blobs, monkeypatch, env, B, check, mf2):
     """mf_kernel's GRU_A elementwise has a select-free form for workgroups
     whose conditioning and states lie within the host's range bounds, and the
     exact form with x86's out-of-range/NaN selects otherwise.  Force the exact
@@ -153,6 +154,7 @@ def test_matrix_core_range_paths_match_oracle(require_gpu, blobs, monkeypatch, e
     PCM and final GRU_A states against the oracle."""
     name, _, val = env.partition("=")
     monkeypatch.setenv(name, val or "1")
+    monkeypatch.setenv("LPCNET_MF2", mf2)  # mf_kernel / mf2_kernel
     F = 6
     blob = blobs["streams_int8"]
     b = L.LPCNetBatch(B, 0, blob)
@@ -397,8 +399,8 @@ def test_restore_refuses_out_of_range_last_exc(require_gpu, blobs):
 
 def test_8192_streams_one_gpu_match_oracle(require_gpu, blobs):
     """BASELINE configs[4]'s total stream count on one GPU: LPCNetBatch(8192)
-    through the device-resident multi-frame path (mf_kernel<4>: 2048
-    workgroups in 8 rounds over the CUs, chunked frame network), against the
+    through the device-resident multi-frame path (mf2_kernel: 1024
+    workgroups of two staggered 4-stream groups, chunked frame network), against the
     CPU oracle on two streams of every 1024-stream shard (PCM and final GRU
     states bit for bit), and shard 3 run alone as a 1024-stream batch gives
     the same PCM for its streams."""
@@ -406,7 +408,7 @@ def test_8192_streams_one_gpu_match_oracle(require_gpu, blobs):
     blob = blobs["streams_int8"]
     allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
     b = L.LPCNetBatch(B, 0, blob)
-    assert b.info().quad_path == 4 and b.info().streams_per_workgroup == 4
+    assert b.info().quad_path == 6 and b.info().streams_per_workgroup == 8  # mf2_kernel from 2048 streams
     b.reset_timers(1)
     got = np.concatenate([_frames(b, allf, 0, 2), _frames(b, allf, 2, F)], 0)
     assert b.kernel_frames(0) == F and b.kernel_ms(0)[1] == 3  # 2 single-frame launches + one of 6
@@ -424,6 +426,76 @@ def test_8192_streams_one_gpu_match_oracle(require_gpu, blobs):
     c = L.LPCNetBatch(1024, 0, blob)
     alone = np.concatenate([_frames(c, allf[:, 3072:4096], 0, 2), _frames(c, allf[:, 3072:4096], 2, F)], 0)
     assert np.array_equal(alone, got[:, 3072:4096])
+
+
+@pytest.mark.parametrize("B", [9, 70, 1030, 2048])
+def test_mf2_kernel_equals_mf_kernel(require_gpu, blobs, monkeypatch, B):
+    """mf2_kernel (two 4-stream groups per workgroup, half a sample apart;
+    LPCNET_MF2=1 forces it at any batch) against mf_kernel (LPCNET_MF2=0):
+    the PCM and the complete stream state byte for byte, every stream,
+    through the per-frame host path (with a partial frame, N = 81, and a
+    per-stream reset) and the device-resident multi-frame path (runs that
+    start inside the FEATURES_DELAY frames and span chunk boundaries);
+    ragged last workgroups at 9 and 70 streams.  Preload and trace calls fall
+    back to mf_kernel on the same batch.  Stream 0 against the oracle."""
+    F = 40
+    blob = blobs["streams_int8"]
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    outs, states = [], []
+    for mf2 in ("0", "1"):
+        monkeypatch.setenv("LPCNET_MF2", mf2)
+        b = L.LPCNetBatch(B, 0, blob)
+        assert b.info().quad_path == (6 if mf2 == "1" else 4)
+        parts = [np.stack([b.synthesize(allf[f]) for f in range(3)])]
+        parts.append(np.pad(b.synthesize(allf[3], 81), ((0, 0), (0, 79)))[None])
+        b.reset(B - 1)
+        parts.append(_frames(b, allf, 4, 7))
+        parts.append(_frames(b, allf, 7, F))
+        outs.append(np.concatenate(parts, 0))
+        states.append([bytes(b.save_state(s)) for s in range(B)])
+        b.close()
+    assert np.abs(outs[0][8:].astype(np.float64)).mean() > 100
+    bad = np.nonzero((outs[1] != outs[0]).any(axis=2))
+    assert not len(bad[0]), list(zip(bad[0][:8], bad[1][:8]))
+    badst = [s for s in range(B) if states[1][s] != states[0][s]]
+    assert not badst, badst[:8]
+    o = O.Oracle(blob, 0)
+    ref = [o.synthesize(allf[f, 0]) for f in range(3)] + [np.pad(o.synthesize(allf[3, 0], 81), (0, 79))]
+    ref += [o.synthesize(allf[f, 0]) for f in range(4, F)]
+    assert np.array_equal(outs[1][:, 0], np.stack(ref))
+
+
+def test_mf2_batch_falls_back_for_preload_and_trace(require_gpu, blobs, monkeypatch):
+    """A 2048-stream batch (mf2_kernel) takes mf_kernel for a teacher-forced
+    call and for a traced call: PCM, logits and excitation against the oracle."""
+    monkeypatch.delenv("LPCNET_MF2", raising=False)
+    B, F = 2048, 5
+    blob = blobs["streams_int8"]
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    b = L.LPCNetBatch(B, 0, blob)
+    assert b.info().quad_path == 6
+    check = (0, 1500, 2047)
+    refs = {s: O.Oracle(blob, 0) for s in check}
+    t = np.arange(160)
+    for f in range(F):
+        if f == 3:
+            teacher = np.stack([(2000 * np.sin(0.02 * (s % 5 + 1) * t)).astype(np.int16) for s in range(B)])
+            out = b.synthesize_impl(allf[f], teacher, 60)
+            for s in check:
+                exp = refs[s].synthesize(allf[f, s], 160, preload=teacher[s][:60])
+                assert np.array_equal(out[s], exp), (f, s)
+        elif f == 4:
+            b.set_trace(True)
+            out = b.synthesize(allf[f])
+            lg, ex = b.get_trace(160)
+            for s in check:
+                exp, elg, eex, _ = refs[s].synthesize(allf[f, s], 160, trace=True)
+                assert np.array_equal(out[s], exp) and np.array_equal(ex[s], eex), (f, s)
+                assert np.array_equal(bits(lg[s]), bits(elg)), (f, s)
+        else:
+            out = b.synthesize(allf[f])
+            for s in check:
+                assert np.array_equal(out[s], refs[s].synthesize(allf[f, s])), (f, s)
 
 
 CHECK256 = (0, 1, 128, 254, 255)
