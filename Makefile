@@ -15,7 +15,7 @@ CSRC := lpcnet_amd/csrc
 HDRS := include/lpcnet.h include/lpcnet_mi355x.h $(CSRC)/lpcnet_engine.h $(CSRC)/device_math.h $(CSRC)/sampler.h $(CSRC)/lds_flags.h $(CSRC)/mf_common.h $(CSRC)/l2_warm.h $(CSRC)/pow10_dd.h $(CSRC)/rcp_table_x86.inc
 EXTRA ?=
 COMMON := $(EXTRA) -O3 -fPIC -ffp-contract=off -fno-fast-math -std=c++17 -Iinclude -I$(CSRC) -fvisibility=hidden -Wall -Wno-unused-function
-OBJS := $(BUILD)/kernels.o $(BUILD)/mf_kernel.o $(BUILD)/mf2_kernel.o $(BUILD)/fp_kernel.o $(BUILD)/selftest.o $(BUILD)/frame_kernel.o $(BUILD)/engine.o $(BUILD)/lpc_kernel.o $(BUILD)/chunk_kernel.o $(BUILD)/model_gen.o
+OBJS := $(BUILD)/kernels.o $(BUILD)/mf_kernel.o $(BUILD)/mf2_kernel.o $(BUILD)/fp_kernel.o $(BUILD)/selftest.o $(BUILD)/frame_kernel.o $(BUILD)/engine.o $(BUILD)/lpc_kernel.o $(BUILD)/chunk_kernel.o $(BUILD)/model_gen.o $(BUILD)/host_rcpps.o
 
 SYNTH := tools/lpcnet_synth
 
@@ -64,6 +64,10 @@ $(BUILD)/chunk_kernel.o: $(CSRC)/chunk_kernel.hip $(HDRS) | $(BUILD)
 
 $(BUILD)/model_gen.o: $(CSRC)/model_gen.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -c $< -o $@
+
+# host-only: the CPU's own rcpps (x86 SSE), system compiler
+$(BUILD)/host_rcpps.o: $(CSRC)/host_rcpps.cpp include/lpcnet_mi355x.h | $(BUILD)
+	$(CXX) -O2 -fPIC -msse2 -ffp-contract=off -std=c++17 -Iinclude -fvisibility=hidden -Wall -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread

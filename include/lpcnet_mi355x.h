@@ -48,6 +48,10 @@ typedef struct {
   float lpc_gamma;
   int features_delay;
   int end2end;
+  /* 1: block rows longer than the fast kernels' register tables (trained
+   * Sparsify masks): mf_kernel runs its split form, fp_kernel its streamed
+   * (long) form */
+  int long_rows;
 } LPCNetModelInfo;
 
 /* Create a batch of nb_streams streams on HIP device `device`.
@@ -185,8 +189,24 @@ LPCNET_EXPORT void lpcnet_mi355x_synthetic_features(unsigned stream, int nframes
  * GPU `device`, through the engine's lpc_kernel (diagnostics / parity: the
  * synthesis entry points run the same kernel per frame).  Returns 0 or -1. */
 LPCNET_EXPORT int lpcnet_mi355x_device_lpc(int device, const float *cepstra, float *lpc, int n);
-/* The rcpps table the device activations use (2048 entries). */
+/* The rcpps table the device activations use by default (2048 entries:
+ * the Intel build host's rcpps of the top 11 mantissa bits,
+ * tests/golden/rcp_x86.bin). */
 LPCNET_EXPORT const uint32_t *lpcnet_mi355x_rcp_table(void);
+/* This host CPU's rcpps (_mm_rcp_ps, vec_avx.h:408,437) of every float in
+ * [1, 2) as 4096 entries of the top 12 mantissa bits (entries == 4096).
+ * Returns the number of mantissas / exponents the 12-bit, exponent-invariant
+ * form does not reproduce (0: the table is exact), or -1. */
+LPCNET_EXPORT int lpcnet_mi355x_host_rcp_table(uint32_t *tab, int entries);
+/* Same-box parity: the device activations use rcpps table `tab` (4096
+ * entries as lpcnet_mi355x_host_rcp_table returns; NULL restores the
+ * default Intel table).  A table other than the default disables the
+ * hardware-reciprocal shortcut (proven equal only to the Intel table), so
+ * the batch runs the lockstep sample kernel and the per-frame frame kernel
+ * (every activation through the table).  The environment variable
+ * LPCNET_RCP=host selects this host's table at load time (drop-in API).
+ * Returns 0, or -1 (no model loaded / device error). */
+LPCNET_EXPORT int lpcnet_batch_set_rcp_table(LPCNetBatch *b, const uint32_t *tab);
 /* Device numerics self-test (diagnostics, not the synthesis path): runs one
  * routine of the kernels' arithmetic (lpcnet_amd/csrc/device_math.h) on GPU
  * `device` elementwise over n 32-bit inputs: op 0 tanh8_approx, 1

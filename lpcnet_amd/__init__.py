@@ -58,6 +58,9 @@ def _load():
         "lpcnet_batch_model_info": (i, [vp, vp]),
         "lpcnet_batch_set_kernel": (i, [vp, i]),
         "lpcnet_batch_set_model_constants": (i, [vp, f, i, i]),
+        "lpcnet_batch_set_rcp_table": (i, [vp, vp]),
+        "lpcnet_mi355x_host_rcp_table": (i, [vp, i]),
+        "lpcnet_mi355x_pool_stats": (i, [vp, vp, vp, vp]),
         "lpcnet_batch_reset": (None, [vp]),
         "lpcnet_batch_reset_stream": (i, [vp, i]),
         "lpcnet_batch_nb_streams": (i, [vp]),
@@ -108,19 +111,21 @@ class ModelInfo(C.Structure):
                 ("bytes_shared_per_sample", C.c_double), ("bytes_per_stream_sample", C.c_double),
                 ("ops_per_sample", C.c_double), ("streams_per_workgroup", C.c_int), ("quad_path", C.c_int),
                 ("lds_bytes", C.c_int), ("mfma_ops_per_group_sample", C.c_double),
-                ("lpc_gamma", C.c_float), ("features_delay", C.c_int), ("end2end", C.c_int)]
+                ("lpc_gamma", C.c_float), ("features_delay", C.c_int), ("end2end", C.c_int),
+                ("long_rows", C.c_int)]
 
     @property
     def kernel_name(self) -> str:
         """Demangled template instance of the sample kernel this model runs
         (as rocprofv3 names it)."""
         sat = "true" if self.may_saturate else "false"
+        lr = "true" if self.long_rows else "false"
         if self.quad_path == 4:
-            return f"mf_kernel<{self.streams_per_workgroup}, false, false>"
+            return f"mf_kernel<{self.streams_per_workgroup}, false, {lr}>"
         if self.quad_path == 6:
             return "mf2_kernel<4>"
         if self.quad_path == 5:
-            return "fp_kernel<false>"
+            return f"fp_kernel<false, {lr}>"
         quad = "true" if self.quad_path == 1 else "false"
         return f"sample_kernel<{self.streams_per_workgroup}, {self.variant}, {sat}, {quad}>"
 
@@ -199,6 +204,14 @@ def device_lpc(cepstra: np.ndarray, device: int = 0) -> np.ndarray:
     return out
 
 
+def host_rcp_table() -> tuple[np.ndarray, int]:
+    """This host CPU's rcpps as the 4096-entry (top 12 mantissa bits) table
+    and the number of mantissas/exponents that form does not reproduce."""
+    t = np.zeros(4096, np.uint32)
+    bad = lib.lpcnet_mi355x_host_rcp_table(t.ctypes.data, 4096)
+    return t, bad
+
+
 def rcp_table() -> np.ndarray:
     p = lib.lpcnet_mi355x_rcp_table()
     return np.ctypeslib.as_array(p, shape=(2048,)).copy()
@@ -264,6 +277,13 @@ class LPCNetBatch:
         """LPC_GAMMA / FEATURES_DELAY / END2END of the loaded model (the reference's
         nnet_data.h constants); see lpcnet_batch_set_model_constants."""
         if lib.lpcnet_batch_set_model_constants(self._b, lpc_gamma, features_delay, 1 if end2end else 0) != 0:
+            raise LPCNetError(last_error())
+
+    def set_rcp_table(self, table: np.ndarray | None) -> None:
+        """Same-box parity: the rcpps table of the device activations (4096
+        entries, see host_rcp_table; None = the default Intel table)."""
+        t = None if table is None else np.ascontiguousarray(table, np.uint32)
+        if lib.lpcnet_batch_set_rcp_table(self._b, None if t is None else t.ctypes.data) != 0:
             raise LPCNetError(last_error())
 
     def set_spin_limit(self, polls: int) -> None:

@@ -68,12 +68,12 @@ __device__ __forceinline__ float rcp_x86(float x, const uint32_t *tab)
   /* _mm256_rcp_ps of a Pade denominator (its only use, tanh8_approx and
    * sigmoid8_approx): den = fma(fma(D2,X2,D1),X2,D0) with positive D's and
    * X2 = X*X lies in [952.72, +inf] or is NaN.  rcpps there is the
-   * 2048-entry table of the top 11 mantissa bits, rebiased; results below
+   * table of the top RCP_TABLE_BITS mantissa bits, rebiased; results below
    * 2^-126 (and rcp(+inf)) are +0.  ldexp + flush reproduces it for every
    * such den (oracle/checks/exact_identities.c (4)); a NaN den only occurs
    * with a NaN numerator, whose product stays NaN.  The table load is pinned
    * (empty asm) so the select stays branch-free. */
-  uint32_t t = tab[__builtin_amdgcn_ubfe(__float_as_uint(x), 12, 11)];
+  uint32_t t = tab[__builtin_amdgcn_ubfe(__float_as_uint(x), 23 - RCP_TABLE_BITS, RCP_TABLE_BITS)];
   asm volatile("" : "+v"(t));
   return rcp_x86_fix(x, t);
 }
@@ -120,7 +120,7 @@ __device__ __forceinline__ void rcp_x86_n(float (&x)[N], const uint32_t *tab)
   }
   uint32_t t[N];
 #pragma unroll
-  for (int k = 0; k < N; k++) t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(x[k]), 12, 11)];
+  for (int k = 0; k < N; k++) t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(x[k]), 23 - RCP_TABLE_BITS, RCP_TABLE_BITS)];
 #pragma unroll
   for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
 #pragma unroll
@@ -175,7 +175,7 @@ __device__ __forceinline__ void sigmoid_x86_fin_n(float (&X)[N], const uint32_t 
     num[k] = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
     den[k] = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
     num[k] = num[k] * X[k];
-    t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(den[k]), 12, 11)];
+    t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(den[k]), 23 - RCP_TABLE_BITS, RCP_TABLE_BITS)];
   }
 #pragma unroll
   for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
@@ -224,7 +224,7 @@ __device__ __forceinline__ void tanh_x86_fin_n(float (&X)[N], const uint32_t *ta
   }
   uint32_t t[N];
 #pragma unroll
-  for (int k = 0; k < N; k++) t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(den[k]), 12, 11)];
+  for (int k = 0; k < N; k++) t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(den[k]), 23 - RCP_TABLE_BITS, RCP_TABLE_BITS)];
 #pragma unroll
   for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
 #pragma unroll

@@ -306,6 +306,10 @@ struct LPCNetBatch {
   bool reg = false;
   int kernel_mode = 0;   /* 0 auto, 1 lockstep sample_kernel, 4 matrix-core mf_kernel, 5 fp32 fp_kernel */
   ModelConst mc{1.0f, DEFAULT_FEATURES_DELAY, 0}; /* FEATURES_DELAY / LPC_GAMMA / END2END of the model */
+  /* rcpps table of the device activations (RCP_ENTRIES, device form t + kRcpBias);
+   * rcp_custom: not the default Intel table (lpcnet_batch_set_rcp_table) */
+  bool rcp_custom = false;
+  std::vector<uint32_t> rcp_dev;
   bool mf_ok = false;    /* model fits the matrix-core register tables */
   bool mf = false;       /* mf_kernel (mode 4) */
   bool mf2 = false;      /* large batches: mf2_kernel (two staggered 4-stream groups per workgroup) for
@@ -425,6 +429,9 @@ void choose_kernel(LPCNetBatch *b)
   b->info.mfma_ops_per_group_sample = 0;
   int mode = b->kernel_mode;
   if (mode == 0) mode = b->fp_ok ? 5 : (b->mf_ok ? 4 : 1);
+  /* a custom rcpps table: every activation through the table (the fast
+   * kernels' hardware-reciprocal shortcut is proven for the Intel table only) */
+  if (b->rcp_custom) mode = 1;
   if (mode == 5 && b->fp_ok && fp_lds_bytes() <= 160 * 1024) {
     b->fp = true;
     b->info.streams_per_workgroup = 1;
@@ -830,9 +837,25 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
 
   /* ---- LDS image ---- */
   std::vector<unsigned char> img(IMG_VAR, 0);
-  uint32_t rcp_dev[2048]; /* device form: t + (127 << 23), see rcp_x86_fix */
-  for (int i = 0; i < 2048; i++) rcp_dev[i] = kRcpTable[i] + kRcpBias;
-  memcpy(&img[IMG_RCP], rcp_dev, sizeof(rcp_dev));
+  /* device form: t + (127 << 23), see rcp_x86_fix; the default is the Intel
+   * table (11 bits, each entry twice); a custom table stays across reloads,
+   * LPCNET_RCP=host selects this host's at load time */
+  std::vector<uint32_t> rcp_dev(RCP_ENTRIES);
+  if (b->rcp_custom && (int)b->rcp_dev.size() == RCP_ENTRIES) {
+    rcp_dev = b->rcp_dev;
+  } else {
+    for (int i = 0; i < RCP_ENTRIES; i++) rcp_dev[i] = kRcpTable[i >> (RCP_TABLE_BITS - 11)] + kRcpBias;
+    if (const char *e = getenv("LPCNET_RCP"))
+      if (!strcmp(e, "host")) {
+        std::vector<uint32_t> h(RCP_ENTRIES);
+        if (lpcnet_mi355x_host_rcp_table(h.data(), RCP_ENTRIES) != 0) {
+          set_err("LPCNET_RCP=host: this host's rcpps is not a 12-bit exponent-invariant table");
+          return -1;
+        }
+        for (int i = 0; i < RCP_ENTRIES; i++) rcp_dev[i] = h[i] + kRcpBias;
+      }
+  }
+  memcpy(&img[IMG_RCP], rcp_dev.data(), RCP_ENTRIES * 4);
   for (int i = 0; i < 256; i++) {
     float u = host_ulaw2lin((float)i);
     memcpy(&img[IMG_ULAW + 4 * i], &u, 4);
@@ -1077,14 +1100,68 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     for (int k = 0; k < (int)gb_blocks[rb].size() && fp_ok; k++)
       if (gb_blocks[rb][k] != 4 * k) fp_ok = false;
   }
+  /* block rows longer than the register tables (trained masks, see
+   * mf_plan): the long form streams every slot of the z/r and h chains */
+  bool fp_long = false;
   for (int w = 0; w < SAMPLE_WAVES && fp_ok; w++)
     for (int j = 0; j < 8; j++) {
       if ((int)ga_blocks[w * 8 + j].size() > FP_ZF || (int)ga_blocks[NA / 8 + w * 8 + j].size() > FP_ZF ||
           (int)ga_blocks[2 * (NA / 8) + w * 8 + j].size() > FP_HF)
-        fp_ok = false;
+        fp_long = true;
     }
-  if (fp_ok) {
-    const float *wa = (const float *)gaw->data, *wb = (const float *)gbw;
+  if (getenv("LPCNET_FP_FORCE_LONG")) fp_long = true; /* tests: the long form on any model */
+  std::vector<float4> fplzr, fplh;
+  std::vector<uint32_t> fploff;
+  if (fp_ok && fp_long) {
+    const float *wa = (const float *)gaw->data;
+    const float nz = -0.f;
+    int KZ = 1, KH = 1;
+    for (int rb = 0; rb < NA / 8; rb++) {
+      KZ = std::max(KZ, (int)std::max(ga_blocks[rb].size(), ga_blocks[NA / 8 + rb].size()));
+      KH = std::max(KH, (int)ga_blocks[2 * (NA / 8) + rb].size());
+    }
+    /* [wave][slot][64 lanes]: z/r weights as the packed pairs (2 float4), h
+     * weights (float4); offsets: z quad | r quad << 8, then h quad */
+    fplzr.assign((size_t)SAMPLE_WAVES * KZ * 64 * 2, make_float4(nz, nz, nz, nz));
+    fplh.assign((size_t)SAMPLE_WAVES * KH * 64, make_float4(nz, nz, nz, nz));
+    fploff.assign((size_t)SAMPLE_WAVES * (KZ + KH) * 64, (uint32_t)(NA / 4) * 0x0101u); /* the +0 quad */
+    for (int w = 0; w < SAMPLE_WAVES; w++) {
+      int kz = 0, kh = 0;
+      for (int j = 0; j < 8; j++) {
+        kz = std::max(kz, (int)std::max(ga_blocks[w * 8 + j].size(), ga_blocks[NA / 8 + w * 8 + j].size()));
+        kh = std::max(kh, (int)ga_blocks[2 * (NA / 8) + w * 8 + j].size());
+      }
+      sa.fp_nzr[w] = kz;
+      sa.fp_nh[w] = kh;
+      for (int l = 0; l < 64; l++) {
+        const int j = l >> 3, r = l & 7;
+        for (int g = 0; g < 3; g++) {
+          const int rb = g * (NA / 8) + w * 8 + j;
+          for (int t = 0; t < (int)ga_blocks[rb].size(); t++) {
+            const float *src = wa + 32 * (size_t)(ga_first[rb] + t);
+            const float4 v = make_float4(src[0 * 8 + r], src[1 * 8 + r], src[2 * 8 + r], src[3 * 8 + r]);
+            const uint32_t q = (uint32_t)(ga_blocks[rb][t] / 4);
+            if (g < 2) {
+              float4 &lo = fplzr[(((size_t)w * KZ + t) * 64 + l) * 2], &hi = fplzr[(((size_t)w * KZ + t) * 64 + l) * 2 + 1];
+              (g == 0 ? lo.x : lo.y) = v.x;
+              (g == 0 ? lo.z : lo.w) = v.y;
+              (g == 0 ? hi.x : hi.y) = v.z;
+              (g == 0 ? hi.z : hi.w) = v.w;
+              uint32_t &o = fploff[((size_t)w * KZ + t) * 64 + l];
+              o = (o & ~(0xFFu << (8 * g))) | (q << (8 * g));
+            } else {
+              fplh[((size_t)w * KH + t) * 64 + l] = v;
+              fploff[(size_t)SAMPLE_WAVES * KZ * 64 + ((size_t)w * KH + t) * 64 + l] = q;
+            }
+          }
+        }
+      }
+    }
+    sa.fpl_kz = KZ;
+    sa.fpl_kh = KH;
+  }
+  if (fp_ok && !fp_long) {
+    const float *wa = (const float *)gaw->data;
     const float nz = -0.f;
     fpzr.assign((size_t)SAMPLE_WAVES * 2 * FP_ZF * 64, make_float4(nz, nz, nz, nz));
     fph.assign((size_t)SAMPLE_WAVES * FP_HF * 64, make_float4(nz, nz, nz, nz));
@@ -1121,6 +1198,14 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
         }
       }
     }
+    for (int w = 0; w < SAMPLE_WAVES; w++) {
+      sa.fp_nzr[w] = fp_nzr[w];
+      sa.fp_nh[w] = fp_nh[w];
+    }
+  }
+  if (fp_ok) {
+    /* dense GRU_B input weights, column quad major (both forms) */
+    const float *wb = (const float *)gbw;
     fpgb.resize((size_t)(NA / 4) * GB_ROWS);
     for (int rb = 0; rb < GB_ROWS / 8; rb++)
       for (int k = 0; k < NA / 4; k++)
@@ -1128,11 +1213,8 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
           const float *src = wb + 32 * (size_t)(gb_first[rb] + k);
           fpgb[(size_t)k * GB_ROWS + rb * 8 + r] = make_float4(src[0 * 8 + r], src[1 * 8 + r], src[2 * 8 + r], src[3 * 8 + r]);
         }
-    for (int w = 0; w < SAMPLE_WAVES; w++) {
-      sa.fp_nzr[w] = fp_nzr[w];
-      sa.fp_nh[w] = fp_nh[w];
-    }
   }
+  sa.fp_long = fp_ok && fp_long ? 1 : 0;
 
   /* choose streams per workgroup and check the LDS budget of the lockstep
    * kernel: the whole image in LDS, or -- models with long block rows -- only
@@ -1198,7 +1280,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     UP(fa.proj_b, pb.data(), pb.size() * 4);
   }
   UP(fa.embed_pitch, embed_pitch, 256 * EP * 4);
-  UP(fa.rcp, rcp_dev, sizeof(rcp_dev));
+  UP(fa.rcp, rcp_dev.data(), RCP_ENTRIES * 4);
   UP(sa.emb_sig, emb_sig, 256 * GA_ROWS * 4);
   UP(sa.emb_pred, emb_pred, 256 * GA_ROWS * 4);
   UP(sa.emb_exc, emb_exc, 256 * GA_ROWS * 4);
@@ -1267,12 +1349,17 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     }
     UP(sa.mf_gb, mfgb.data(), mfgb.size() * 4);
   }
-  if (fp_ok) {
+  if (fp_ok && !fp_long) {
     UP(sa.fp_zr, fpzr.data(), fpzr.size() * sizeof(float4));
     UP(sa.fp_h, fph.data(), fph.size() * sizeof(float4));
-    UP(sa.fp_gb, fpgb.data(), fpgb.size() * sizeof(float4));
     UP(sa.fp_off, fpoff.data(), fpoff.size() * 4);
   }
+  if (fp_ok && fp_long) {
+    UP(sa.fpl_zr, fplzr.data(), fplzr.size() * sizeof(float4));
+    UP(sa.fpl_h, fplh.data(), fplh.size() * sizeof(float4));
+    UP(sa.fpl_off, fploff.data(), fploff.size() * 4);
+  }
+  if (fp_ok) UP(sa.fp_gb, fpgb.data(), fpgb.size() * sizeof(float4));
   if (!int8) {
     UP(sa.ga_wf, ga_wf.data(), ga_wf.size() * sizeof(float4));
     UP(sa.gb_recf, gbrec, 3 * NB * NB * 4);
@@ -1283,6 +1370,12 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   b->sa = sa;
   b->fa = fa;
   b->mc = mc;
+  {
+    std::vector<uint32_t> dflt(RCP_ENTRIES);
+    for (int i = 0; i < RCP_ENTRIES; i++) dflt[i] = kRcpTable[i >> (RCP_TABLE_BITS - 11)] + kRcpBias;
+    b->rcp_custom = rcp_dev != dflt;
+    b->rcp_dev = rcp_dev;
+  }
   b->variant = variant;
   b->sat = sat;
   b->reg = reg;
@@ -1320,6 +1413,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     b->mf_ga_ops = 2.0 * n4 * 1024.0;
     b->mf_gb_ops = 2.0 * 2.0 * MF_GB_TILES * 16384.0;
   }
+  in.long_rows = (mf_ok && sa.mf_split) || (fp_ok && sa.fp_long) ? 1 : 0;
   in.lpc_gamma = mc.lpc_gamma;
   in.features_delay = mc.delay;
   in.end2end = mc.end2end;
@@ -1710,6 +1804,25 @@ LPCNET_EXPORT int lpcnet_batch_set_model_constants(LPCNetBatch *b, float lpc_gam
   b->info.lpc_gamma = mc.lpc_gamma;
   b->info.features_delay = mc.delay;
   b->info.end2end = mc.end2end;
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_set_rcp_table(LPCNetBatch *b, const uint32_t *tab)
+{
+  if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
+  std::vector<uint32_t> dev(RCP_ENTRIES), dflt(RCP_ENTRIES);
+  for (int i = 0; i < RCP_ENTRIES; i++) {
+    dflt[i] = kRcpTable[i >> (RCP_TABLE_BITS - 11)] + kRcpBias;
+    dev[i] = tab ? tab[i] + kRcpBias : dflt[i];
+  }
+  if (b->set_device()) return -1;
+  HIPCHK(hipStreamSynchronize(b->stream));
+  /* the LDS image's table section and the frame network's global copy */
+  HIPCHK(hipMemcpy((unsigned char *)b->sa.image + IMG_RCP, dev.data(), RCP_ENTRIES * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((void *)b->fa.rcp, dev.data(), RCP_ENTRIES * 4, hipMemcpyHostToDevice));
+  b->rcp_dev = dev;
+  b->rcp_custom = dev != dflt;
+  choose_kernel(b);
   return 0;
 }
 
@@ -2104,7 +2217,7 @@ static uint64_t pool_key(const unsigned char *data, int len)
   mix(data, (size_t)len);
   mix(&len, sizeof(len));
   /* load-time overrides change the model bound to the same bytes */
-  for (const char *e : {"LPCNET_LPC_GAMMA", "LPCNET_FEATURES_DELAY", "LPCNET_END2END", "LPCNET_KERNEL"}) {
+  for (const char *e : {"LPCNET_LPC_GAMMA", "LPCNET_FEATURES_DELAY", "LPCNET_END2END", "LPCNET_KERNEL", "LPCNET_RCP"}) {
     const char *v = getenv(e);
     mix(e, strlen(e));
     if (v) mix(v, strlen(v));

@@ -160,7 +160,94 @@ __device__ __forceinline__ float h_chain(const float4 *hw, const float4 *xb, con
   return y;
 }
 
-template <bool TRACE>
+/* Long form (trained masks with block rows beyond the register tables):
+ * the z/r chains over n slots streamed from the global tables, FPL_D slots
+ * of weights and column quads in flight, the state quads read one slot
+ * ahead.  Same FMA order as zr_chain (slot order = the reference's block
+ * order; padding slots are -0 weights on the +0 quad). */
+constexpr int FPL_D = 8;
+__device__ __forceinline__ v2f zr_chain_stream(const float4 *xp, const float4 *w2 /* lane's slot 0 (lo, hi) */,
+                                               const uint32_t *of /* lane's slot 0 */, int n, v2f acc)
+{
+  float4 lo[FPL_D], hi[FPL_D];
+  uint32_t oo[FPL_D];
+#pragma unroll
+  for (int d = 0; d < FPL_D; d++)
+    if (d < n) {
+      lo[d] = w2[(size_t)d * 128];
+      hi[d] = w2[(size_t)d * 128 + 1];
+      oo[d] = of[(size_t)d * 64];
+    }
+  float gz = acc.x, gr = acc.y;
+  float4 p = xp[oo[0] & 0xFF], q = xp[(oo[0] >> 8) & 0xFF];
+#pragma unroll 1
+  for (int base = 0; base < n; base += FPL_D) {
+#pragma unroll
+    for (int d = 0; d < FPL_D; d++) {
+      const int t = base + d;
+      if (t < n) {
+        const float4 a = lo[d], b = hi[d];
+        const float4 pc = p, qc = q;
+        /* next slot's state quads (its offsets arrived FPL_D slots ago) */
+        if (t + 1 < n) {
+          const uint32_t on = oo[(d + 1) % FPL_D];
+          p = xp[on & 0xFF];
+          q = xp[(on >> 8) & 0xFF];
+        }
+        if (t + FPL_D < n) {
+          lo[d] = w2[(size_t)(t + FPL_D) * 128];
+          hi[d] = w2[(size_t)(t + FPL_D) * 128 + 1];
+          oo[d] = of[(size_t)(t + FPL_D) * 64];
+        }
+        gz = __builtin_fmaf(a.x, pc.x, gz);
+        gr = __builtin_fmaf(a.y, qc.x, gr);
+        gz = __builtin_fmaf(a.z, pc.y, gz);
+        gr = __builtin_fmaf(a.w, qc.y, gr);
+        gz = __builtin_fmaf(b.x, pc.z, gz);
+        gr = __builtin_fmaf(b.y, qc.z, gr);
+        gz = __builtin_fmaf(b.z, pc.w, gz);
+        gr = __builtin_fmaf(b.w, qc.w, gr);
+        asm volatile("" : "+v"(gz), "+v"(gr));
+      }
+    }
+  }
+  return v2f{gz, gr};
+}
+
+/* the h chain of the long form: every slot streamed */
+__device__ __forceinline__ float h_chain_stream(const float4 *hw /* lane's slot 0 */, const uint32_t *of, const float4 *xb, int n,
+                                                float y)
+{
+  float4 w[FPL_D];
+  uint32_t oo[FPL_D];
+#pragma unroll
+  for (int d = 0; d < FPL_D; d++)
+    if (d < n) {
+      w[d] = hw[(size_t)d * 64];
+      oo[d] = of[(size_t)d * 64];
+    }
+  float4 x = xb[oo[0] & 0xFF];
+#pragma unroll 1
+  for (int base = 0; base < n; base += FPL_D) {
+#pragma unroll
+    for (int d = 0; d < FPL_D; d++) {
+      const int t = base + d;
+      if (t < n) {
+        const float4 wt = w[d], xt = x;
+        if (t + 1 < n) x = xb[oo[(d + 1) % FPL_D] & 0xFF];
+        if (t + FPL_D < n) {
+          w[d] = hw[(size_t)(t + FPL_D) * 64];
+          oo[d] = of[(size_t)(t + FPL_D) * 64];
+        }
+        y = fma4(wt, xt, y);
+        asm volatile("" : "+v"(y));
+      }
+    }
+  }
+  return y;
+}
+
+template <bool TRACE, bool LONG>
 __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
 {
   extern __shared__ uint4 lds4[];
@@ -223,7 +310,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
     float st = ps->gru_a_state[i];
     v4f wz[FP_ZF], wr[FP_ZF];
     uint32_t oz[FP_ZF / 4], orr[FP_ZF / 4], oh[FP_HF / 4];
-    {
+    if (!LONG) {
       const v4f *t = (const v4f *)A.fp_zr + (size_t)g * 2 * FP_ZF * 64 + lane;
 #pragma unroll
       for (int k = 0; k < FP_ZF; k++) {
@@ -250,6 +337,11 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
     /* h row (nnet.c:439 + the h rows of the sparse product): bias + diag*state
      * then the chain over the column blocks of h_A(n) in buffer xb */
     auto hchain = [&](const float4 *xb) -> float {
+      if constexpr (LONG) {
+        size_t ho = (size_t)g * A.fpl_kh * 64 + lane;
+        asm volatile("" : "+v"(ho));
+        return h_chain_stream(A.fpl_h + ho, A.fpl_off + (size_t)SAMPLE_WAVES * A.fpl_kz * 64 + ho, xb, nh, bh + dh * st);
+      }
       size_t ho = (size_t)(g * FP_HF * 64 + lane);
       asm volatile("" : "+v"(ho)); /* same weights every sample: do not hoist their loads */
       const float4 *hw = A.fp_h + ho;
@@ -271,14 +363,16 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
     for (int n = 0; n < A.N; n++) {
       const float4 *xp = xs + (n & 1) * FP_SLOTS;   /* h_A(n-1) */
       float4 *xn = xs + ((n + 1) & 1) * FP_SLOTS;   /* h_A(n) */
-      keep_packed(oz);
-      keep_packed(orr);
-      /* first column quads of the z and r chains, before the indices land */
       v4f xz[FP_XD], xr[FP_XD];
+      if (!LONG) {
+        keep_packed(oz);
+        keep_packed(orr);
+        /* first column quads of the z and r chains, before the indices land */
 #pragma unroll
-      for (int d = 0; d < FP_XD; d++) {
-        xz[d] = fp_xv(xp, oz, d);
-        xr[d] = fp_xv(xp, orr, d);
+        for (int d = 0; d < FP_XD; d++) {
+          xz[d] = fp_xv(xp, oz, d);
+          xr[d] = fp_xv(xp, orr, d);
+        }
       }
       stamp(5);
       flag_wait<1>(ixseq, n + 1, abort_w, A.spin_limit);
@@ -308,6 +402,11 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
       stamp(1);
       /* z and r rows (nnet.c:434 + sparse product): two interleaved chains */
       v2f acc = {tz + inz, tr + inr};
+      if constexpr (LONG) {
+        size_t zo = (size_t)g * A.fpl_kz * 64 + lane;
+        asm volatile("" : "+v"(zo));
+        acc = zr_chain_stream(xp, A.fpl_zr + 2 * zo, A.fpl_off + zo, nzr, acc);
+      } else
       switch ((nzr + 1) / 2) {
         case 0: case 1: zr_chain<2>(xp, wz, wr, oz, orr, xz, xr, acc); break;
         case 2: zr_chain<4>(xp, wz, wr, oz, orr, xz, xr, acc); break;
@@ -525,18 +624,19 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
   }
 }
 
-template <bool TRACE>
+template <bool TRACE, bool LONG>
 static int launch_fp_t(const SampleArgs &a, hipStream_t stream)
 {
-  if (ensure_dyn_lds((const void *)fp_kernel<TRACE>, 160 * 1024 - IMG_VAR)) return -1;
-  hipLaunchKernelGGL((fp_kernel<TRACE>), dim3(warm_grid(a.nstreams, a.nstreams)), dim3(FP_THREADS), fp_lds_bytes() - IMG_VAR, stream, a);
+  if (ensure_dyn_lds((const void *)fp_kernel<TRACE, LONG>, 160 * 1024 - IMG_VAR)) return -1;
+  hipLaunchKernelGGL((fp_kernel<TRACE, LONG>), dim3(warm_grid(a.nstreams, a.nstreams)), dim3(FP_THREADS), fp_lds_bytes() - IMG_VAR, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_fp(const SampleArgs &a, void *stream)
 {
   hipStream_t st = (hipStream_t)stream;
-  return a.trace_logits ? launch_fp_t<true>(a, st) : launch_fp_t<false>(a, st);
+  if (a.fp_long) return a.trace_logits ? launch_fp_t<true, true>(a, st) : launch_fp_t<false, true>(a, st);
+  return a.trace_logits ? launch_fp_t<true, false>(a, st) : launch_fp_t<false, false>(a, st);
 }
 
 }  // namespace lpcnet_mi355x

@@ -92,12 +92,18 @@ struct alignas(16) StreamState {
   int pad[1];
 };
 
-/* The device rcpps table holds t + kRcpBias (device_math.h rcp_x86_fix). */
+/* The device rcpps table holds t + kRcpBias (device_math.h rcp_x86_fix),
+ * indexed by the top RCP_TABLE_BITS mantissa bits of the Pade denominator:
+ * 12, so one table format holds both the Intel build host's rcpps (a
+ * function of the top 11 bits: each entry twice) and the AMD EPYC GPU-box
+ * host's (a function of the top 12 bits, profiles/r03/box_rcpps.json). */
 constexpr uint32_t kRcpBias = 127u << 23;
+constexpr int RCP_TABLE_BITS = 12;
+constexpr int RCP_ENTRIES = 1 << RCP_TABLE_BITS;
 
 /* Fixed sections of the sample kernel's LDS image (byte offsets). */
-constexpr int IMG_RCP = 0;                       /* 2048 u32 rcpps table */
-constexpr int IMG_ULAW = IMG_RCP + 2048 * 4;     /* 256 f32 ulaw2lin */
+constexpr int IMG_RCP = 0;                       /* RCP_ENTRIES u32 rcpps table */
+constexpr int IMG_ULAW = IMG_RCP + RCP_ENTRIES * 4; /* 256 f32 ulaw2lin */
 constexpr int IMG_LOGIT = IMG_ULAW + 256 * 4;    /* 256 f32 sampling logit table */
 constexpr int IMG_FCW = IMG_LOGIT + 256 * 4;     /* dual_fc weights [256][2][16] f32 */
 constexpr int IMG_FCB = IMG_FCW + 256 * 32 * 4;  /* dual_fc bias [2][256] */
@@ -139,7 +145,7 @@ struct FrameArgs {
   const float *gadf_w, *gadf_b, *gbdf_w, *gbdf_b;
   const float *proj_w, *proj_b; /* gadf | gbdf as one [COND][GA_ROWS + GB_ROWS] matrix, bias */
   const float *embed_pitch;
-  const uint32_t *rcp; /* 2048-entry table in global memory */
+  const uint32_t *rcp; /* RCP_ENTRIES-entry table in global memory */
   unsigned long long *stamps; /* optional diagnostics [grid][16] s_memtime per phase */
   /* chunk_kernel only: features = [nframes][B][NF], lpc_new = [nframes][B][NLPC],
    * outputs of frame f into cond[f * B .. f * B + B) */
@@ -206,6 +212,13 @@ struct SampleArgs {
   const uint32_t *fp_off;
   int fp_nzr[SAMPLE_WAVES];    /* slots of the z/r chains per GRU_A wave */
   int fp_nh[SAMPLE_WAVES];     /* slots of the h chains */
+  /* fp_kernel long form (block rows beyond FP_ZF / FP_HF): every slot
+   * streamed, [wave][slot][64 lanes]: z/r packed pairs (2 float4), h float4,
+   * offsets (z quad | r quad << 8 for fpl_kz slots, then h quads) */
+  int fp_long;
+  int fpl_kz, fpl_kh;
+  const float4 *fpl_zr, *fpl_h;
+  const uint32_t *fpl_off;
   const float4 *ga_wf;   /* fp32 variant: GRU_A blocks [chunk][k][64] float4 */
   const float4 *gb_wf;   /* fp32 variant: GRU_B blocks [rb][k][8 rows][2] float4 (in c) */
   const float *gb_recf;  /* fp32 variant: GRU_B recurrent [NB][GB_ROWS] */

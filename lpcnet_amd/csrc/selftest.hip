@@ -21,8 +21,8 @@ namespace lpcnet_mi355x {
 __global__ void numerics_kernel(int op, const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int n,
                                 const uint32_t *__restrict__ rcp_g)
 {
-  __shared__ uint32_t rcp[2048];
-  for (int k = threadIdx.x; k < 2048; k += blockDim.x) rcp[k] = rcp_g[k];
+  __shared__ uint32_t rcp[RCP_ENTRIES];
+  for (int k = threadIdx.x; k < RCP_ENTRIES; k += blockDim.x) rcp[k] = rcp_g[k];
   __syncthreads();
   if (op == 8) {
     /* kiss99 (kiss99.c:59-81): n draws from the state in[0..3], one lane */
@@ -91,12 +91,12 @@ extern "C" LPCNET_EXPORT int lpcnet_mi355x_device_numerics(int device, int op, c
   const size_t nin = op == 8 ? 4 : (size_t)n;
   uint32_t *d_in = nullptr, *d_out = nullptr, *d_rcp = nullptr;
   const uint32_t *tab = lpcnet_mi355x_rcp_table();
-  std::vector<uint32_t> rcp_dev(2048);
-  for (int i = 0; i < 2048; i++) rcp_dev[i] = tab[i] + kRcpBias;
+  std::vector<uint32_t> rcp_dev(RCP_ENTRIES);
+  for (int i = 0; i < RCP_ENTRIES; i++) rcp_dev[i] = tab[i >> (RCP_TABLE_BITS - 11)] + kRcpBias; /* 11-bit x86 table */
   int rc = -1;
   if (hipMalloc(&d_in, nin * 4) == hipSuccess && hipMalloc(&d_out, (size_t)n * 4) == hipSuccess &&
-      hipMalloc(&d_rcp, 2048 * 4) == hipSuccess && hipMemcpy(d_in, in, nin * 4, hipMemcpyHostToDevice) == hipSuccess &&
-      hipMemcpy(d_rcp, rcp_dev.data(), 2048 * 4, hipMemcpyHostToDevice) == hipSuccess) {
+      hipMalloc(&d_rcp, RCP_ENTRIES * 4) == hipSuccess && hipMemcpy(d_in, in, nin * 4, hipMemcpyHostToDevice) == hipSuccess &&
+      hipMemcpy(d_rcp, rcp_dev.data(), RCP_ENTRIES * 4, hipMemcpyHostToDevice) == hipSuccess) {
     const int grid = op == 8 ? 1 : (n + 255) / 256;
     hipLaunchKernelGGL(numerics_kernel, dim3(grid), dim3(256), 0, 0, op, d_in, d_out, n, d_rcp);
     if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&

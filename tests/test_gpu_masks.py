@@ -67,6 +67,38 @@ def test_forced_split_matches_golden(require_gpu, monkeypatch):
     assert np.array_equal(bits(st["gru_b_state"]), bits(G["final_gru_b_state"]))
 
 
+def test_forced_long_fp32_matches_golden(require_gpu, monkeypatch):
+    """fp_kernel's long form (every z/r/h slot streamed from global memory)
+    on the default fp32 model == the golden fixture, PCM and final states."""
+    monkeypatch.setenv("LPCNET_FP_FORCE_LONG", "1")
+    G = np.load(os.path.join(O.GOLDEN, "streams_fp32.npz"))
+    b = L.LPCNetBatch(len(G["streams"]), 0, L.synthetic_model(1, 1))
+    info = b.info()
+    assert info.quad_path == 5 and info.long_rows == 1
+    for fr in range(G["pcm"].shape[1]):
+        assert np.array_equal(b.synthesize(G["features"][:, fr, :20]), G["pcm"][:, fr]), fr
+    st = b.get_state(0)
+    assert np.array_equal(bits(st["gru_a_state"]), bits(G["final_gru_a_state"]))
+    assert np.array_equal(bits(st["gru_b_state"]), bits(G["final_gru_b_state"]))
+
+
+@pytest.mark.parametrize("B", [1, 70])
+def test_skewed_fp32_on_fp_kernel(require_gpu, B):
+    """Skewed fp32 model: the automatic kernel is fp_kernel's long form,
+    against the oracle (host frames, then the overlapped device path)."""
+    F = 8
+    blob = L.synthetic_model(1, 1, skewed=True)
+    b = L.LPCNetBatch(B, 0, blob)
+    assert b.info().quad_path == 5 and b.info().long_rows == 1
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    out = np.concatenate([np.stack([b.synthesize(allf[f]) for f in range(3)]), _frames(b, allf, 3, F)], 0)
+    assert np.abs(out[3:].astype(np.float64)).mean() > 100
+    for s in (0, B - 1):
+        o = O.Oracle(blob, 1)
+        exp = np.stack([o.synthesize(allf[f, s]) for f in range(F)])
+        assert np.array_equal(out[:, s], exp), s
+
+
 @pytest.mark.parametrize("B,check", [(1, (0,)), (70, (0, 69)), (256, (0, 255)), (1030, (0, 517, 1029))])
 def test_skewed_int8_on_matrix_cores(require_gpu, B, check):
     """Skewed (Sparsify-like) int8 model: the automatic kernel is mf_kernel
@@ -76,7 +108,7 @@ def test_skewed_int8_on_matrix_cores(require_gpu, B, check):
     F = 8
     blob = L.synthetic_model(1, 0, skewed=True)
     b = L.LPCNetBatch(B, 0, blob)
-    assert b.info().quad_path == 4, b.info().quad_path
+    assert b.info().quad_path == 4 and b.info().long_rows == 1, b.info().quad_path
     allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
     out = np.concatenate([np.stack([b.synthesize(allf[f]) for f in range(3)]), _frames(b, allf, 3, F)], 0)
     assert np.abs(out[3:].astype(np.float64)).mean() > 100
