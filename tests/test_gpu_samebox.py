@@ -45,7 +45,10 @@ def test_engine_with_host_rcpps_matches_live_reference(require_gpu, variant):
             differ += int(np.sum(exp != ports[s].synthesize(allf[f, s])))
     print(f"host rcpps {'equals' if intel else 'differs from'} the Intel table; the live reference differs from "
           f"the Intel-table reference in {differ} of {B * F * 160} samples")
-    if not intel:
+    if not intel and variant == 0:
+        # the int8 model's PCM visibly depends on the host (the fp32 one may
+        # not flip a sample in 14 frames: a rcpps difference changes a
+        # logit's last bits, rarely a decision)
         assert differ > 0
     # back to the default table: the Intel-table numerics of the golden fixtures
     b.set_rcp_table(None)
