@@ -18,14 +18,14 @@ cd /tmp
 # kernel trace + stats of the bench command (all four configurations; two
 # warmup frames = the silent FEATURES_DELAY frames, so every non-silent
 # launch of a multi-frame kernel covers the same number of frames)
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps $STEPS --warmup 2 --no-cpu --no-latency > "$R/gpurun_out/prof.log" 2>&1 || { echo "rocprof trace rc=$?"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps $STEPS --warmup 2 --no-cpu --no-latency --no-capacity > "$R/gpurun_out/prof.log" 2>&1 || { echo "rocprof trace rc=$?"; exit 1; }
 echo "trace ok"
 # PMC passes: one counter group per run (slot limits, MI355X_MICROARCH.md)
 for cfg in "b1024:--streams 1024" "b256:--streams 256" "b1:--streams 1" "b1_fp32:--streams 1 --variant fp32"; do
   name=${cfg%%:*}; args=${cfg#*:}
   for pass in "fetch:FETCH_SIZE" "write:WRITE_SIZE" "l2:TCC_HIT_sum TCC_MISS_sum" "mfma:SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
     pn=${pass%%:*}; ctr=${pass#*:}
-    timeout -s KILL 120 rocprofv3 --pmc $ctr -d "$R/gpurun_out/pmc_${pn}_${name}" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 2 $args --no-cpu --no-batch1 --no-latency > "$R/gpurun_out/pmc_${pn}_${name}.log" 2>&1 || { echo "pmc $pn $name rc=$?"; exit 1; }
+    timeout -s KILL 120 rocprofv3 --pmc $ctr -d "$R/gpurun_out/pmc_${pn}_${name}" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 2 $args --no-cpu --no-batch1 --no-latency --no-capacity > "$R/gpurun_out/pmc_${pn}_${name}.log" 2>&1 || { echo "pmc $pn $name rc=$?"; exit 1; }
   done
   echo "pmc $name ok"
 done
