@@ -247,6 +247,9 @@ def latency(L, blob, B, measured_ms):
             "sampler_walk": float(sm[11]),
             "sampler_post": float(sm[12]),
             "sampler_wait_at_Y": float(sm[1]),
+            "sampler_wait_at_X": float(sm[5]),
+            "gru_a_recurrent_slowest_wave": float(ga[:, 2].max()),
+            "gru_a_wait_at_X_fastest_wave": float(ga[:, 5].min()),
         }
     elif info.quad_path == 5:
         # fp_kernel (fp32, one stream per workgroup): hardware wave

@@ -489,7 +489,18 @@ static int mf_wave_cost(const std::vector<std::vector<int>> &ga, const int *ub8)
 #define MF_SAMPLER_SIMD_WEIGHT 27
 #endif
 
-static std::vector<int> mf_assign_unit_blocks(const std::vector<std::vector<int>> &ga)
+/* per-SIMD load of six GRU_A wave costs: waves 0/4 and 1/5 pair up; 2 and 3
+ * pair with a sampler (its priority chain takes most of their SIMD: measured
+ * ~74 cycles per slot there against ~27 per slot of a wave pair) */
+static int mf_simd_score(const int *c)
+{
+  return std::max(std::max(c[0] + c[4], c[1] + c[5]), (MF_SAMPLER_SIMD_WEIGHT * std::max(c[2], c[3])) / 10);
+}
+
+/* extra[w]: a fixed per-wave cost on top of its own rows (split models: the
+ * hosted pieces) */
+static std::vector<int> mf_assign_unit_blocks(const std::vector<std::vector<int>> &ga, const int *extra = nullptr,
+                                              int iters = 40000)
 {
   constexpr int NUB = NA / 8;
   std::vector<int> perm(NUB);
@@ -500,16 +511,13 @@ static std::vector<int> mf_assign_unit_blocks(const std::vector<std::vector<int>
   auto score = [&](const std::vector<int> &p, long &sum) {
     int c[SAMPLE_WAVES];
     sum = 0;
-    for (int w = 0; w < SAMPLE_WAVES; w++) sum += (c[w] = mf_wave_cost(ga, &p[8 * w]));
-    /* per-SIMD load: waves 0/4 and 1/5 pair up; 2 and 3 pair with a sampler
-     * (its priority chain takes most of their SIMD: measured ~74 cycles per
-     * slot there against ~27 per slot of a wave pair) */
-    return std::max(std::max(c[0] + c[4], c[1] + c[5]), (MF_SAMPLER_SIMD_WEIGHT * std::max(c[2], c[3])) / 10);
+    for (int w = 0; w < SAMPLE_WAVES; w++) sum += (c[w] = mf_wave_cost(ga, &p[8 * w]) + (extra ? extra[w] : 0));
+    return mf_simd_score(c);
   };
   long best_sum;
   int best = score(perm, best_sum);
   uint32_t rng = 12345u;
-  for (int it = 0; it < 40000; it++) {
+  for (int it = 0; it < iters; it++) {
     rng = rng * 1664525u + 1013904223u;
     const int a = (rng >> 8) % NUB;
     rng = rng * 1664525u + 1013904223u;
@@ -620,74 +628,101 @@ struct MfPlan {
   int nzr[SAMPLE_WAVES] = {}, nh[SAMPLE_WAVES] = {}, nfzr[SAMPLE_WAVES] = {}, nfh[SAMPLE_WAVES] = {};
 };
 
-bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P)
+/* hosted-piece merge cost of a wave, in MFMA slots: its partial sums'
+ * LDS adds (per gate hosted) */
+#ifndef MF_HOST_ADD_SLOTS
+#define MF_HOST_ADD_SLOTS 4
+#endif
+
+/* One candidate split (own caps T, piece sizes F) laid out: own rows ->
+ * lane groups balanced together with the hosted pieces (which waves host z/r
+ * and h pieces: every subset that holds them and fits the registers, scored
+ * by the per-SIMD load), pieces -> lane groups of the hosting waves.
+ * Returns the score (-1: does not fit). */
+static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const int T[3], const int F[3], int iters)
 {
   constexpr int NUB = NA / 8, NLG = SAMPLE_WAVES * 8;
-  int kmax[3] = {0, 0, 0};
-  for (int g = 0; g < 3; g++)
-    for (int u = 0; u < NUB; u++) kmax[g] = std::max(kmax[g], (int)ga[g * NUB + u].size());
-  auto pieces_needed = [&](int g, int T, int F) {
-    long n = 0;
+  P.own[0] = T[0];
+  P.own[1] = T[1];
+  P.own[2] = T[2];
+  for (int g = 0; g < 3; g++) {
+    P.pieces[g].clear();
     for (int u = 0; u < NUB; u++) {
       const int K = (int)ga[g * NUB + u].size();
-      if (K > T) n += F > 0 ? (K - T + F - 1) / F : 1000000;
+      for (int t0 = T[g]; t0 < K; t0 += F[g]) P.pieces[g].push_back(MfPiece{u, t0, std::min(K, t0 + F[g])});
     }
-    return n;
-  };
-  if (std::max(kmax[0], kmax[1]) <= MF_ZMAX && kmax[2] <= MF_HMAX && !getenv("LPCNET_MF_FORCE_SPLIT")) {
-    P.split = false;
-  } else {
-    /* smallest per-sample MFMA count 2 (Tzr + Fzr) + (Th + Fh) whose pieces
-     * fit one per lane group (LPCNET_MF_FORCE_SPLIT: split even a model that
-     * fits, with the smallest own cap, for tests) */
-    const bool force = getenv("LPCNET_MF_FORCE_SPLIT") != nullptr;
-    long best = -1;
-    int bz[2] = {0, 0}, bh[2] = {0, 0};
-    for (int Tz = 4; Tz <= MF_ZMAX; Tz += 4)
-      for (int Fz = 0; Tz + Fz <= MF_ZMAX; Fz += 4) {
-        const long pz = std::max(pieces_needed(0, Tz, Fz), pieces_needed(1, Tz, Fz));
-        if (pz > NLG || (Fz > 0 && pz == 0)) continue;
-        for (int Th = 4; Th <= MF_HMAX; Th += 4)
-          for (int Fh = 0; Th + Fh <= MF_HMAX; Fh += 4) {
-            const long ph = pieces_needed(2, Th, Fh);
-            if (ph > NLG || (Fh > 0 && ph == 0)) continue;
-            if (force && pz + ph == 0) continue;
-            const long cost = 2 * (Tz + Fz) + Th + Fh;
-            if (best < 0 || cost < best || (force && cost == best && Tz < bz[0])) {
-              best = cost;
-              bz[0] = Tz; bz[1] = Fz; bh[0] = Th; bh[1] = Fh;
-            }
-          }
-      }
-    if (best < 0) return false; /* does not fit even split: the lockstep kernel runs it */
-    P.split = true;
-    P.own[0] = P.own[1] = bz[0];
-    P.own[2] = bh[0];
-    const int F[3] = {bz[1], bz[1], bh[1]};
-    for (int g = 0; g < 3; g++) {
-      P.pieces[g].clear();
-      for (int u = 0; u < NUB; u++) {
-        const int K = (int)ga[g * NUB + u].size();
-        for (int t0 = P.own[g]; t0 < K; t0 += F[g]) P.pieces[g].push_back(MfPiece{u, t0, std::min(K, t0 + F[g])});
-      }
-    }
+    if ((int)P.pieces[g].size() > NLG) return -1;
   }
-  /* own parts -> unit-block assignment (balance, see mf_assign_unit_blocks) */
   std::vector<std::vector<int>> own(ga.size());
   for (int g = 0; g < 3; g++)
     for (int u = 0; u < NUB; u++) {
       const std::vector<int> &v = ga[g * NUB + u];
-      own[g * NUB + u].assign(v.begin(), v.begin() + std::min((int)v.size(), P.own[g]));
+      own[g * NUB + u].assign(v.begin(), v.begin() + std::min((int)v.size(), T[g]));
     }
-  P.perm = mf_assign_unit_blocks(own);
-  /* pieces -> lane groups, spread over the waves (lane group 8w + j in the
-   * order j-major, w-minor) */
+  const int npz = (int)std::max(P.pieces[0].size(), P.pieces[1].size()), nph = (int)P.pieces[2].size();
+  int extra[SAMPLE_WAVES] = {};
+  int mz = 0, mh = 0; /* hosting waves (bit masks) */
+  long best = -1;
+  P.perm = mf_assign_unit_blocks(own, extra, iters);
+  for (int round = 0; round < 2; round++) {
+    int c[SAMPLE_WAVES], gz[SAMPLE_WAVES], gh[SAMPLE_WAVES];
+    for (int w = 0; w < SAMPLE_WAVES; w++) {
+      c[w] = mf_wave_cost(own, &P.perm[8 * w]);
+      size_t az = 0, ah = 0;
+      for (int j = 0; j < 8; j++) {
+        const int ub = P.perm[8 * w + j];
+        az = std::max(az, std::max(own[ub].size(), own[NUB + ub].size()));
+        ah = std::max(ah, own[2 * NUB + ub].size());
+      }
+      gz[w] = (int)(az + 3) / 4;
+      gh[w] = (int)(ah + 3) / 4;
+    }
+    best = -1;
+    for (int sz = 0; sz < (1 << SAMPLE_WAVES); sz++) {
+      if (8 * __builtin_popcount(sz) < npz || (npz == 0 && sz)) continue;
+      for (int sh = 0; sh < (1 << SAMPLE_WAVES); sh++) {
+        if (8 * __builtin_popcount(sh) < nph || (nph == 0 && sh)) continue;
+        int cc[SAMPLE_WAVES];
+        bool ok = true;
+        long sum = 0;
+        for (int w = 0; w < SAMPLE_WAVES && ok; w++) {
+          cc[w] = c[w];
+          if (sz >> w & 1) {
+            ok &= 4 * gz[w] + F[0] <= MF_ZMAX;
+            cc[w] += 2 * F[0] + 2 * MF_HOST_ADD_SLOTS;
+          }
+          if (sh >> w & 1) {
+            ok &= 4 * gh[w] + F[2] <= MF_HMAX;
+            cc[w] += F[2] + MF_HOST_ADD_SLOTS;
+          }
+          sum += cc[w];
+        }
+        if (!ok) continue;
+        const long sc = (long)mf_simd_score(cc) * 4096 + sum;
+        if (best < 0 || sc < best) {
+          best = sc;
+          mz = sz;
+          mh = sh;
+        }
+      }
+    }
+    if (best < 0) return -1;
+    if (round == 1) break;
+    /* re-balance the own rows around the hosting waves' extra load */
+    for (int w = 0; w < SAMPLE_WAVES; w++)
+      extra[w] = (mz >> w & 1 ? 2 * F[0] + 2 * MF_HOST_ADD_SLOTS : 0) + (mh >> w & 1 ? F[2] + MF_HOST_ADD_SLOTS : 0);
+    P.perm = mf_assign_unit_blocks(own, extra, iters);
+  }
+  /* pieces -> lane groups of the hosting waves, spread over those waves
+   * (lane group j of each hosting wave, then j + 1) */
   for (int g = 0; g < 3; g++) {
+    const int m = g < 2 ? mz : mh;
+    std::vector<int> lgs;
+    for (int j = 0; j < 8; j++)
+      for (int w = 0; w < SAMPLE_WAVES; w++)
+        if (m >> w & 1) lgs.push_back(8 * w + j);
     P.host[g].assign(NLG, -1);
-    for (int p = 0; p < (int)P.pieces[g].size(); p++) {
-      const int lg = 8 * (p % SAMPLE_WAVES) + p / SAMPLE_WAVES;
-      P.host[g][lg] = p;
-    }
+    for (int p = 0; p < (int)P.pieces[g].size(); p++) P.host[g][lgs[p]] = p;
   }
   for (int w = 0; w < SAMPLE_WAVES; w++) {
     int kz = 0, kh = 0, fz = 0, fh = 0;
@@ -705,9 +740,64 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P)
     P.nh[w] = (kh + 3) / 4;
     P.nfzr[w] = (fz + 3) / 4;
     P.nfh[w] = (fh + 3) / 4;
-    if (4 * (P.nzr[w] + P.nfzr[w]) > MF_ZMAX || 4 * (P.nh[w] + P.nfh[w]) > MF_HMAX) return false;
+    if (4 * (P.nzr[w] + P.nfzr[w]) > MF_ZMAX || 4 * (P.nh[w] + P.nfh[w]) > MF_HMAX) return -1;
   }
-  return true;
+  return best;
+}
+
+bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P)
+{
+  constexpr int NUB = NA / 8;
+  int kmax[3] = {0, 0, 0};
+  for (int g = 0; g < 3; g++)
+    for (int u = 0; u < NUB; u++) kmax[g] = std::max(kmax[g], (int)ga[g * NUB + u].size());
+  const bool force = getenv("LPCNET_MF_FORCE_SPLIT") != nullptr;
+  if (std::max(kmax[0], kmax[1]) <= MF_ZMAX && kmax[2] <= MF_HMAX && !force) {
+    P.split = false;
+    const int T[3] = {MF_ZMAX, MF_ZMAX, MF_HMAX}, F[3] = {0, 0, 0};
+    return mf_layout(ga, P, T, F, 40000) >= 0;
+  }
+  /* split: every own cap / piece size pair, screened with a short
+   * assignment search, the best re-laid-out in full (LPCNET_MF_FORCE_SPLIT:
+   * split even a model that fits -- pieces required -- for tests) */
+  P.split = true;
+  long best = -1;
+  int bt[3] = {0, 0, 0}, bf[3] = {0, 0, 0};
+  for (int Tz = 4; Tz <= MF_ZMAX; Tz += 4)
+    for (int Fz = 0; Tz + Fz <= MF_ZMAX; Fz += 4)
+      for (int Th = 4; Th <= MF_HMAX; Th += 4)
+        for (int Fh = 0; Th + Fh <= MF_HMAX; Fh += 4) {
+          bool need = false, fits = true;
+          for (int g = 0; g < 3; g++) {
+            const int T = g < 2 ? Tz : Th, F = g < 2 ? Fz : Fh;
+            for (int u = 0; u < NUB; u++) {
+              const int K = (int)ga[g * NUB + u].size();
+              need |= K > T;
+              if (K > T && F == 0) fits = false;
+            }
+            /* a piece size with nothing to carry is padding */
+            bool any = false;
+            for (int u = 0; u < NUB; u++) any |= (int)ga[g * NUB + u].size() > T;
+            if (F > 0 && !any && g != 0 && g != 1) fits = false;
+          }
+          if (Fz > 0) {
+            bool any = false;
+            for (int u = 0; u < NUB; u++) any |= std::max(ga[u].size(), ga[NUB + u].size()) > (size_t)Tz;
+            if (!any) fits = false;
+          }
+          if (!fits || (force && !need)) continue;
+          MfPlan C;
+          const int T[3] = {Tz, Tz, Th}, F[3] = {Fz, Fz, Fh};
+          const long sc = mf_layout(ga, C, T, F, 1500);
+          if (sc < 0) continue;
+          if (best < 0 || sc < best) {
+            best = sc;
+            bt[0] = bt[1] = Tz; bt[2] = Th;
+            bf[0] = bf[1] = Fz; bf[2] = Fh;
+          }
+        }
+  if (best < 0) return false; /* does not fit even split: the lockstep kernel runs it */
+  return mf_layout(ga, P, bt, bf, 40000) >= 0;
 }
 
 /* The model constants of a blob (see load_model); -1 on a malformed record
@@ -1000,6 +1090,11 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
       fprintf(stderr, " own caps z/r %d h %d, pieces z %zu r %zu h %zu; groups per wave (own zr, hosted zr, own h, hosted h):",
               plan.own[0], plan.own[2], plan.pieces[0].size(), plan.pieces[1].size(), plan.pieces[2].size());
       for (int w = 0; w < SAMPLE_WAVES; w++) fprintf(stderr, " (%d %d %d %d)", plan.nzr[w], plan.nfzr[w], plan.nh[w], plan.nfh[w]);
+      for (int g = 0; g < 3; g++) {
+        std::vector<int> per(NA / 8, 0);
+        for (const MfPiece &pc : plan.pieces[g]) per[pc.unit]++;
+        fprintf(stderr, "%s max pieces per row %d", g ? "," : ";", per.empty() ? 0 : *std::max_element(per.begin(), per.end()));
+      }
     }
     fprintf(stderr, "\n");
   }
@@ -1067,6 +1162,14 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
           }
         }
       }
+    }
+    /* bit 16 of a lane's entry of gate g: its own row (unit mf_units[lane])
+     * has hosted pieces there, whose sums it merges after barrier X */
+    for (int g = 0; g < 3; g++) {
+      std::vector<char> has(NA / 8, 0);
+      for (const MfPiece &pc : plan.pieces[g]) has[pc.unit] = 1;
+      for (int t = 0; t < SAMPLE_WAVES * 64; t++)
+        if (has[mf_units[t] / 8]) mf_frow[(size_t)g * SAMPLE_WAVES * 64 + t] |= 1 << 16;
     }
     /* GRU_B: dense A tiles, lane l = row 16g + l%16, k = 64kt + 16(l/16) + byte */
     std::vector<int8_t> dense((size_t)GB_ROWS * NA, 0), drec((size_t)GB_ROWS * NB, 0);

@@ -107,47 +107,41 @@ __device__ __forceinline__ void mf_run(const unsigned char *lds, const uint32_t 
   }
 }
 
-/* Split models (engine.cpp mf_plan): the z and r products over the own
- * groups [0, no) into az / ar and over the hosted piece's groups [no, no +
- * nf) into fz / fr (another row's partial sums); x words of the next group
- * read while the current group's MFMAs run.  Runtime group counts: this
- * work hides behind the sampler chain. */
-__device__ __forceinline__ void mf_zr_split(const unsigned char *lds, const uint32_t (&wz)[MF_ZMAX],
-                                            const uint32_t (&wr)[MF_ZMAX], const uint32_t (&oz)[MF_ZMAX / 2],
-                                            const uint32_t (&orr)[MF_ZMAX / 2], int no, int nf, v4i &az, v4i &ar,
-                                            v4i &fz, v4i &fr)
+/* Split models (engine.cpp mf_plan): the z and r products over NO own
+ * groups into az / ar and NF hosted groups (a piece of another row) into
+ * fz / fr, compile-time counts (a runtime own/hosted choice per group makes
+ * the compiler issue the next group's LDS reads only after the current
+ * group's MFMAs have drained: measured ~1.7K extra cycles per sample).  x
+ * words of group 0 come preloaded in xz / xr; those of group g+1 are read
+ * while group g's MFMAs run. */
+template <int NO, int NF>
+__device__ __forceinline__ void mf_zr_ct(const unsigned char *lds, const uint32_t (&wz)[MF_ZMAX],
+                                         const uint32_t (&wr)[MF_ZMAX], const uint32_t (&oz)[MF_ZMAX / 2],
+                                         const uint32_t (&orr)[MF_ZMAX / 2], uint32_t (&xz)[4], uint32_t (&xr)[4],
+                                         v4i &az, v4i &ar, v4i &fz, v4i &fr)
 {
-  const int ng = no + nf;
-  uint32_t xz[4], xr[4];
+  static_assert(NO + NF <= MF_ZMAX / 4, "z/r groups");
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    xz[k] = mf_x(lds, oz, k);
-    xr[k] = mf_x(lds, orr, k);
-  }
+  for (int g = 0; g < NO + NF; g++) {
+    uint32_t nz[4], nr[4];
+    if (g + 1 < NO + NF) {
 #pragma unroll
-  for (int g = 0; g < MF_ZMAX / 4; g++) {
-    if (g < ng) {
-      uint32_t nz[4], nr[4];
-      if (g + 1 < MF_ZMAX / 4 && g + 1 < ng) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          nz[k] = mf_x(lds, oz, 4 * (g + 1) + k);
-          nr[k] = mf_x(lds, orr, 4 * (g + 1) + k);
-        }
+      for (int k = 0; k < 4; k++) {
+        nz[k] = mf_x(lds, oz, 4 * (g + 1) + k);
+        nr[k] = mf_x(lds, orr, 4 * (g + 1) + k);
       }
-      if (g < no) {
+    }
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          az = mfma4(xz[k], wz[4 * g + k], az);
-          ar = mfma4(xr[k], wr[4 * g + k], ar);
-        }
+    for (int k = 0; k < 4; k++) {
+      if (g < NO) {
+        az = mfma4(xz[k], wz[4 * g + k], az);
+        ar = mfma4(xr[k], wr[4 * g + k], ar);
       } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          fz = mfma4(xz[k], wz[4 * g + k], fz);
-          fr = mfma4(xr[k], wr[4 * g + k], fr);
-        }
+        fz = mfma4(xz[k], wz[4 * g + k], fz);
+        fr = mfma4(xr[k], wr[4 * g + k], fr);
       }
+    }
+    if (g + 1 < NO + NF) {
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         xz[k] = nz[k];
@@ -157,33 +151,75 @@ __device__ __forceinline__ void mf_zr_split(const unsigned char *lds, const uint
   }
 }
 
-/* the same for one gate of NS slots (h) */
-template <int NS>
-__device__ __forceinline__ void mf_run_split(const unsigned char *lds, const uint32_t (&w)[NS], const uint32_t (&o)[NS / 2],
-                                             int no, int nf, v4i &a, v4i &f)
+/* the same for the h gate: NO own groups over two chains a[], NF hosted
+ * groups over two chains f[] */
+template <int NO, int NF>
+__device__ __forceinline__ void mf_h_ct(const unsigned char *lds, const uint32_t (&w)[MF_HMAX],
+                                        const uint32_t (&o)[MF_HMAX / 2], uint32_t (&x)[4], v4i (&a)[2], v4i (&f)[2])
 {
-  const int ng = no + nf;
-  uint32_t x[4];
+  static_assert(NO + NF <= MF_HMAX / 4, "h groups");
 #pragma unroll
-  for (int k = 0; k < 4; k++) x[k] = mf_x(lds, o, k);
+  for (int g = 0; g < NO + NF; g++) {
+    uint32_t n[4];
+    if (g + 1 < NO + NF) {
 #pragma unroll
-  for (int g = 0; g < NS / 4; g++) {
-    if (g < ng) {
-      uint32_t n[4];
-      if (g + 1 < NS / 4 && g + 1 < ng) {
+      for (int k = 0; k < 4; k++) n[k] = mf_x(lds, o, 4 * (g + 1) + k);
+    }
 #pragma unroll
-        for (int k = 0; k < 4; k++) n[k] = mf_x(lds, o, 4 * (g + 1) + k);
-      }
-      if (g < no) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) a = mfma4(x[k], w[4 * g + k], a);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++) f = mfma4(x[k], w[4 * g + k], f);
-      }
+    for (int k = 0; k < 4; k++) {
+      if (g < NO)
+        a[k & 1] = mfma4(x[k], w[4 * g + k], a[k & 1]);
+      else
+        f[k & 1] = mfma4(x[k], w[4 * g + k], f[k & 1]);
+    }
+    if (g + 1 < NO + NF) {
 #pragma unroll
       for (int k = 0; k < 4; k++) x[k] = n[k];
     }
+  }
+}
+
+/* runtime (no, nf) -> the compile-time forms (every count the plan allows) */
+__device__ __forceinline__ void mf_zr_split(const unsigned char *lds, const uint32_t (&wz)[MF_ZMAX],
+                                            const uint32_t (&wr)[MF_ZMAX], const uint32_t (&oz)[MF_ZMAX / 2],
+                                            const uint32_t (&orr)[MF_ZMAX / 2], int no, int nf, uint32_t (&xz)[4],
+                                            uint32_t (&xr)[4], v4i &az, v4i &ar, v4i &fz, v4i &fr)
+{
+  switch (no * 8 + nf) {
+#define MF_ZC(O, F)                                                   \
+  case O * 8 + F:                                                     \
+    mf_zr_ct<O, F>(lds, wz, wr, oz, orr, xz, xr, az, ar, fz, fr);     \
+    break;
+    MF_ZC(0, 1) MF_ZC(0, 2) MF_ZC(0, 3) MF_ZC(0, 4)
+    MF_ZC(1, 0) MF_ZC(1, 1) MF_ZC(1, 2) MF_ZC(1, 3)
+    MF_ZC(2, 0) MF_ZC(2, 1) MF_ZC(2, 2)
+    MF_ZC(3, 0) MF_ZC(3, 1)
+    MF_ZC(4, 0)
+#undef MF_ZC
+    default: break;
+  }
+}
+
+__device__ __forceinline__ void mf_h_split(const unsigned char *lds, const uint32_t (&w)[MF_HMAX],
+                                           const uint32_t (&o)[MF_HMAX / 2], int no, int nf, uint32_t (&x)[4],
+                                           v4i (&a)[2], v4i (&f)[2])
+{
+  switch (no * 16 + nf) {
+#define MF_HC(O, F)                                \
+  case O * 16 + F:                                 \
+    mf_h_ct<O, F>(lds, w, o, x, a, f);             \
+    break;
+    MF_HC(0, 1) MF_HC(0, 2) MF_HC(0, 3) MF_HC(0, 4) MF_HC(0, 5) MF_HC(0, 6) MF_HC(0, 7) MF_HC(0, 8)
+    MF_HC(1, 0) MF_HC(1, 1) MF_HC(1, 2) MF_HC(1, 3) MF_HC(1, 4) MF_HC(1, 5) MF_HC(1, 6) MF_HC(1, 7)
+    MF_HC(2, 0) MF_HC(2, 1) MF_HC(2, 2) MF_HC(2, 3) MF_HC(2, 4) MF_HC(2, 5) MF_HC(2, 6)
+    MF_HC(3, 0) MF_HC(3, 1) MF_HC(3, 2) MF_HC(3, 3) MF_HC(3, 4) MF_HC(3, 5)
+    MF_HC(4, 0) MF_HC(4, 1) MF_HC(4, 2) MF_HC(4, 3) MF_HC(4, 4)
+    MF_HC(5, 0) MF_HC(5, 1) MF_HC(5, 2) MF_HC(5, 3)
+    MF_HC(6, 0) MF_HC(6, 1) MF_HC(6, 2)
+    MF_HC(7, 0) MF_HC(7, 1)
+    MF_HC(8, 0)
+#undef MF_HC
+    default: break;
   }
 }
 

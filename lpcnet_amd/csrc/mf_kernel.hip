@@ -49,7 +49,7 @@ struct MfLds {
   static constexpr int okw = 8 * 4;           /* per-GRU_A-wave "inputs in range" words */
   static constexpr int gbw = 3 * 64 * 16;     /* GRU_B recurrent A tiles [3][64 lanes] (LDS, not registers) */
   static constexpr int total = x + xb + sb + ix + pcm + cnd + gbs + gbr + okw + gbw;
-  static constexpr int part = 3 * (NA + 1) * S * 4; /* split models: hosted partial sums [3][NA + 1][S] (row NA: none) */
+  static constexpr int part = 3 * (NA + 1) * S * 4; /* split models: hosted partial sums [3][S][NA + 1] (row NA: none) */
 };
 
 int mf_lds_bytes(int S, int split)
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   int *gbr = gbs + S * GB_ROWS;
   int *okw = gbr + GB_ROWS;
   v4i *gbw = (v4i *)(okw + 8);
-  int *part = (int *)(gbw + 3 * 64); /* SPLIT: [3][NA + 1][S] */
+  int *part = (int *)(gbw + 3 * 64); /* SPLIT: [3][S][NA + 1] (rows contiguous: a lane group's 8 rows on 8 banks) */
   /* fixed image sections (rcpps / u-law / logit tables, dual_fc) in static
    * LDS: addresses into dynamic LDS carry an extra add of its base per
    * access, on the activation and walk chains */
@@ -212,8 +212,18 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     /* split models: this lane's hosted groups and the rows their partial
      * sums belong to (NA: none) */
     const int nfzr = SPLIT ? A.mf_nfzr[wv] : 0, nfh = SPLIT ? A.mf_nfh[wv] : 0;
-    const int frz = SPLIT ? A.mf_frow[tid] : NA, frr = SPLIT ? A.mf_frow[SAMPLE_THREADS + tid] : NA,
-              frh = SPLIT ? A.mf_frow[2 * SAMPLE_THREADS + tid] : NA;
+    /* split models: the rows this lane's hosted pieces belong to (NA: none),
+     * 9 bits per gate, and per gate whether this thread's own unit has
+     * hosted pieces to merge (bits 27..29), in one register for the whole
+     * launch */
+    uint32_t frow = 0;
+    if constexpr (SPLIT) {
+      const uint32_t *fro = (const uint32_t *)A.mf_frow + tid;
+      const uint32_t e0 = fro[0], e1 = fro[SAMPLE_THREADS], e2 = fro[2 * SAMPLE_THREADS];
+      frow = (e0 & 0x1FF) | (e1 & 0x1FF) << 9 | (e2 & 0x1FF) << 18 | (e0 >> 16 & 1) << 27 | (e1 >> 16 & 1) << 28 |
+             (e2 >> 16 & 1) << 29;
+    }
+
     __syncthreads(); /* image in LDS */
     bool fast = true;
     for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8_state(st[s]);
@@ -231,7 +241,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
      * computed right after the recurrent product (off the X->Y critical path):
      * az/ar, the (subias + diag*state) terms of z and r, and the whole
      * recurrent h-gate value (nnet.c:431-440) */
-    int az[S], ar[S], ah[S], hseed[S];
+    int az[S], ar[S], ah[S];
     float tz[S], tr[S], hpre[S];
     auto recurrent = [&]() {
       v4i vz[1] = {{wsz, wsz, wsz, wsz}}, vr[1] = {{wsr, wsr, wsr, wsr}}, vh[2] = {{wsh, wsh, wsh, wsh}, {0, 0, 0, 0}};
@@ -241,14 +251,28 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
       if constexpr (SPLIT) {
         /* own groups into v*, the hosted piece into f*, whose partial sums
          * go to their row's owner through LDS (exact int32 adds, any order);
-         * the owners add them after barrier X */
-        v4i fz = {0, 0, 0, 0}, fr = {0, 0, 0, 0}, fh = {0, 0, 0, 0};
-        mf_zr_split(lds, wz, wr, oz, orr, nzr, nfzr, vz[0], vr[0], fz, fr);
-        mf_run_split<MF_HMAX>(lds, wh, oh, nh, nfh, vh[0], fh);
+         * the owners add them after barrier X.  Group 0's x words of both
+         * products are read first: the h product's are in flight while the
+         * z/r MFMAs run (the two switches break the prefetch chain) */
+        v4i fz = {0, 0, 0, 0}, fr = {0, 0, 0, 0}, fh[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+        uint32_t xz[4], xr[4], xh[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          xz[k] = mf_x(lds, oz, k);
+          xr[k] = mf_x(lds, orr, k);
+          xh[k] = mf_x(lds, oh, k);
+        }
+        mf_zr_split(lds, wz, wr, oz, orr, nzr, nfzr, xz, xr, vz[0], vr[0], fz, fr);
+        mf_h_split(lds, wh, oh, nh, nfh, xh, vh, fh);
+        uint32_t fp = frow;
+        asm volatile("" : "+v"(fp)); /* unpacked here, not hoisted into three registers */
+        const int frz = (int)(fp & 0x1FF), frr = (int)((fp >> 9) & 0x1FF), frh = (int)((fp >> 18) & 0x1FF);
+        /* only lanes hosting a piece add (a shared dummy row would
+         * serialise every other lane's atomic on one LDS address) */
         for (int s = 0; s < S; s++) {
-          atomicAdd(&part[(0 * (NA + 1) + frz) * S + s], fz[s]);
-          atomicAdd(&part[(1 * (NA + 1) + frr) * S + s], fr[s]);
-          atomicAdd(&part[(2 * (NA + 1) + frh) * S + s], fh[s]);
+          if (frz != NA) atomicAdd(&part[(0 * S + s) * (NA + 1) + frz], fz[s]);
+          if (frr != NA) atomicAdd(&part[(1 * S + s) * (NA + 1) + frr], fr[s]);
+          if (frh != NA) atomicAdd(&part[(2 * S + s) * (NA + 1) + frh], fh[0][s] + fh[1][s]);
         }
       } else if (TRACE) {
         mf_zr<1>(lds, wz, wr, oz, orr, nzr, vz, vr);
@@ -285,7 +309,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         tz[s] = bz + dz * st[s];
         tr[s] = br + dr * st[s];
         if constexpr (SPLIT)
-          hseed[s] = cvt_rne((bh + dh * st[s]) * kScale);
+          ah[s] += cvt_rne((bh + dh * st[s]) * kScale); /* the seed now: int32 sums associate */
         else
           hpre[s] = (float)(ah[s] + cvt_rne((bh + dh * st[s]) * kScale)) * kScale1;
       }
@@ -351,18 +375,33 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
             }
           }
           if constexpr (SPLIT) {
-            /* the hosted pieces' partial sums of this lane's rows (written
-             * between barriers Y and X), then cleared for the next sample */
-            for (int s = 0; s < S; s++) {
-              int *pz = &part[(0 * (NA + 1) + i) * S + s], *pr = &part[(1 * (NA + 1) + i) * S + s],
-                  *ph = &part[(2 * (NA + 1) + i) * S + s];
-              az[s] += *pz;
-              ar[s] += *pr;
-              hpre[s] = (float)((ah[s] + *ph) + hseed[s]) * kScale1;
-              *pz = 0;
-              *pr = 0;
-              *ph = 0;
-            }
+            /* the hosted pieces' partial sums of this thread's rows (written
+             * between barriers Y and X), then cleared for the next sample;
+             * only rows that have pieces (LDS bandwidth: all six waves do
+             * this at once, on the critical path) */
+            uint32_t fp = frow;
+            asm volatile("" : "+v"(fp));
+            if (fp >> 27 & 1)
+              for (int s = 0; s < S; s++) {
+                int *pz = &part[(0 * S + s) * (NA + 1) + i];
+                az[s] += *pz;
+                *pz = 0;
+              }
+            if (fp >> 28 & 1)
+              for (int s = 0; s < S; s++) {
+                int *pr = &part[(1 * S + s) * (NA + 1) + i];
+                ar[s] += *pr;
+                *pr = 0;
+              }
+            int hadd[S];
+            for (int s = 0; s < S; s++) hadd[s] = 0;
+            if (fp >> 29 & 1)
+              for (int s = 0; s < S; s++) {
+                int *ph = &part[(2 * S + s) * (NA + 1) + i];
+                hadd[s] = *ph;
+                *ph = 0;
+              }
+            for (int s = 0; s < S; s++) hpre[s] = (float)(ah[s] + hadd[s]) * kScale1;
           }
           if (stamping) {
             /* diagnostic only: wait for every gather before the stamp */
