@@ -124,7 +124,7 @@ def max_over_ranks(dist, x):
     return float(t.item())
 
 
-def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1, preheat_ms=0.0):
+def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1, preheat_ms=0.0, kernel=0):
     """Returns (seconds for `steps` frames, kernel ms / launches, info, pcm).
     The timed region carries HIP events around each sample-kernel launch
     (timers=1; 2 adds the frame kernel); the frame kernel's own time comes
@@ -135,6 +135,8 @@ def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1,
     feats = np.ascontiguousarray(feats, np.float32)  # [F][B][20]
     ndev = max(1, L.device_count())
     b = L.LPCNetBatch(B, int(os.environ.get("LOCAL_RANK", "0")) % ndev, blob)
+    if kernel:
+        b.set_kernel(kernel)
     d_feat = b.device_alloc(feats.nbytes)
     d_pcm = b.device_alloc((F + extra) * B * 160 * 2)
     b.h2d(d_feat, feats)
@@ -418,6 +420,27 @@ def skewed_lines(L, args):
     return out
 
 
+def lockstep_lines(L, args):
+    """The lockstep sample kernel (kernels.hip, mode 1): the kernel of every
+    model the fast kernels do not take -- saturating int8 models (int16
+    maddubs saturation emulated), fp32 models with a sparse GRU_B -- and of
+    the same-box parity mode.  Measured on the saturating int8 model at 1024
+    streams (automatic selection), and forced on the default int8 model at
+    1024 streams and the default fp32 model at batch 1, beside the fast
+    kernels' lines for the same models."""
+    out = {}
+    cases = (("sat_int8_b1024", L.synthetic_model(1, L.VARIANT_INT8, saturating=True), 1024, 0),
+             ("int8_b1024_forced", L.synthetic_model(1, L.VARIANT_INT8), 1024, 1),
+             ("fp32_b1_forced", L.synthetic_model(1, L.VARIANT_FP32), 1, 1))
+    for name, blob, B, mode in cases:
+        nf = max(args.steps, 20)
+        dt, (k, n, kf, _, _), info, _ = run_batch(L, blob, B, 0, args.warmup, nf, None, args.timers, args.preheat_ms,
+                                                  kernel=mode)
+        out[name] = {"samples_per_s": B * nf * 160 / dt, "sample_kernel_ms_per_frame": k / max(kf, 1),
+                     "kernel": info.kernel_name, "quad_path": info.quad_path}
+    return out
+
+
 def main():
     args = parse()
     world, rank, local, dist = dist_setup(args)
@@ -473,6 +496,7 @@ def main():
         out["batch256"] = side_line(L, blob, 256, args, "b256", "int8")
     if rank == 0 and world == 1 and not args.no_batch1:
         out["skewed_int8"] = skewed_lines(L, args)
+        out["lockstep"] = lockstep_lines(L, args)
     if rank == 0 and world == 1 and not args.no_capacity:
         out["capacity"] = capacity(L, blob, args)
     if rank == 0 and world == 1 and not args.no_cpu:
