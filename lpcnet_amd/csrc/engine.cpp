@@ -955,6 +955,21 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     memcpy(&img[IMG_LOGIT + 4 * i], &lg, 4);
   }
   memcpy(&img[IMG_FCW], fc_w, 256 * 32 * 4);
+  bool fc_fin = true;
+  {
+    /* dual-FC node sums (nnet.c:193-199) are bounded by |bias| + 2 sum|w|
+     * for GRU_B states within [-2, 2]: far below 2^60 and finite, tanh8's
+     * flush and NaN selects are dead (tanh_x86_fin_n) */
+    bool fin = true;
+    for (int c = 0; c < 2 && fin; c++)
+      for (int i = 0; i < 256 && fin; i++) {
+        double bd = fabs((double)fc_b[c * 256 + i]);
+        for (int j = 0; j < 16; j++) bd += 2.0 * fabs((double)fc_w[i * 32 + c * 16 + j]);
+        fin = std::isfinite(bd) && bd < 0x1p59;
+      }
+    const char *fe = getenv("LPCNET_FC_EXACT"); /* test hook: force the exact form */
+    fc_fin = fin && !(fe && atoi(fe));
+  }
   memcpy(&img[IMG_FCB], fc_b, 512 * 4);
   memcpy(&img[IMG_FCF], fc_f, 512 * 4);
   auto align16 = [&]() { img.resize((img.size() + 15) / 16 * 16, 0); };
@@ -967,6 +982,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   };
   SampleArgs sa;
   memset(&sa, 0, sizeof(sa));
+  sa.fc_fin = fc_fin ? 1 : 0;
   std::vector<float4> ga_wf, gb_wf_unused;
   if (int8) sa.gb_rec_off = (int)put(gbrec, 3 * NB * NB);
   /* blocks per lane for each (wave, gate) of the GRU_A layout */

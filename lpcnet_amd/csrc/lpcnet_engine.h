@@ -196,6 +196,10 @@ struct SampleArgs {
                                         streams: the elementwise step's range selects are dead (mf_kernel);
                                         negative: never */
   float mf_h_bound;                  /* the same for the h gate's conditioning (tanh range) */
+  int fc_fin;                        /* every dual-FC node sum |bias| + 2 sum|w| is finite and below
+                                        2^59: with GRU_B states within [-2, 2] (int8 models keep them
+                                        there; checked per launch) the walk's tanh takes the
+                                        select-free form */
   const float *mf_emb[3];            /* sig/pred/exc tables with columns in lane order:
                                         [256][3][SAMPLE_WAVES * 64], column p = unit mf_unit[p] */
   int mf_nzr[SAMPLE_WAVES];          /* own 4-slot groups per GRU_A wave: z and r */

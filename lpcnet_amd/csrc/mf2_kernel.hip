@@ -269,8 +269,10 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
     const bool samp = ms < S;
     const bool samp_w = samp && (S == 4 || half == 0);
     const int msc = samp ? ms : 0;
-    /* GRU_B lanes: (unit quad gq, stream gs, gi), unit gu = 4gq + gi */
-    const int gq = lane >> 4, gs = (lane & 15) >> 2, gi = lane & 3, gu = 4 * gq + gi, sl = min(gs, S - 1);
+    /* GRU_B lanes: (stream gs, unit gu) = (lane / 16, lane % 16); states
+     * as the MFMA A operand (row m = stream m/4), weight tiles as B: D
+     * register 0 is unit gu of stream gs (mf_kernel) */
+    const int gs = lane >> 4, gu = lane & 15, sl = min(gs, S - 1), sx = min(gu >> 2, S - 1);
     const bool gown = gs < S && (S == 4 ? (gs >> 1) : gs) == sw;
 
     float lsr[2][NLPC], pred[2], deemph[2], sbv[2];
@@ -289,6 +291,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
       g_act[g] = gown && active[g * S + sl];
       sbv[g] = A.st[min(s0 + g * S + sl, A.nstreams - 1)].gru_b_state[gu];
     }
+
     /* GRU_B input tiles in registers, the recurrent ones in LDS */
     v4i wt[MF_GB_IN];
 #pragma unroll
@@ -348,29 +351,28 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
       /* GRU_B (nnet.c:345-361): recurrent product on q(h_B(t-1)), input
        * product on q(h_A(t)), all S streams of the group as MFMA columns */
       v4i acc[3], accr[3];
-      const v4i xr = *(const v4i *)(xb + (g * S + sl) * NB);
+      const v4i xr = *(const v4i *)(xb + (g * S + sx) * NB); /* k 0..15; the tiles' other K chunks are zero */
 #pragma unroll
       for (int q = 0; q < 3; q++) {
-        acc[q] = *(const v4i *)(myg + (g * S + sl) * GB_ROWS + 16 * q + 4 * gq);
-        accr[q] = *(const v4i *)(gbr + 16 * q + 4 * gq);
+        acc[q] = v4i{myg[(g * S + sl) * GB_ROWS + 16 * q + gu], 0, 0, 0};
+        accr[q] = v4i{gbr[16 * q + gu], 0, 0, 0};
       }
 #pragma unroll
-      for (int q = 0; q < 3; q++) accr[q] = mfma16(gbw[q * 64 + lane], xr, accr[q]);
+      for (int q = 0; q < 3; q++) accr[q] = mfma16(xr, gbw[q * 64 + lane], accr[q]);
       v4i xk[6];
 #pragma unroll
-      for (int kt = 0; kt < 6; kt++) xk[kt] = *(const v4i *)(xa + (g * S + sl) * MF_XSTR + 64 * kt + 16 * gq);
+      for (int kt = 0; kt < 6; kt++) xk[kt] = *(const v4i *)(xa + (g * S + sx) * MF_XSTR + 64 * kt + 16 * gs);
 #pragma unroll
       for (int kt = 0; kt < 6; kt++)
 #pragma unroll
-        for (int q = 0; q < 2; q++) acc[q] = mfma16(wt[q * 6 + kt], xk[kt], acc[q]);
+        for (int q = 0; q < 2; q++) acc[q] = mfma16(xk[kt], wt[q * 6 + kt], acc[q]);
 #pragma unroll
-      for (int kt = 0; kt < 6; kt++) acc[2] = mfma16(wt[12 + kt], xk[kt], acc[2]);
-      auto pick = [&](const v4i &a) -> int { return gi == 0 ? a[0] : (gi == 1 ? a[1] : (gi == 2 ? a[2] : a[3])); };
-      float zrb[2] = {(float)pick(acc[0]) * kScale1 + (float)pick(accr[0]) * kScale1,
-                      (float)pick(acc[1]) * kScale1 + (float)pick(accr[1]) * kScale1};
+      for (int kt = 0; kt < 6; kt++) acc[2] = mfma16(xk[kt], wt[12 + kt], acc[2]);
+      float zrb[2] = {(float)acc[0][0] * kScale1 + (float)accr[0][0] * kScale1,
+                      (float)acc[1][0] * kScale1 + (float)accr[1][0] * kScale1};
       sigmoid_x86_fin_n<2, true>(zrb, rcp);
-      float hh[1] = {(float)pick(acc[2]) * kScale1 + ((float)pick(accr[2]) * kScale1) * zrb[1]};
-      tanh_x86_n<1, true>(hh, rcp);
+      float hh[1] = {(float)acc[2][0] * kScale1 + ((float)accr[2][0] * kScale1) * zrb[1]};
+      tanh_x86_fin_n<1, true>(hh, rcp); /* |hh| < 2^19: int32 sums x 2^-14 */
       sbv[g] = zrb[0] * sbv[g] + (1.f - zrb[0]) * hh[0];
       if (gown) sbuf[(g * S + gs) * NB + gu] = sbv[g];
       __builtin_amdgcn_wave_barrier();
@@ -392,6 +394,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
           lpr[4 * j] = v.x; lpr[4 * j + 1] = v.y; lpr[4 * j + 2] = v.z; lpr[4 * j + 3] = v.w;
         }
       }
+      /* (the select-free walk of mf_kernel measured 1 % slower here) */
       const WalkOut R = dual_fc_walk<false>(F, t03, t47, xv, pred[g], lsr[g], lpr, nullptr, deemph[g]);
       if (samp_w && hl == 0) *(int4 *)(ix + (g * S + ms) * 4) = ix_word(R.su, R.pu, R.exc);
       /* bookkeeping (lpcnet.c:262-269) and the output sample */

@@ -447,10 +447,13 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     const bool samp_w = samp && (S == 4 || half == 0);  /* lanes owning the stream's outputs */
     const int ms = samp ? my_s : 0;
     const bool my_active = samp && s0 + ms < A.nstreams && frame_count_of(A, s0 + ms) > A.delay;
-    /* GRU_B: lane = (unit quad gq, stream gs, gi): unit gu = 4gq + gi of
-     * stream gs; the MFMA columns are (gs, gi), so D register gi of this lane
-     * holds row 4gq + gi.  gown: stream gs is one of this wave's. */
-    const int gq = lane >> 4, gs = (lane & 15) >> 2, gi = lane & 3, gu = 4 * gq + gi, sl = min(gs, S - 1);
+    /* GRU_B: lane = (stream gs, unit gu) = (lane / 16, lane % 16).  The
+     * quantised states are the MFMA A operand (row m = stream m/4 of the
+     * group: rows 4gs .. 4gs+3 are stream gs), the weight tiles the B
+     * operand (column n = GRU_B row n of the gate), so D register 0 of this
+     * lane is row 4gs, column gu: unit gu of stream gs, no register pick.
+     * gown: stream gs is one of this wave's. */
+    const int gs = lane >> 4, gu = lane & 15, sl = min(gs, S - 1), sx = min(gu >> 2, S - 1);
     const bool gown = gs < S && (S == 4 ? (gs >> 1) : gs) == sw;
     const bool gact = gown && s0 + gs < A.nstreams && frame_count_of(A, s0 + gs) > A.delay;
 
@@ -470,6 +473,11 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
       rz = p->rng[0]; rw = p->rng[1]; rj = p->rng[2]; rc = p->rng[3];
     }
     float sbv = A.st[min(s0 + sl, A.nstreams - 1)].gru_b_state[gu];
+    /* the walk's select-free tanh: dual-FC node sums bounded by the model
+     * (fc_fin) for GRU_B states within [-2, 2]; int8 GRU_B updates keep a
+     * state there (convex combinations of it and tanh outputs), so the
+     * launch-time check covers the launch */
+    const bool walk_fin = A.fc_fin && __builtin_amdgcn_readfirstlane((int)(__ballot(!(fabsf(sbv) <= 2.f)) == 0ull));
     /* GRU_B weight tiles in registers; with 4 streams the 3 recurrent
      * tiles live in LDS instead (read in the samplers' slack before barrier
      * Y: 12 registers fewer, no spill) */
@@ -488,7 +496,6 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     auto put_xb = [&]() {
       if (gown) xb[gs * NB + gu] = (unsigned char)quant_s8_state(sbv);
     };
-    auto pick = [&](const v4i &a) -> int { return gi == 0 ? a[0] : (gi == 1 ? a[1] : (gi == 2 ? a[2] : a[3])); };
     __syncthreads(); /* image in LDS */
     FcLane F;
     F.init(img, lane);
@@ -550,14 +557,14 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
           lane_thresholds(F, logit_tab, r0, r1, t03, t47);
           /* GRU_B recurrent product (nnet.c:355-361) needs only q(h_B(n-1)):
            * before barrier Y.  Seeds are the accumulator inputs. */
-          const v4i xr = *(const v4i *)(xb + sl * NB);
+          const v4i xr = *(const v4i *)(xb + sx * NB); /* k 0..15; the tiles' other K chunks are zero */
 #pragma unroll
           for (int g = 0; g < 3; g++) {
-            acc[g] = *(const v4i *)(gbs + sl * GB_ROWS + 16 * g + 4 * gq);
-            accr[g] = *(const v4i *)(gbr + 16 * g + 4 * gq);
+            acc[g] = v4i{gbs[sl * GB_ROWS + 16 * g + gu], 0, 0, 0};
+            accr[g] = v4i{gbr[16 * g + gu], 0, 0, 0};
           }
 #pragma unroll
-          for (int g = 0; g < 3; g++) accr[g] = mfma16(kGbwLds ? gbw[g * 64 + lane] : wt[(MF_GB_IN + g) % kRegTiles], xr, accr[g]);
+          for (int g = 0; g < 3; g++) accr[g] = mfma16(xr, kGbwLds ? gbw[g * 64 + lane] : wt[(MF_GB_IN + g) % kRegTiles], accr[g]);
         }
         stamp(0);
         __syncthreads(); /* Y */
@@ -567,22 +574,22 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
           /* GRU_B input product (nnet.c:345-353), 48 x 384, all S streams */
           v4i xk[6];
 #pragma unroll
-          for (int kt = 0; kt < 6; kt++) xk[kt] = *(const v4i *)(xa + sl * MF_XSTR + 64 * kt + 16 * gq);
+          for (int kt = 0; kt < 6; kt++) xk[kt] = *(const v4i *)(xa + sx * MF_XSTR + 64 * kt + 16 * gs);
           /* z and r tiles first: their sigmoids overlap the h tile's MFMAs */
 #pragma unroll
           for (int kt = 0; kt < 6; kt++)
 #pragma unroll
-            for (int g = 0; g < 2; g++) acc[g] = mfma16(wt[g * 6 + kt], xk[kt], acc[g]);
+            for (int g = 0; g < 2; g++) acc[g] = mfma16(xk[kt], wt[g * 6 + kt], acc[g]);
 #pragma unroll
-          for (int kt = 0; kt < 6; kt++) acc[2] = mfma16(wt[12 + kt], xk[kt], acc[2]);
+          for (int kt = 0; kt < 6; kt++) acc[2] = mfma16(xk[kt], wt[12 + kt], acc[2]);
           stamp(10);
           /* GRU_B elementwise (nnet.c:362-371), unit gu of stream sl */
-          float zrb[2] = {(float)pick(acc[0]) * kScale1 + (float)pick(accr[0]) * kScale1,
-                          (float)pick(acc[1]) * kScale1 + (float)pick(accr[1]) * kScale1};
+          float zrb[2] = {(float)acc[0][0] * kScale1 + (float)accr[0][0] * kScale1,
+                          (float)acc[1][0] * kScale1 + (float)accr[1][0] * kScale1};
           sigmoid_x86_fin_n<2, true>(zrb, rcp);
-          float hh[1] = {(float)pick(acc[2]) * kScale1 + ((float)pick(accr[2]) * kScale1) * zrb[1]};
+          float hh[1] = {(float)acc[2][0] * kScale1 + ((float)accr[2][0] * kScale1) * zrb[1]};
           stamp(14);
-          tanh_x86_n<1, true>(hh, rcp);
+          tanh_x86_fin_n<1, true>(hh, rcp); /* |hh| < 2^19: int32 sums x 2^-14 */
           sbv = zrb[0] * sbv + (1.f - zrb[0]) * hh[0];
           if (gown) sbuf[gs * NB + gu] = sbv;
         }
@@ -608,11 +615,14 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
             stamp(k);
           }
         };
-        const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
-                                              deemph, wst);
+        const WalkOut R = walk_fin ? dual_fc_walk<TRACE, true>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
+                                                               deemph, wst)
+                                   : dual_fc_walk<TRACE, false>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
+                                                                deemph, wst);
 #else
-        const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
-                                              deemph);
+        const short *teach = n < A.preload ? pcmbuf + ms * FRAME + n : nullptr;
+        const WalkOut R = walk_fin ? dual_fc_walk<TRACE, true>(F, t03, t47, xv, pred, lsr, lpr, teach, deemph)
+                                   : dual_fc_walk<TRACE, false>(F, t03, t47, xv, pred, lsr, lpr, teach, deemph);
 #endif
         stamp(11);
         if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + ms * 4) = ix_word(R.su, R.pu, R.exc);

@@ -45,20 +45,27 @@ struct FcLane {
   }
 
   /* factor*tanh(bias + w.x) of this lane, plus the other channel's term
-   * (nnet.c:196-205: sum1 + sum2 through DPP quad_perm [1,0,3,2]) */
+   * (nnet.c:196-205: sum1 + sum2 through DPP quad_perm [1,0,3,2]).  FIN:
+   * the node sum is known finite and below 2^60 (SampleArgs::fc_fin and
+   * GRU_B states within [-2, 2]), tanh without its flush and NaN selects */
+  template <bool FIN = false>
   __device__ __forceinline__ float node_logit(float bias, float factor, const float *w, const float (&xv)[NB]) const
   {
     float sum = bias;
 #pragma unroll
     for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
-    return node_logit_tail(sum, factor);
+    return node_logit_tail<FIN>(sum, factor);
   }
 
   /* the same from the finished dot product sum */
+  template <bool FIN = false>
   __device__ __forceinline__ float node_logit_tail(float sum, float factor) const
   {
     float v[1] = {sum};
-    tanh_x86_n<1, true>(v, rcp);
+    if constexpr (FIN)
+      tanh_x86_fin_n<1, true>(v, rcp);
+    else
+      tanh_x86_n<1, true>(v, rcp);
     const float vv = factor * v[0];
     const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(vv), 0xB1, 0xF, 0xF, false));
     return ch2 ? o + vv : vv + o;
@@ -124,7 +131,7 @@ struct WalkNoStamp {
  * Lanes hl and hl + 16 hold the same candidate c = hl & 15; the low 16
  * convert its output sample to u-law, the high 16 its pred(n+1), so one
  * lin2ulaw serves both indices. */
-template <bool TRACE, class ST = WalkNoStamp>
+template <bool TRACE, bool FIN = false, class ST = WalkNoStamp>
 __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, float t47, const float (&xv)[NB], float pred,
                                                 const float (&lsr)[NLPC], const float (&lpr)[NLPC], const short *teach,
                                                 float deemph, ST st = ST())
@@ -139,7 +146,7 @@ __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, floa
   for (int j = 1; j < NLPC; j++) lprod[j] = lsr[j - 1] * lpr[j];
   int val;
   {
-    const float l = F.node_logit(F.b03, F.f03, F.w03, xv);
+    const float l = F.node_logit<FIN>(F.b03, F.f03, F.w03, xv);
     st(2, l);
     val = walk_round(half_bits(__ballot(t03 < l), F.half));
     if (TRACE) {
@@ -192,7 +199,7 @@ __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, floa
   int sp_u = lin2ulaw_x86(F.hl < 16 ? sp_pcm : sp_pred);
   int low;
   {
-    const float l = F.node_logit_tail(sum, f47);
+    const float l = F.node_logit_tail<FIN>(sum, f47);
     st(15, l);
     /* the speculation is needed only when not teaching: pin it before the
      * ballot, or the compiler sinks it into that branch, after the round */

@@ -142,7 +142,7 @@ def test_matrix_core_kernel_edge_cases_at_bench_size(require_gpu, blobs):
         assert np.array_equal(bits(st["gru_b_state"]), bits(g)), s
 
 
-@pytest.mark.parametrize("env", ["LPCNET_MF_EXACT", "LPCNET_MF_ZR_BOUND=0.05", "LPCNET_MF_ZR_BOUND=1.5"])
+@pytest.mark.parametrize("env", ["LPCNET_MF_EXACT", "LPCNET_MF_ZR_BOUND=0.05", "LPCNET_MF_ZR_BOUND=1.5", "LPCNET_FC_EXACT"])
 @pytest.mark.parametrize("B,check", [(1030, (0, 1, 2, 3, 517, 1029)), (70, (0, 37, 69))])
 @pytest.mark.parametrize("mf2", ["0", "1"])
 def test_matrix_core_range_paths_match_oracle(require_gpu, blobs, monkeypatch, env, B, check, mf2):
@@ -363,6 +363,35 @@ def test_restore_refuses_out_of_range_gru_state(require_gpu, blobs):
     for f in range(4):
         ref.synthesize(allf[f])
     assert np.array_equal(b.synthesize(allf[4]), ref.synthesize(allf[4]))
+
+
+@pytest.mark.parametrize("mf2", ["0", "1"])
+def test_walk_exact_form_for_states_outside_the_bound(require_gpu, blobs, monkeypatch, mf2):
+    """The dual-FC walk takes its select-free tanh only when the model's node
+    sums are bounded (SampleArgs::fc_fin) and every GRU_B state of the
+    workgroup lies within [-2, 2] at launch.  A restored NaN GRU_B state
+    (accepted by restore) must send that workgroup through the exact x86
+    form: the same PCM as with the exact form forced (LPCNET_FC_EXACT)."""
+    import struct
+    monkeypatch.setenv("LPCNET_MF2", mf2)
+    blob = blobs["streams_int8"]
+    B, F = 2048 if mf2 == "1" else 3, 7
+    allf = np.stack([feats(s % 3, F) for s in range(B)], 1)
+    outs = []
+    for exact in ("0", "1"):
+        monkeypatch.setenv("LPCNET_FC_EXACT", exact)
+        b = L.LPCNetBatch(B, 0, blob)
+        b.set_kernel(4)
+        for f in range(4):
+            b.synthesize(allf[f])
+        snap = bytearray(b.save_state(1))
+        off = bytes(snap).find(b.get_state(1)["gru_b_state"].tobytes())
+        assert off >= 0
+        struct.pack_into("<f", snap, off + 4 * 3, float("nan"))
+        b.restore_state(1, bytes(snap))
+        outs.append(np.stack([b.synthesize(allf[f]) for f in range(4, F)], 1))
+        b.close()
+    assert np.array_equal(outs[0], outs[1])
 
 
 def test_restore_refuses_out_of_range_last_exc(require_gpu, blobs):
