@@ -121,7 +121,7 @@ class ModelInfo(C.Structure):
         sat = "true" if self.may_saturate else "false"
         lr = "true" if self.long_rows else "false"
         if self.quad_path == 4:
-            return f"mf_kernel<{self.streams_per_workgroup}, false, {lr}>"
+            return f"mf_kernel<{self.streams_per_workgroup}, 0, {lr}>"
         if self.quad_path == 6:
             return "mf2_kernel<4>"
         if self.quad_path == 5:

@@ -59,9 +59,13 @@ int mf_lds_bytes(int S, int split)
   return IMG_VAR + base + (split ? part : 0);
 }
 
-template <int S, bool TRACE, bool SPLIT>
+/* DIAG: 0 the production kernel, 1 with the per-sample logit / excitation
+ * trace (SampleArgs::trace_logits), 2 with the s_memtime phase stamps
+ * (SampleArgs::stamps): the plain kernel carries no diagnostic branch */
+template <int S, int DIAG, bool SPLIT>
 __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
 {
+  constexpr bool TRACE = DIAG == 1;
   extern __shared__ uint4 lds4[];
   unsigned char *lds = (unsigned char *)lds4;
   using L = MfLds<S>;
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     pcmbuf[s * FRAME + n] = A.pcm[(size_t)min(s0 + s, A.nstreams - 1) * A.N + n];
   }
 
-  const bool stamping = A.stamps != nullptr;
+  constexpr bool stamping = DIAG == 2;
   unsigned long long stp[16] = {};
   unsigned long long t_prev = 0, t_loop0 = 0;
   auto stamp = [&](int k) {
@@ -548,8 +552,13 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         __syncthreads(); /* X */
         stamp(5);
         v4i acc[3], accr[3];
+        float lpd[NLPC];
         if (samp) {
           finish();
+          /* pred(n+1)'s candidate-independent products, off the chain */
+          lpd[0] = 0.f;
+#pragma unroll
+          for (int j = 1; j < NLPC; j++) lpd[j] = lsr[j - 1] * lpr[j];
           stamp(13);
           /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
           const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
@@ -615,14 +624,14 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
             stamp(k);
           }
         };
-        const WalkOut R = walk_fin ? dual_fc_walk<TRACE, true>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
-                                                               deemph, wst)
-                                   : dual_fc_walk<TRACE, false>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
-                                                                deemph, wst);
+        const WalkOut R = walk_fin ? dual_fc_walk_p<TRACE, true>(F, t03, t47, xv, pred, lpd, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
+                                                                 deemph, wst)
+                                   : dual_fc_walk_p<TRACE, false>(F, t03, t47, xv, pred, lpd, lpr, n < A.preload ? pcmbuf + ms * FRAME + n : nullptr,
+                                                                  deemph, wst);
 #else
         const short *teach = n < A.preload ? pcmbuf + ms * FRAME + n : nullptr;
-        const WalkOut R = walk_fin ? dual_fc_walk<TRACE, true>(F, t03, t47, xv, pred, lsr, lpr, teach, deemph)
-                                   : dual_fc_walk<TRACE, false>(F, t03, t47, xv, pred, lsr, lpr, teach, deemph);
+        const WalkOut R = walk_fin ? dual_fc_walk_p<TRACE, true>(F, t03, t47, xv, pred, lpd, lpr, teach, deemph)
+                                   : dual_fc_walk_p<TRACE, false>(F, t03, t47, xv, pred, lpd, lpr, teach, deemph);
 #endif
         stamp(11);
         if (samp_w && hl == 0 && n + 1 < A.N) *(int4 *)(ix + ms * 4) = ix_word(R.su, R.pu, R.exc);
@@ -686,13 +695,13 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   }
 }
 
-template <int S, bool TRACE, bool SPLIT>
+template <int S, int DIAG, bool SPLIT>
 static int launch_mf_t(const SampleArgs &a, int lds_bytes, hipStream_t stream)
 {
-  if (ensure_dyn_lds((const void *)mf_kernel<S, TRACE, SPLIT>, 160 * 1024 - IMG_VAR)) return -1;
+  if (ensure_dyn_lds((const void *)mf_kernel<S, DIAG, SPLIT>, 160 * 1024 - IMG_VAR)) return -1;
   const int grid = warm_grid((a.nstreams + S - 1) / S, a.nstreams);
   /* lds_bytes counts the static image too (mf_lds_bytes) */
-  hipLaunchKernelGGL((mf_kernel<S, TRACE, SPLIT>), dim3(grid), dim3(MF_THREADS), lds_bytes - IMG_VAR, stream, a);
+  hipLaunchKernelGGL((mf_kernel<S, DIAG, SPLIT>), dim3(grid), dim3(MF_THREADS), lds_bytes - IMG_VAR, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -700,8 +709,13 @@ template <int S>
 static int launch_mf_s(const SampleArgs &a, int lds_bytes, hipStream_t st)
 {
   if (a.mf_split)
-    return a.trace_logits ? launch_mf_t<S, true, true>(a, lds_bytes, st) : launch_mf_t<S, false, true>(a, lds_bytes, st);
-  return a.trace_logits ? launch_mf_t<S, true, false>(a, lds_bytes, st) : launch_mf_t<S, false, false>(a, lds_bytes, st);
+    return a.trace_logits ? launch_mf_t<S, 1, true>(a, lds_bytes, st)
+           : a.stamps     ? launch_mf_t<S, 2, true>(a, lds_bytes, st)
+                          : launch_mf_t<S, 0, true>(a, lds_bytes, st);
+  /* a trace takes precedence over the stamps (never requested together) */
+  return a.trace_logits ? launch_mf_t<S, 1, false>(a, lds_bytes, st)
+         : a.stamps     ? launch_mf_t<S, 2, false>(a, lds_bytes, st)
+                        : launch_mf_t<S, 0, false>(a, lds_bytes, st);
 }
 
 int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream)

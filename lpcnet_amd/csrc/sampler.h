@@ -131,19 +131,17 @@ struct WalkNoStamp {
  * Lanes hl and hl + 16 hold the same candidate c = hl & 15; the low 16
  * convert its output sample to u-law, the high 16 its pred(n+1), so one
  * lin2ulaw serves both indices. */
+/* lprod[j] (j >= 1) = lsr[j - 1] * lpr[j]: the candidate-independent
+ * products of pred(n+1) (lpcnet.c:252 after the history shift); the
+ * reference multiplies and subtracts separately (no FMA), so a product
+ * computed ahead -- before barrier Y, off the sampler chain -- is the same
+ * float */
 template <bool TRACE, bool FIN = false, class ST = WalkNoStamp>
-__device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, float t47, const float (&xv)[NB], float pred,
-                                                const float (&lsr)[NLPC], const float (&lpr)[NLPC], const short *teach,
-                                                float deemph, ST st = ST())
+__device__ __forceinline__ WalkOut dual_fc_walk_p(const FcLane &F, float t03, float t47, const float (&xv)[NB], float pred,
+                                                  const float (&lprod)[NLPC], const float (&lpr)[NLPC], const short *teach,
+                                                  float deemph, ST st = ST())
 {
   WalkOut R;
-  /* the candidate-independent products of pred(n+1) (lpcnet.c:252 after the
-   * history shift), issued beside round 1's dependent chain: the reference
-   * multiplies and subtracts separately (no FMA), so a product computed
-   * ahead is the same float */
-  float lprod[NLPC];
-#pragma unroll
-  for (int j = 1; j < NLPC; j++) lprod[j] = lsr[j - 1] * lpr[j];
   int val;
   {
     const float l = F.node_logit<FIN>(F.b03, F.f03, F.w03, xv);
@@ -240,6 +238,19 @@ __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, floa
     R.pn = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(sp_pred)));
   }
   return R;
+}
+
+/* the same with the products formed here, beside round 1's dependent chain */
+template <bool TRACE, bool FIN = false, class ST = WalkNoStamp>
+__device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, float t47, const float (&xv)[NB], float pred,
+                                                const float (&lsr)[NLPC], const float (&lpr)[NLPC], const short *teach,
+                                                float deemph, ST st = ST())
+{
+  float lprod[NLPC];
+  lprod[0] = 0.f;
+#pragma unroll
+  for (int j = 1; j < NLPC; j++) lprod[j] = lsr[j - 1] * lpr[j];
+  return dual_fc_walk_p<TRACE, FIN, ST>(F, t03, t47, xv, pred, lprod, lpr, teach, deemph, st);
 }
 
 }  // namespace lpcnet_mi355x
