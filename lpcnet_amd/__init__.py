@@ -125,7 +125,7 @@ class ModelInfo(C.Structure):
         if self.quad_path == 6:
             return "mf2_kernel<4>"
         if self.quad_path == 5:
-            return f"fp_kernel<false, {lr}>"
+            return f"fp_kernel<0, {lr}>"
         quad = "true" if self.quad_path == 1 else "false"
         return f"sample_kernel<{self.streams_per_workgroup}, {self.variant}, {sat}, {quad}>"
 

@@ -247,9 +247,12 @@ __device__ __forceinline__ float h_chain_stream(const float4 *hw /* lane's slot 
   return y;
 }
 
-template <bool TRACE, bool LONG>
+/* DIAG: 0 the production kernel, 1 with the logit / excitation trace, 2
+ * with the s_memtime phase stamps (mf_kernel.hip) */
+template <int DIAG, bool LONG>
 __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
 {
+  constexpr bool TRACE = DIAG == 1;
   extern __shared__ uint4 lds4[];
   unsigned char *lds = (unsigned char *)lds4;
   using L = FpLds;
@@ -285,7 +288,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
   if (tid < 8) done[tid] = 0;
   if (tid == 0) *abort_w = 0;
 
-  const bool stamping = A.stamps != nullptr;
+  constexpr bool stamping = DIAG == 2;
   unsigned long long stp[10] = {};
   unsigned long long t_prev = 0, t_loop0 = 0;
   auto stamp = [&](int k) {
@@ -508,6 +511,11 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
     };
     for (int n = 0; n < A.N; n++) {
       finish();
+      /* pred(n+1)'s candidate-independent products, off the walk */
+      float lpd[NLPC];
+      lpd[0] = 0.f;
+#pragma unroll
+      for (int j = 1; j < NLPC; j++) lpd[j] = lsr[j - 1] * lpr[j];
       /* the two kiss99 draws of this sample and their thresholds (nnet.c:178-184) */
       const uint32_t r0 = kiss99_next(rz, rw, rj, rc);
       const uint32_t r1 = kiss99_next(rz, rw, rj, rc);
@@ -579,7 +587,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
         }
       }
       stamp(3);
-      const WalkOut R = dual_fc_walk<TRACE>(F, t03, t47, xv, pred, lsr, lpr, n < A.preload ? pcmbuf + n : nullptr, deemph);
+      const WalkOut R = dual_fc_walk_p<TRACE>(F, t03, t47, xv, pred, lpd, lpr, n < A.preload ? pcmbuf + n : nullptr, deemph);
       if (n + 1 < A.N && lane == 0) {
         *(int4 *)ix = make_int4(R.su, R.pu, R.exc, 0);
         flag_publish(ixseq, n + 2);
@@ -591,7 +599,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
         for (int b = 1; b < 8; b++) v = lane == b ? R.lg[b] : v;
         A.trace_logits[((size_t)sid * A.N + n) * 8 + lane] = v;
       }
-      if (A.trace_exc && lane == 0) A.trace_exc[(size_t)sid * A.N + n] = R.exc;
+      if (TRACE && A.trace_exc && lane == 0) A.trace_exc[(size_t)sid * A.N + n] = R.exc;
       pend_pcm = R.pcm;
       pend_pred = R.pn;
       pend_exc = R.exc;
@@ -624,19 +632,20 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
   }
 }
 
-template <bool TRACE, bool LONG>
+template <int DIAG, bool LONG>
 static int launch_fp_t(const SampleArgs &a, hipStream_t stream)
 {
-  if (ensure_dyn_lds((const void *)fp_kernel<TRACE, LONG>, 160 * 1024 - IMG_VAR)) return -1;
-  hipLaunchKernelGGL((fp_kernel<TRACE, LONG>), dim3(warm_grid(a.nstreams, a.nstreams)), dim3(FP_THREADS), fp_lds_bytes() - IMG_VAR, stream, a);
+  if (ensure_dyn_lds((const void *)fp_kernel<DIAG, LONG>, 160 * 1024 - IMG_VAR)) return -1;
+  hipLaunchKernelGGL((fp_kernel<DIAG, LONG>), dim3(warm_grid(a.nstreams, a.nstreams)), dim3(FP_THREADS), fp_lds_bytes() - IMG_VAR, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_fp(const SampleArgs &a, void *stream)
 {
   hipStream_t st = (hipStream_t)stream;
-  if (a.fp_long) return a.trace_logits ? launch_fp_t<true, true>(a, st) : launch_fp_t<false, true>(a, st);
-  return a.trace_logits ? launch_fp_t<true, false>(a, st) : launch_fp_t<false, false>(a, st);
+  if (a.fp_long)
+    return a.trace_logits ? launch_fp_t<1, true>(a, st) : a.stamps ? launch_fp_t<2, true>(a, st) : launch_fp_t<0, true>(a, st);
+  return a.trace_logits ? launch_fp_t<1, false>(a, st) : a.stamps ? launch_fp_t<2, false>(a, st) : launch_fp_t<0, false>(a, st);
 }
 
 }  // namespace lpcnet_mi355x
