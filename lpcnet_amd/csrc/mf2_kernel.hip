@@ -164,7 +164,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
     __syncthreads(); /* initial q(h_A) of both groups, ix of both groups, seeds */
 
     /* one group's recurrent terms, for its next elementwise step */
-    int az[S], ar[S];
+    float az[S], ar[S]; /* the recurrent sums as exact floats (ga_elementwise) */
     float tz[S], tr[S], hpre[S];
     auto recurrent = [&](auto gc) {
       constexpr int g = decltype(gc)::value;
@@ -192,8 +192,8 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
           break;
       }
       for (int s = 0; s < S; s++) {
-        az[s] = vz[0][s];
-        ar[s] = vr[0][s];
+        az[s] = (float)vz[0][s];
+        ar[s] = (float)vr[0][s];
         tz[s] = bz + dz * st[g][s];
         tr[s] = br + dr * st[g][s];
         hpre[s] = (float)((vh[0][s] + vh[1][s]) + cvt_rne((bh + dh * st[g][s]) * kScale)) * kScale1;

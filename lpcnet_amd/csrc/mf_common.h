@@ -225,15 +225,22 @@ __device__ __forceinline__ void mf_h_split(const unsigned char *lds, const uint3
 
 /* compute_sparse_gru elementwise (nnet.c:431-447) of one GRU_A unit for S
  * streams, from the gathered rows e (nnet.c:484-491 sums in the reference's
- * order), the recurrent sums az/ar, the state terms tz/tr and the recurrent
- * h-gate value hpre; FAST: the range-guarded select-free forms.  Scalar
+ * order), the recurrent sums faz/far, the state terms tz/tr and the recurrent
+ * h-gate value hpre; FAST: the range-guarded select-free forms.
+ *
+ * faz/far are the int32 recurrent sums as floats: a sum over at most 384
+ * u8 x s8 products is below 384 * 255 * 128 < 2^24, so the float is exact,
+ * and with the seed r = rint((t + in) * SCALE) below 0.99 * 2^31 (the FAST
+ * range guard) the int32 sum az + r cannot wrap, so (float)(az + (int)r)
+ * = RNE(az + r) = faz + r as one float add: vec_avx.h:804-806,852-854's
+ * cvtps_epi32 / add_epi32 / cvtepi32_ps in two VALU ops fewer.  Scalar
  * float ops only: packed v_pk_add/mul_f32 (explicit or SLP-formed -- this
  * file is built with -fno-slp-vectorize) cost more SIMD issue cycles than
  * the scalar pairs, and waves 0/4 and 1/5 share one SIMD's VALU here
  * (measured: 7,450 -> 7,240 cycles per sample at 1024 streams). */
 template <int S, bool FAST, bool HW, typename Stamp>
 __device__ __forceinline__ void ga_elementwise(float (&st)[S], const float (&e)[S][9], const float *cnd, int tid,
-                                               const int (&az)[S], const int (&ar)[S], const float (&tz)[S],
+                                               const float (&faz)[S], const float (&far)[S], const float (&tz)[S],
                                                const float (&tr)[S], const float (&hpre)[S], const uint32_t *rcp,
                                                unsigned char *xa_i, bool stamping, Stamp &stamp)
 {
@@ -245,11 +252,12 @@ __device__ __forceinline__ void ga_elementwise(float (&st)[S], const float (&e)[
     const float inr = ((cnd[(NA + tid) * S + s] + e[s][1]) + e[s][4]) + e[s][7];
     inh[s] = ((cnd[(2 * NA + tid) * S + s] + e[s][2]) + e[s][5]) + e[s][8];
     if (FAST) {
-      zrv[s] = (float)(az[s] + cvt_rne_fin((tz[s] + inz) * kScale)) * kScale1;
-      zrv[S + s] = (float)(ar[s] + cvt_rne_fin((tr[s] + inr) * kScale)) * kScale1;
+      zrv[s] = (faz[s] + __builtin_rintf((tz[s] + inz) * kScale)) * kScale1;
+      zrv[S + s] = (far[s] + __builtin_rintf((tr[s] + inr) * kScale)) * kScale1;
     } else {
-      zrv[s] = (float)(az[s] + cvt_rne((tz[s] + inz) * kScale)) * kScale1;
-      zrv[S + s] = (float)(ar[s] + cvt_rne((tr[s] + inr) * kScale)) * kScale1;
+      /* x86's INT_MIN for out-of-range / NaN seeds and the wrapping add */
+      zrv[s] = (float)((int)faz[s] + cvt_rne((tz[s] + inz) * kScale)) * kScale1;
+      zrv[S + s] = (float)((int)far[s] + cvt_rne((tr[s] + inr) * kScale)) * kScale1;
     }
     hv[s] = hpre[s];
   }

@@ -246,6 +246,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
      * az/ar, the (subias + diag*state) terms of z and r, and the whole
      * recurrent h-gate value (nnet.c:431-440) */
     int az[S], ar[S], ah[S];
+    float faz[S], far[S]; /* az / ar as exact floats (ga_elementwise) */
     float tz[S], tr[S], hpre[S];
     auto recurrent = [&]() {
       v4i vz[1] = {{wsz, wsz, wsz, wsz}}, vr[1] = {{wsr, wsr, wsr, wsr}}, vh[2] = {{wsh, wsh, wsh, wsh}, {0, 0, 0, 0}};
@@ -309,6 +310,8 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
       for (int s = 0; s < S; s++) {
         az[s] = vz[0][s];
         ar[s] = vr[0][s];
+        faz[s] = (float)vz[0][s];
+        far[s] = (float)vr[0][s];
         ah[s] = vh[0][s] + vh[1][s];
         tz[s] = bz + dz * st[s];
         tr[s] = br + dr * st[s];
@@ -405,7 +408,11 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
                 hadd[s] = *ph;
                 *ph = 0;
               }
-            for (int s = 0; s < S; s++) hpre[s] = (float)(ah[s] + hadd[s]) * kScale1;
+            for (int s = 0; s < S; s++) {
+              hpre[s] = (float)(ah[s] + hadd[s]) * kScale1;
+              faz[s] = (float)az[s];
+              far[s] = (float)ar[s];
+            }
           }
           if (stamping) {
             /* diagnostic only: wait for every gather before the stamp */
@@ -419,9 +426,9 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
           /* compute_sparse_gru elementwise (nnet.c:431-447): one uniform
            * branch per sample into straight-line code for all S streams */
           if (__builtin_amdgcn_readfirstlane((int)fast))
-            ga_elementwise<S, true, kHwA>(st, e, cnd, tid, az, ar, tz, tr, hpre, rcp, xa + i, stamping, stamp);
+            ga_elementwise<S, true, kHwA>(st, e, cnd, tid, faz, far, tz, tr, hpre, rcp, xa + i, stamping, stamp);
           else
-            ga_elementwise<S, false, kHwA>(st, e, cnd, tid, az, ar, tz, tr, hpre, rcp, xa + i, stamping, stamp);
+            ga_elementwise<S, false, kHwA>(st, e, cnd, tid, faz, far, tz, tr, hpre, rcp, xa + i, stamping, stamp);
         }
         stamp(0);
         __syncthreads(); /* Y */
