@@ -492,9 +492,11 @@ static int mf_wave_cost(const std::vector<std::vector<int>> &ga, const int *ub8)
 /* per-SIMD load of six GRU_A wave costs: waves 0/4 and 1/5 pair up; 2 and 3
  * pair with a sampler (its priority chain takes most of their SIMD: measured
  * ~74 cycles per slot there against ~27 per slot of a wave pair) */
+static thread_local int g_mf_simd_weight = MF_SAMPLER_SIMD_WEIGHT; /* set per layout (LPCNET_MF_SIMD_W: tuning hook) */
+
 static int mf_simd_score(const int *c)
 {
-  return std::max(std::max(c[0] + c[4], c[1] + c[5]), (MF_SAMPLER_SIMD_WEIGHT * std::max(c[2], c[3])) / 10);
+  return std::max(std::max(c[0] + c[4], c[1] + c[5]), (g_mf_simd_weight * std::max(c[2], c[3])) / 10);
 }
 
 /* extra[w]: a fixed per-wave cost on top of its own rows (split models: the
@@ -639,7 +641,8 @@ struct MfPlan {
  * and h pieces: every subset that holds them and fits the registers, scored
  * by the per-SIMD load), pieces -> lane groups of the hosting waves.
  * Returns the score (-1: does not fit). */
-static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const int T[3], const int F[3], int iters)
+static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const int T[3], const int F[3], int iters,
+                      int simd_w = MF_SAMPLER_SIMD_WEIGHT)
 {
   constexpr int NUB = NA / 8, NLG = SAMPLE_WAVES * 8;
   P.own[0] = T[0];
@@ -663,6 +666,8 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
   int extra[SAMPLE_WAVES] = {};
   int mz = 0, mh = 0; /* hosting waves (bit masks) */
   long best = -1;
+  if (const char *v = getenv("LPCNET_MF_ITERS")) iters = atoi(v); /* tuning hooks */
+  g_mf_simd_weight = getenv("LPCNET_MF_SIMD_W") ? atoi(getenv("LPCNET_MF_SIMD_W")) : simd_w;
   P.perm = mf_assign_unit_blocks(own, extra, iters);
   for (int round = 0; round < 2; round++) {
     int c[SAMPLE_WAVES], gz[SAMPLE_WAVES], gh[SAMPLE_WAVES];
@@ -745,7 +750,13 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
   return best;
 }
 
-bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P)
+/* S4: the plan of a 4-streams-per-workgroup mf_kernel batch (1024-2047
+ * streams), whose Y -> X half is bound by the GRU_A recurrent product of the
+ * waves sharing a SIMD with a sampler (~3x the cycles per MFMA of a wave
+ * pair at 4 streams): those SIMDs weighted 3.3x and a longer search (same
+ * box, 1024 streams: -1 to -2 % frame step); 2.7x and the short search at
+ * one and two streams per workgroup and for mf2_kernel */
+bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, bool S4 = false)
 {
   constexpr int NUB = NA / 8;
   int kmax[3] = {0, 0, 0};
@@ -755,7 +766,7 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P)
   if (std::max(kmax[0], kmax[1]) <= MF_ZMAX && kmax[2] <= MF_HMAX && !force) {
     P.split = false;
     const int T[3] = {MF_ZMAX, MF_ZMAX, MF_HMAX}, F[3] = {0, 0, 0};
-    return mf_layout(ga, P, T, F, 40000) >= 0;
+    return S4 ? mf_layout(ga, P, T, F, 400000, 33) >= 0 : mf_layout(ga, P, T, F, 40000) >= 0;
   }
   /* split: every own cap / piece size pair, screened with a short
    * assignment search, the best re-laid-out in full (LPCNET_MF_FORCE_SPLIT:
@@ -788,7 +799,7 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P)
           if (!fits || (force && !need)) continue;
           MfPlan C;
           const int T[3] = {Tz, Tz, Th}, F[3] = {Fz, Fz, Fh};
-          const long sc = mf_layout(ga, C, T, F, 1500);
+          const long sc = mf_layout(ga, C, T, F, 1500, S4 ? 33 : MF_SAMPLER_SIMD_WEIGHT);
           if (sc < 0) continue;
           if (best < 0 || sc < best) {
             best = sc;
@@ -797,7 +808,7 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P)
           }
         }
   if (best < 0) return false; /* does not fit even split: the lockstep kernel runs it */
-  return mf_layout(ga, P, bt, bf, 40000) >= 0;
+  return mf_layout(ga, P, bt, bf, 40000, S4 ? 33 : MF_SAMPLER_SIMD_WEIGHT) >= 0;
 }
 
 /* The model constants of a blob (see load_model); -1 on a malformed record
@@ -1099,7 +1110,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   std::vector<uint32_t> mft, mfgb;
   bool mf_ok = int8 && !sat && !getenv("LPCNET_NO_MFMA");
   MfPlan plan;
-  if (mf_ok) mf_ok = mf_plan(ga_blocks, plan);
+  if (mf_ok) mf_ok = mf_plan(ga_blocks, plan, b->B >= 1024 && b->B < MF2_MIN_STREAMS);
   if (getenv("LPCNET_VERBOSE")) {
     fprintf(stderr, "lpcnet: mf_kernel plan: %s", !mf_ok ? "not applicable" : plan.split ? "split" : "unsplit");
     if (mf_ok) {
