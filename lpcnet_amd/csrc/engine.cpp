@@ -750,14 +750,18 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
   return best;
 }
 
-/* S4: the plan of a 4-streams-per-workgroup mf_kernel batch (1024-2047
- * streams), whose Y -> X half is bound by the GRU_A recurrent product of the
- * waves sharing a SIMD with a sampler (~3x the cycles per MFMA of a wave
- * pair at 4 streams): those SIMDs weighted 3.3x and a longer search (same
- * box, 1024 streams: -1 to -2 % frame step); 2.7x and the short search at
- * one and two streams per workgroup and for mf2_kernel */
-bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, bool S4 = false)
+/* cls: the kernel the plan serves.  1: mf_kernel at 4 streams per
+ * workgroup (1024-2047 streams), whose Y -> X half is bound by the GRU_A
+ * recurrent product of the waves sharing a SIMD with a sampler (~3x the
+ * cycles per MFMA of a wave pair): those SIMDs weighted 3.3x and a longer
+ * search (same box, 1024 streams: -0.6 to -1.1 % frame step).  2:
+ * mf2_kernel (from 2048 streams), whose samplers idle half of each phase:
+ * 2.0x (2048 streams -2.1 %, 8192 -0.7 %).  0: 2.7x, one and two streams
+ * per workgroup. */
+bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, int cls = 0)
 {
+  const bool S4 = cls == 1;
+  const int w_unsplit = cls == 1 ? 33 : cls == 2 ? 20 : MF_SAMPLER_SIMD_WEIGHT;
   constexpr int NUB = NA / 8;
   int kmax[3] = {0, 0, 0};
   for (int g = 0; g < 3; g++)
@@ -766,7 +770,7 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, bool S4 = false
   if (std::max(kmax[0], kmax[1]) <= MF_ZMAX && kmax[2] <= MF_HMAX && !force) {
     P.split = false;
     const int T[3] = {MF_ZMAX, MF_ZMAX, MF_HMAX}, F[3] = {0, 0, 0};
-    return S4 ? mf_layout(ga, P, T, F, 400000, 33) >= 0 : mf_layout(ga, P, T, F, 40000) >= 0;
+    return mf_layout(ga, P, T, F, S4 ? 400000 : 40000, w_unsplit) >= 0;
   }
   /* split: every own cap / piece size pair, screened with a short
    * assignment search, the best re-laid-out in full (LPCNET_MF_FORCE_SPLIT:
@@ -1110,7 +1114,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   std::vector<uint32_t> mft, mfgb;
   bool mf_ok = int8 && !sat && !getenv("LPCNET_NO_MFMA");
   MfPlan plan;
-  if (mf_ok) mf_ok = mf_plan(ga_blocks, plan, b->B >= 1024 && b->B < MF2_MIN_STREAMS);
+  if (mf_ok) mf_ok = mf_plan(ga_blocks, plan, b->B >= MF2_MIN_STREAMS ? 2 : b->B >= 1024 ? 1 : 0);
   if (getenv("LPCNET_VERBOSE")) {
     fprintf(stderr, "lpcnet: mf_kernel plan: %s", !mf_ok ? "not applicable" : plan.split ? "split" : "unsplit");
     if (mf_ok) {
