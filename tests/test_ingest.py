@@ -207,3 +207,88 @@ def test_reordered_blob_loads_on_device_same_pcm(require_gpu, blob):
     b = L.LPCNetBatch(len(G["streams"]), 0, good)
     for fr in range(6):
         assert np.array_equal(b.synthesize(G["features"][:, fr, :20]), G["pcm"][:, fr]), fr
+
+
+def _fuzz_cases(blob, n, seed):
+    """Seeded random corruptions of the blob's structure: header fields
+    (size, block size, type, name bytes), idx words, truncations at any
+    offset, record drops and duplications."""
+    rng = np.random.default_rng(seed)
+    for _ in range(n):
+        recs = records(blob)
+        kind = int(rng.integers(0, 6))
+        r = recs[int(rng.integers(0, len(recs)))]
+        if kind == 0:  # size / block-size fields
+            field = 12 + 4 * int(rng.integers(0, 2))
+            v = struct.unpack_from("<i", r[1], field)[0]
+            struct.pack_into("<i", r[1], field, int(v + rng.choice([-64, -32, -4, -1, 1, 4, 32, 64, 1 << 20, -(1 << 30)])))
+            out = join(recs)
+        elif kind == 1:  # name / type bytes
+            pos = int(rng.choice([4, 8, 20 + int(rng.integers(0, 44))]))
+            r[1][pos] ^= int(rng.integers(1, 256))
+            out = join(recs)
+        elif kind == 2:  # an idx word
+            idx = [q for q in recs if q[0].endswith("_idx")]
+            q = idx[int(rng.integers(0, len(idx)))]
+            w = idx_words(q)
+            w[int(rng.integers(0, len(w)))] += int(rng.choice([-8, -4, -1, 1, 4, 8, 400, -400]))
+            put_idx(q, w)
+            out = join(recs)
+        elif kind == 3:  # truncation anywhere
+            out = join(recs)[:int(rng.integers(0, len(blob)))]
+        elif kind == 4:  # a record dropped
+            recs.remove(r)
+            out = join(recs)
+        else:  # a record duplicated in front (find_array_entry takes the first)
+            dup = [r[0], bytearray(r[1]), bytearray(r[2])]
+            set_size(dup, size=max(0, struct.unpack_from("<i", dup[1], 12)[0] - 4))
+            recs.insert(0, dup)
+            out = join(recs)
+        yield kind, out
+
+
+@pytest.mark.parametrize("variant", ["int8", "fp32"])
+def test_fuzzed_blobs_engine_and_oracle_agree(variant):
+    """200 seeded random corruptions per variant: the engine's loader never
+    crashes, and it accepts exactly the blobs the CPU oracle (the reference's
+    parse rules restated) accepts."""
+    base = L.synthetic_model(1, L.VARIANT_INT8 if variant == "int8" else L.VARIANT_FP32)
+    seen = {"accepted": 0, "rejected": 0}
+    for k, (kind, b) in enumerate(_fuzz_cases(base, 200, 7 if variant == "int8" else 8)):
+        try:
+            L.validate_model(b)
+            eng = True
+        except L.LPCNetError:
+            eng = False
+        try:
+            O.Oracle(b, 0 if variant == "int8" else 1)
+            orc = True
+        except ValueError:
+            orc = False
+        assert eng == orc, (k, kind, eng, orc)
+        seen["accepted" if eng else "rejected"] += 1
+    assert seen["rejected"] > 50 and seen["accepted"] > 0, seen
+
+
+def test_fuzzed_accepted_blobs_same_pcm_as_oracle(require_gpu):
+    """The corrupted blobs both loaders accept (header versions, names of
+    records synthesis does not bind, duplicates, ...) synthesise on the GPU
+    exactly what the oracle synthesises from them."""
+    base = L.synthetic_model(1, L.VARIANT_INT8)
+    feats = L.synthetic_features(3, 4)[:, :20]
+    done = 0
+    for kind, b in _fuzz_cases(base, 200, 7):
+        try:
+            L.validate_model(b)
+        except L.LPCNetError:
+            continue
+        o = O.Oracle(b, 0)
+        exp = np.stack([o.synthesize(feats[f]) for f in range(4)])
+        bt = L.LPCNetBatch(1, 0, b)
+        got = np.stack([bt.synthesize(feats[f][None, :])[0] for f in range(4)])
+        bt.close()
+        assert np.array_equal(got, exp), kind
+        done += 1
+        if done == 6:
+            break
+    assert done > 0
