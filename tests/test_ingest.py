@@ -270,6 +270,7 @@ def test_fuzzed_blobs_engine_and_oracle_agree(variant):
     assert seen["rejected"] > 50 and seen["accepted"] > 0, seen
 
 
+@pytest.mark.gpu
 def test_fuzzed_accepted_blobs_same_pcm_as_oracle(require_gpu):
     """The corrupted blobs both loaders accept (header versions, names of
     records synthesis does not bind, duplicates, ...) synthesise on the GPU
