@@ -1113,6 +1113,15 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
   /* ---- matrix-core tables (non-saturating int8 models, mf_kernel) ---- */
   std::vector<uint32_t> mft, mfgb;
   bool mf_ok = int8 && !sat && !getenv("LPCNET_NO_MFMA");
+  /* the matrix-core GRU_B is a dense tile: a row block listing one block
+   * position twice (find_idx_check accepts it, and sparse_sgemv_accum8x4
+   * adds both blocks) has no dense form -- the lockstep kernel runs such a
+   * model, block by block as the reference does */
+  for (int rb = 0; rb < GB_ROWS / 8 && mf_ok; rb++) {
+    std::vector<int> pos = gb_blocks[rb];
+    std::sort(pos.begin(), pos.end());
+    if (std::adjacent_find(pos.begin(), pos.end()) != pos.end()) mf_ok = false;
+  }
   MfPlan plan;
   if (mf_ok) mf_ok = mf_plan(ga_blocks, plan, b->B >= MF2_MIN_STREAMS ? 2 : b->B >= 1024 ? 1 : 0);
   if (getenv("LPCNET_VERBOSE")) {

@@ -293,3 +293,37 @@ def test_fuzzed_accepted_blobs_same_pcm_as_oracle(require_gpu):
         if done == 6:
             break
     assert done > 0
+
+
+def _dup_position(w):
+    """a row block listing one block position twice (the reference's
+    find_idx_check accepts it; sparse_sgemv_accum8x4 adds both blocks)"""
+    w = w.copy()
+    p = 0
+    while w[p] < 2:
+        p += w[p] + 1
+    w[p + 2] = w[p + 1]
+    return w
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["int8", "fp32"])
+@pytest.mark.parametrize("idx", ["sparse_gru_a_recurrent_weights_idx", "gru_b_weights_idx"])
+@pytest.mark.parametrize("B", [1, 3])
+def test_duplicate_block_positions_match_oracle(require_gpu, variant, idx, B):
+    """Duplicate block positions in a row block, on whichever kernel the
+    engine picks for such a model (GRU_B: the lockstep kernel, whose blocks
+    are summed one by one; GRU_A: the fast kernels' slots): PCM identical to
+    the oracle."""
+    v = L.VARIANT_INT8 if variant == "int8" else L.VARIANT_FP32
+    b = mutated(L.synthetic_model(1, v), _mut_idx(idx, _dup_position))
+    L.validate_model(b)
+    F = 5
+    feats = np.stack([L.synthetic_features(s, F)[:, :20] for s in range(B)], 1)
+    bt = L.LPCNetBatch(B, 0, b)
+    got = np.stack([bt.synthesize(feats[f]) for f in range(F)], 1)
+    bt.close()
+    for s in range(B):
+        o = O.Oracle(b, 0 if variant == "int8" else 1)
+        exp = np.stack([o.synthesize(feats[f, s]) for f in range(F)])
+        assert np.array_equal(got[s], exp), s
