@@ -327,3 +327,23 @@ def test_duplicate_block_positions_match_oracle(require_gpu, variant, idx, B):
         o = O.Oracle(b, 0 if variant == "int8" else 1)
         exp = np.stack([o.synthesize(feats[f, s]) for f in range(F)])
         assert np.array_equal(got[s], exp), s
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [600, 1024, 2048])
+def test_duplicate_gru_a_positions_wide_batches_match_oracle(require_gpu, B):
+    """A duplicated GRU_A recurrent block position on the 2- and 4-stream
+    mf_kernel forms and on mf2_kernel: sampled streams identical to the
+    oracle (the register tables add the block twice, as the reference)."""
+    b = mutated(L.synthetic_model(1, L.VARIANT_INT8), _mut_idx("sparse_gru_a_recurrent_weights_idx", _dup_position))
+    F = 4
+    feats = np.stack([L.synthetic_features(s, F)[:, :20] for s in range(B)], 1)
+    bt = L.LPCNetBatch(B, 0, b)
+    got = np.stack([bt.synthesize(feats[f]) for f in range(F)], 1)
+    name = bt.info().kernel_name
+    bt.close()
+    assert "mf" in name, name
+    for s in (0, B // 2 + 1, B - 1):
+        o = O.Oracle(b, 0)
+        exp = np.stack([o.synthesize(feats[f, s]) for f in range(F)])
+        assert np.array_equal(got[s], exp), (name, s)
