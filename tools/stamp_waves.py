@@ -1,5 +1,5 @@
 """Per-wave mean s_memtime phase stamps of one stamped frame (diagnostic):
-python tools/stamp_waves.py B [model]  -> one row per wave, slots 0..15
+python tools/stamp_waves.py B [default|skewed]  -> one row per wave, slots 0..15
 (cycles per sample; slot meanings: mf_kernel.hip stamp() calls)."""
 import os, sys
 import numpy as np
@@ -7,7 +7,7 @@ sys.path.insert(0, os.getcwd())
 import lpcnet_amd as L
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-blob = L.synthetic_model(1, 0)
+blob = L.synthetic_model(1, 0, skewed=len(sys.argv) > 2 and sys.argv[2] == "skewed")
 b = L.LPCNetBatch(B, 0, blob)
 F = 4
 allf = np.stack([L.synthetic_features(s, F)[:, :20] for s in range(B)], 1)
