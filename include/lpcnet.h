@@ -35,8 +35,23 @@ extern "C" {
 #define NB_FEATURES 20        /* include/lpcnet.h:45 */
 #define NB_TOTAL_FEATURES 36  /* include/lpcnet.h:46 */
 #define LPCNET_FRAME_SIZE (160) /* include/lpcnet.h:53 */
+#define LPCNET_COMPRESSED_SIZE 8             /* include/lpcnet.h:49 */
+#define LPCNET_PACKET_SAMPLES (4 * 160)      /* include/lpcnet.h:51 */
 
 typedef struct LPCNetState LPCNetState;
+typedef struct LPCNetDecState LPCNetDecState;
+
+/* include/lpcnet.h:63-100 -- the 1.6 kb/s decoder.  lpcnet_decode decodes one
+ * LPCNET_COMPRESSED_SIZE-byte packet into LPCNET_PACKET_SAMPLES samples
+ * (src/lpcnet.c:310-319).  This library has no compiled-in model or
+ * codebooks: bind a blob that carries them with
+ * lpcnet_mi355x_decoder_load_model (include/lpcnet_mi355x.h) first;
+ * lpcnet_decode returns -1 (and outputs silence) without one. */
+LPCNET_EXPORT int lpcnet_decoder_get_size(void);
+LPCNET_EXPORT int lpcnet_decoder_init(LPCNetDecState *st);
+LPCNET_EXPORT LPCNetDecState *lpcnet_decoder_create(void);
+LPCNET_EXPORT void lpcnet_decoder_destroy(LPCNetDecState *st);
+LPCNET_EXPORT int lpcnet_decode(LPCNetDecState *st, const unsigned char *buf, short *pcm);
 
 /* include/lpcnet.h:156-160 -- size of an LPCNetState (caller allocation). */
 LPCNET_EXPORT int lpcnet_get_size(void);

@@ -52,6 +52,9 @@ typedef struct {
    * Sparsify masks): mf_kernel runs its split form, fp_kernel its streamed
    * (long) form */
   int long_rows;
+  /* 1: the blob carries the 1.6 kb/s decoder's codebooks (ceps_codebook1..3,
+   * ceps_codebook_diff4), so lpcnet_decode / lpcnet_batch_decode* accept it */
+  int has_codebooks;
 } LPCNetModelInfo;
 
 /* Create a batch of nb_streams streams on HIP device `device`.
@@ -99,6 +102,36 @@ LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features,
  * from pcm (input), exactly as lpcnet.c:256-259; pcm[s][preload..N) is output.
  * N == 0 runs only the frame network (run_frame_network_flush, lpcnet.c:134). */
 LPCNET_EXPORT int lpcnet_batch_synthesize_impl(LPCNetBatch *b, const float *features, short *pcm, int N, int preload);
+
+/* lpcnet_synthesize_tail_impl (src/lpcnet.c:235-271, declared at
+ * lpcnet_private.h:131): N samples of every stream from the conditioning and
+ * LPC already in its state (no frame network); the first `preload` samples
+ * teacher-forced from pcm as above. */
+LPCNET_EXPORT int lpcnet_batch_synthesize_tail_impl(LPCNetBatch *b, short *pcm, int N, int preload);
+
+/* run_frame_network (src/lpcnet.c:82-120) of one frame per stream, no samples.
+ * update_conditions = 1: into the state's conditioning and LPC, as
+ * lpcnet_synthesize_impl(..., N = 0) does; 0: into locals, as
+ * run_frame_network_flush does (lpcnet.c:134-144) -- conv memories, the
+ * lpc_from_cepstrum ring and frame_count advance, the conditioning and LPC
+ * the next tail_impl reads stay. */
+LPCNET_EXPORT int lpcnet_batch_run_frame_network(LPCNetBatch *b, const float *features, int update_conditions);
+
+/* lpcnet_reset_signal (src/lpcnet.c:226-233) on one stream. */
+LPCNET_EXPORT int lpcnet_batch_reset_signal(LPCNetBatch *b, int stream);
+
+/* 1.6 kb/s decoder (lpcnet_decode, src/lpcnet.c:310-319): one 8-byte packet
+ * per stream (decode_packet, lpcnet_dec.c:81-156, on the device) -> 4 frames
+ * synthesised.  Needs a model blob with the codebook records
+ * (LPCNetModelInfo.has_codebooks).  Each stream's vq_mem is part of its state
+ * (reset to zero by lpcnet_batch_reset / _reset_stream, as
+ * lpcnet_decoder_init does; saved and restored with it).
+ * Host I/O: packets [B][8] -> pcm [B][4 * 160]. */
+LPCNET_EXPORT int lpcnet_batch_decode(LPCNetBatch *b, const unsigned char *packets, short *pcm);
+/* Device-resident: d_packets [npackets][B][8] -> d_pcm [4 npackets][B][160]
+ * (the frames-major layout of lpcnet_batch_synthesize_frames); the decoded
+ * features stay in device memory.  Enqueued; lpcnet_batch_sync waits. */
+LPCNET_EXPORT int lpcnet_batch_decode_frames(LPCNetBatch *b, const unsigned char *d_packets, short *d_pcm, int npackets);
 
 /* Snapshot / restore of one stream's complete synthesis state (the struct
  * copies lpcnet_plc.c:223,230 make for speculation).  buf holds
@@ -180,7 +213,9 @@ LPCNET_EXPORT int lpcnet_batch_get_state(LPCNetBatch *b, int stream, float *gru_
  * flags: bit0 = make some int8 pairs able to saturate maddubs; bit1 = GRU_A
  * block masks chosen as training_tf2/lpcnet.py:140-160 (Sparsify) does --
  * a global per-gate energy threshold -- over skewed row energies, so block
- * rows run far above the mean length, as in trained models.
+ * rows run far above the mean length, as in trained models; bit2 = append
+ * synthetic 1.6 kb/s decoder codebooks (ceps_codebook1..3 [1024][17],
+ * ceps_codebook_diff4 [4096][18]; the other arrays are unchanged).
  * Returns the blob size; writes it if buf != NULL and cap is large enough. */
 LPCNET_EXPORT int lpcnet_mi355x_synthetic_model(unsigned seed, int variant, int flags, unsigned char *buf, int cap);
 /* Synthetic feature frames (NB_TOTAL_FEATURES floats each) for stream `stream`. */
@@ -233,6 +268,33 @@ LPCNET_EXPORT int lpcnet_mi355x_device_count(void);
  * the pool `st` belongs to: coalesced launches, handled requests, handles
  * bound.  -1 if st is not bound. */
 LPCNET_EXPORT int lpcnet_mi355x_pool_stats(const LPCNetState *st, long *launches, long *requests, int *streams);
+/* ---- reference-internal entry points on a drop-in handle ----------------
+ * The reference's PLC (lpcnet_plc.c:188-337) drives one LPCNetState through
+ * these functions of lpcnet_private.h:126-132; they are exported here under
+ * the same names and signatures so that code links against this library
+ * unchanged, except for its LPCNetState struct copies (lpcnet_plc.c:223,230),
+ * which become lpcnet_mi355x_state_save / _restore. */
+LPCNET_EXPORT void lpcnet_synthesize_impl(LPCNetState *st, const float *features, short *output, int N, int preload);
+LPCNET_EXPORT void lpcnet_synthesize_tail_impl(LPCNetState *st, short *output, int N, int preload);
+LPCNET_EXPORT void run_frame_network_deferred(LPCNetState *st, const float *features);
+LPCNET_EXPORT void run_frame_network_flush(LPCNetState *st);
+LPCNET_EXPORT void lpcnet_reset_signal(LPCNetState *st);
+/* A handle's whole synthesis state (device stream state + the deferred
+ * feature buffer): buf holds lpcnet_mi355x_state_size() bytes.  Restore
+ * refuses a buffer this engine cannot have produced.  0 / -1. */
+LPCNET_EXPORT int lpcnet_mi355x_state_size(void);
+LPCNET_EXPORT int lpcnet_mi355x_state_save(LPCNetState *st, void *buf);
+LPCNET_EXPORT int lpcnet_mi355x_state_restore(LPCNetState *st, const void *buf);
+/* Release what lpcnet_init bound to st without freeing st: for an
+ * LPCNetState embedded in a caller's struct (as lpcnet_plc.c:63 / lpcnet.c:293
+ * embed theirs) that the caller frees itself.  Memory freed without it is
+ * detected as stale by the next lpcnet_init at that address. */
+LPCNET_EXPORT void lpcnet_mi355x_deinit(LPCNetState *st);
+/* Bind a model to a decoder (the reference binds its compiled-in model and
+ * codebooks in lpcnet_decoder_init; this library has none).  -1 if the blob
+ * is rejected or carries no codebooks. */
+LPCNET_EXPORT int lpcnet_mi355x_decoder_load_model(LPCNetDecState *st, const unsigned char *data, int len);
+
 /* Last error string of this thread. */
 LPCNET_EXPORT const char *lpcnet_mi355x_last_error(void);
 

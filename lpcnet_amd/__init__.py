@@ -94,6 +94,28 @@ def _load():
         "lpcnet_mi355x_device_count": (i, []),
         "lpcnet_mi355x_device_numerics": (i, [i, i, vp, vp, i]),
         "lpcnet_mi355x_last_error": (C.c_char_p, []),
+        # reference-internal entry points on a handle (lpcnet_private.h:126-132)
+        "lpcnet_synthesize_impl": (None, [vp, vp, vp, i, i]),
+        "lpcnet_synthesize_tail_impl": (None, [vp, vp, i, i]),
+        "run_frame_network_deferred": (None, [vp, vp]),
+        "run_frame_network_flush": (None, [vp]),
+        "lpcnet_reset_signal": (None, [vp]),
+        "lpcnet_mi355x_state_size": (i, []),
+        "lpcnet_mi355x_state_save": (i, [vp, vp]),
+        "lpcnet_mi355x_state_restore": (i, [vp, vp]),
+        "lpcnet_mi355x_deinit": (None, [vp]),
+        # 1.6 kb/s decoder (include/lpcnet.h:63-100)
+        "lpcnet_decoder_get_size": (i, []),
+        "lpcnet_decoder_init": (i, [vp]),
+        "lpcnet_decoder_create": (vp, []),
+        "lpcnet_decoder_destroy": (None, [vp]),
+        "lpcnet_decode": (i, [vp, vp, vp]),
+        "lpcnet_mi355x_decoder_load_model": (i, [vp, C.c_char_p, i]),
+        "lpcnet_batch_synthesize_tail_impl": (i, [vp, vp, i, i]),
+        "lpcnet_batch_run_frame_network": (i, [vp, vp, i]),
+        "lpcnet_batch_reset_signal": (i, [vp, i]),
+        "lpcnet_batch_decode": (i, [vp, vp, vp]),
+        "lpcnet_batch_decode_frames": (i, [vp, vp, vp, i]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -112,7 +134,7 @@ class ModelInfo(C.Structure):
                 ("ops_per_sample", C.c_double), ("streams_per_workgroup", C.c_int), ("quad_path", C.c_int),
                 ("lds_bytes", C.c_int), ("mfma_ops_per_group_sample", C.c_double),
                 ("lpc_gamma", C.c_float), ("features_delay", C.c_int), ("end2end", C.c_int),
-                ("long_rows", C.c_int)]
+                ("long_rows", C.c_int), ("has_codebooks", C.c_int)]
 
     @property
     def kernel_name(self) -> str:
@@ -155,11 +177,13 @@ def device_count() -> int:
     return lib.lpcnet_mi355x_device_count()
 
 
-def synthetic_model(seed: int = 1, variant: int = VARIANT_INT8, saturating: bool = False, skewed: bool = False) -> bytes:
+def synthetic_model(seed: int = 1, variant: int = VARIANT_INT8, saturating: bool = False, skewed: bool = False,
+                    codebooks: bool = False) -> bytes:
     """Deterministic synthetic default-size model in the reference blob format.
     skewed: GRU_A masks by a global per-gate threshold over skewed block
-    energies (Sparsify, training_tf2/lpcnet.py:140-160): long block rows."""
-    flags = (1 if saturating else 0) | (2 if skewed else 0)
+    energies (Sparsify, training_tf2/lpcnet.py:140-160): long block rows.
+    codebooks: append the 1.6 kb/s decoder's ceps codebooks (other arrays unchanged)."""
+    flags = (1 if saturating else 0) | (2 if skewed else 0) | (4 if codebooks else 0)
     n = lib.lpcnet_mi355x_synthetic_model(seed, variant, flags, None, 0)
     buf = C.create_string_buffer(n)
     lib.lpcnet_mi355x_synthetic_model(seed, variant, flags, buf, n)
@@ -240,9 +264,81 @@ class LPCNet:
         lib.lpcnet_synthesize(self._st, f.ctypes.data, out.ctypes.data, n)
         return out
 
+    # -- reference-internal entry points (lpcnet_private.h:126-132, the PLC's calls) --
+    def synthesize_impl(self, features: np.ndarray, pcm: np.ndarray, preload: int) -> np.ndarray:
+        """lpcnet_synthesize_impl: pcm [N] int16, the first ``preload`` samples teacher-forced."""
+        f = np.ascontiguousarray(np.asarray(features, np.float32)[:NB_FEATURES])
+        out = np.ascontiguousarray(pcm, np.int16).copy()
+        lib.lpcnet_synthesize_impl(self._st, f.ctypes.data, out.ctypes.data if out.size else None, out.size, preload)
+        return out
+
+    def synthesize_tail_impl(self, pcm: np.ndarray, preload: int = 0) -> np.ndarray:
+        """lpcnet_synthesize_tail_impl: the sample network only, on the current conditioning."""
+        out = np.ascontiguousarray(pcm, np.int16).copy()
+        lib.lpcnet_synthesize_tail_impl(self._st, out.ctypes.data if out.size else None, out.size, preload)
+        return out
+
+    def frame_deferred(self, features: np.ndarray) -> None:
+        """run_frame_network_deferred (lpcnet.c:122-132)."""
+        f = np.ascontiguousarray(np.asarray(features, np.float32)[:NB_FEATURES])
+        lib.run_frame_network_deferred(self._st, f.ctypes.data)
+
+    def frame_flush(self) -> None:
+        """run_frame_network_flush (lpcnet.c:134-144)."""
+        lib.run_frame_network_flush(self._st)
+
+    def reset_signal(self) -> None:
+        """lpcnet_reset_signal (lpcnet.c:226-233)."""
+        lib.lpcnet_reset_signal(self._st)
+
+    def save(self) -> bytes:
+        """The handle's whole synthesis state (replaces the PLC's LPCNetState struct copy)."""
+        buf = C.create_string_buffer(lib.lpcnet_mi355x_state_size())
+        if lib.lpcnet_mi355x_state_save(self._st, buf) != 0:
+            raise LPCNetError(last_error())
+        return buf.raw
+
+    def restore(self, state: bytes) -> None:
+        if lib.lpcnet_mi355x_state_restore(self._st, state) != 0:
+            raise LPCNetError(last_error())
+
     def close(self) -> None:
         if self._st:
             lib.lpcnet_destroy(self._st)
+            self._st = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class LPCNetDecoder:
+    """The 1.6 kb/s decoder: lpcnet_decoder_create / lpcnet_decode (lpcnet.c:283-319)."""
+
+    def __init__(self, blob: bytes):
+        self._st = lib.lpcnet_decoder_create()
+        if not self._st:
+            raise LPCNetError("lpcnet_decoder_create failed")
+        if lib.lpcnet_mi355x_decoder_load_model(self._st, blob, len(blob)) != 0:
+            err = last_error()
+            self.close()
+            raise LPCNetError(f"decoder model: {err}")
+
+    def decode(self, packet: bytes) -> np.ndarray:
+        """One 8-byte packet -> 640 int16 samples."""
+        if len(packet) != 8:
+            raise ValueError("a packet is 8 bytes")
+        buf = C.create_string_buffer(bytes(packet), 8)
+        out = np.zeros(4 * FRAME_SIZE, np.int16)
+        if lib.lpcnet_decode(self._st, buf, out.ctypes.data) != 0:
+            raise LPCNetError(last_error())
+        return out
+
+    def close(self) -> None:
+        if self._st:
+            lib.lpcnet_decoder_destroy(self._st)
             self._st = None
 
     def __del__(self):
@@ -283,6 +379,9 @@ class LPCNetBatch:
         """Same-box parity: the rcpps table of the device activations (4096
         entries, see host_rcp_table; None = the default Intel table)."""
         t = None if table is None else np.ascontiguousarray(table, np.uint32)
+        if t is not None and t.size != 4096:
+            raise ValueError("rcpps table must have 4096 entries (top 12 mantissa bits, see host_rcp_table); "
+                             f"got {t.size}")
         if lib.lpcnet_batch_set_rcp_table(self._b, None if t is None else t.ctypes.data) != 0:
             raise LPCNetError(last_error())
 
@@ -330,6 +429,38 @@ class LPCNetBatch:
         """run_frame_network without samples (lpcnet.c:134 run_frame_network_flush)."""
         f = np.ascontiguousarray(np.asarray(features, np.float32)[:, :NB_FEATURES])
         if lib.lpcnet_batch_synthesize_impl(self._b, f.ctypes.data, None, 0, 0) != 0:
+            raise LPCNetError(last_error())
+
+    def synthesize_tail_impl(self, pcm: np.ndarray, preload: int = 0) -> np.ndarray:
+        """lpcnet_synthesize_tail_impl on every stream: pcm [B, N] (first ``preload`` teacher-forced)."""
+        out = np.ascontiguousarray(pcm, np.int16).copy()
+        n = out.shape[1]
+        if lib.lpcnet_batch_synthesize_tail_impl(self._b, out.ctypes.data if n else None, n, preload) != 0:
+            raise LPCNetError(last_error())
+        return out
+
+    def run_frame_network(self, features: np.ndarray, update_conditions: bool) -> None:
+        """run_frame_network of one frame per stream; update_conditions False = flush semantics."""
+        f = np.ascontiguousarray(np.asarray(features, np.float32)[:, :NB_FEATURES])
+        if lib.lpcnet_batch_run_frame_network(self._b, f.ctypes.data, 1 if update_conditions else 0) != 0:
+            raise LPCNetError(last_error())
+
+    def reset_signal(self, stream: int) -> None:
+        if lib.lpcnet_batch_reset_signal(self._b, stream) != 0:
+            raise LPCNetError(last_error())
+
+    def decode(self, packets: np.ndarray) -> np.ndarray:
+        """lpcnet_decode on every stream: packets [B, 8] uint8 -> pcm [B, 640]."""
+        pk = np.ascontiguousarray(packets, np.uint8)
+        assert pk.shape == (self.B, 8)
+        out = np.zeros((self.B, 4 * FRAME_SIZE), np.int16)
+        if lib.lpcnet_batch_decode(self._b, pk.ctypes.data, out.ctypes.data) != 0:
+            raise LPCNetError(last_error())
+        return out
+
+    def decode_frames(self, d_packets: int, d_pcm: int, npackets: int) -> None:
+        """Enqueue device packets [npackets, B, 8] -> device pcm [4 npackets, B, 160]."""
+        if lib.lpcnet_batch_decode_frames(self._b, d_packets, d_pcm, npackets) != 0:
             raise LPCNetError(last_error())
 
     def save_state(self, stream: int) -> bytes:

@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <cmath>
@@ -30,6 +31,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "lpcnet_engine.h"
@@ -353,6 +355,14 @@ struct LPCNetBatch {
   int *h_status = nullptr;
   int *d_status = nullptr;
   int spin_limit = FLAG_SPIN_LIMIT_DEFAULT;
+  /* 1.6 kb/s decoder (decode_kernel.hip): the model's ceps codebooks (optional
+   * blob records), packets and decoded features of up to DEC_MAX_PACKETS
+   * packets per stream, the host-I/O path's 4-frame PCM */
+  DecodeArgs da{};
+  bool has_codebooks = false;
+  unsigned char *d_packets = nullptr;
+  float *d_dfeat = nullptr;
+  short *d_dpcm = nullptr;
   /* diagnostics */
   unsigned long long *d_stamps = nullptr;
   /* timing */
@@ -891,6 +901,15 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
    * LPCNET_FEATURES_DELAY / LPCNET_END2END override both (drop-in callers) */
   ModelConst mc{1.0f, DEFAULT_FEATURES_DELAY, 0};
   if (model_constants(L, mc)) return -1;
+  /* the 1.6 kb/s decoder's codebooks (lpcnet_private.h:109-112, generated
+   * ceps_codebooks.c in the reference; lpcnet_enc.c:109-119, 709 give their
+   * sizes): optional records -- a blob without them (or with mis-sized ones,
+   * which the reference's parser would never bind either) still synthesises,
+   * only lpcnet_decode refuses it */
+  const Arr *cb[4] = {find(L, "ceps_codebook1"), find(L, "ceps_codebook2"), find(L, "ceps_codebook3"),
+                      find(L, "ceps_codebook_diff4")};
+  bool cb_ok = true;
+  for (int k = 0; k < 4; k++) cb_ok &= cb[k] && cb[k]->size == (k < 3 ? 1024 * (NBANDS - 1) : 4096 * NBANDS) * 4;
   const void *gbw = find_check(L, "gru_b_weights", 32 * nbb * q);
 
   const void *gbrec = find_check(L, "gru_b_recurrent_weights", 3 * NB * NB * q);
@@ -1507,7 +1526,20 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     UP(sa.ga_wf, ga_wf.data(), ga_wf.size() * sizeof(float4));
     UP(sa.gb_recf, gbrec, 3 * NB * NB * 4);
   }
+  DecodeArgs da{};
+  if (cb_ok) {
+    /* lpcnet_dec.c:118: float p = pow(2.f, main_pitch/21.)*PITCH_MIN_PERIOD, per 6-bit main_pitch */
+    std::vector<float> pt(64);
+    for (int m = 0; m < 64; m++) pt[m] = (float)(pow(2.0, m / 21.) * 32);
+    UP(da.cb1, cb[0]->data, cb[0]->size);
+    UP(da.cb2, cb[1]->data, cb[1]->size);
+    UP(da.cb3, cb[2]->data, cb[2]->size);
+    UP(da.cbd, cb[3]->data, cb[3]->size);
+    UP(da.pitch, pt.data(), pt.size() * 4);
+  }
 #undef UP
+  b->da = da;
+  b->has_codebooks = cb_ok;
   sa.image_bytes = (int)img.size();
   sa.image_lds_bytes = image_lds;
   b->sa = sa;
@@ -1557,6 +1589,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     b->mf_gb_ops = 2.0 * 2.0 * MF_GB_TILES * 16384.0;
   }
   in.long_rows = (mf_ok && sa.mf_split) || (fp_ok && sa.fp_long) ? 1 : 0;
+  in.has_codebooks = cb_ok ? 1 : 0;
   in.lpc_gamma = mc.lpc_gamma;
   in.features_delay = mc.delay;
   in.end2end = mc.end2end;
@@ -1604,8 +1637,11 @@ int ensure_trace(LPCNetBatch *b, int N)
  * computed earlier on the same queue (lpcnet_batch_synthesize_frames
  * batches it over many frames). */
 int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_frame, bool run_lpc, short *d_pcm, int N,
-                      int preload = 0, int ovl = -1, int nB = -1)
+                      int preload = 0, int ovl = -1, int nB = -1, bool run_frame = true, bool keep_cond = false)
 {
+  /* run_frame false: the sample network only, on the conditioning already in
+   * the stream states (lpcnet_synthesize_tail_impl, lpcnet.c:235-271);
+   * keep_cond: the frame network of run_frame_network_flush (lpcnet.c:134-144) */
   /* nB: run the first nB streams of the batch only (the drop-in pool's work
    * batch); the overlapped form always runs all of them */
   if (nB < 0 || ovl >= 0) nB = b->B;
@@ -1617,6 +1653,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
   fa.nstreams = nB;
   fa.features = d_features;
   fa.lpc_new = d_lpc_frame;
+  fa.keep_cond = keep_cond ? 1 : 0;
   SampleArgs sa = b->sa;
   sa.st = b->d_state;
   sa.delay = b->mc.delay;
@@ -1644,11 +1681,11 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
   if (e[0]) HIPCHK(hipEventRecord(e[0], fs));
   /* lpc_from_cepstrum of this frame's features: the frame kernel pushes it
    * into the two-frame LPC ring (lpcnet.c:110-112) */
-  if (run_lpc && !b->mc.end2end && launch_lpc(d_features, d_lpc_frame, nB, b->d_lpc_tab, fs)) {
+  if (run_frame && run_lpc && !b->mc.end2end && launch_lpc(d_features, d_lpc_frame, nB, b->d_lpc_tab, fs)) {
     set_err("lpc kernel launch failed");
     return -1;
   }
-  if (launch_frame(fa, fs)) { set_err("frame kernel launch failed"); return -1; }
+  if (run_frame && launch_frame(fa, fs)) { set_err("frame kernel launch failed"); return -1; }
   if (ovl >= 0 && launch_cond_copy(b->d_state, b->d_cond[c], b->B, fs)) {
     set_err("copy launch failed");
     return -1;
@@ -1698,7 +1735,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
     b->ev_pairs[0].push_back(e[2]);
     b->ev_frames[0].push_back(1);
   }
-  b->frames_done(1);
+  if (run_frame) b->frames_done(1);
   for (hipEvent_t x : e)
     if (x) b->ev_taken.push_back(x);
   return 0;
@@ -1903,6 +1940,9 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
   (void)hipFree(b->d_lpc);
   (void)hipFree(b->d_lpc_tab);
   (void)hipFree(b->d_chunk);
+  (void)hipFree(b->d_packets);
+  (void)hipFree(b->d_dfeat);
+  (void)hipFree(b->d_dpcm);
   for (int i = 0; i < 2; i++) {
     (void)hipFree(b->d_cond[i]);
     if (b->ev_frame[i]) (void)hipEventDestroy(b->ev_frame[i]);
@@ -2029,6 +2069,144 @@ LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features,
   return lpcnet_batch_synthesize_impl(b, features, pcm, N, 0);
 }
 
+static int ensure_decode_bufs(LPCNetBatch *b, bool host_io)
+{
+  if (!b->d_packets) HIPCHK(hipMalloc(&b->d_packets, (size_t)DEC_MAX_PACKETS * b->B * 8));
+  if (!b->d_dfeat) HIPCHK(hipMalloc(&b->d_dfeat, sizeof(float) * NF * 4 * DEC_MAX_PACKETS * (size_t)b->B));
+  if (host_io && !b->d_dpcm) HIPCHK(hipMalloc(&b->d_dpcm, sizeof(short) * 4 * FRAME * (size_t)b->B));
+  return 0;
+}
+
+static int decode_ready(LPCNetBatch *b)
+{
+  if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
+  if (!b->has_codebooks) {
+    set_err("lpcnet_decode: the model blob carries no ceps_codebook1/2/3 / ceps_codebook_diff4 records "
+            "(1024x17, 1024x17, 1024x17, 4096x18 floats)");
+    return -1;
+  }
+  return b->set_device();
+}
+
+/* lpcnet_decode (lpcnet.c:310-319) on the first nB streams, host I/O:
+ * packets [nB][8] -> pcm [nB][4 * FRAME] */
+static int decode_first(LPCNetBatch *b, int nB, const unsigned char *packets, short *pcm)
+{
+  if (decode_ready(b)) return -1;
+  if (!packets || !pcm) { set_err("bad arguments"); return -1; }
+  if (ensure_trace(b, FRAME) || ensure_decode_bufs(b, true)) return -1;
+  HIPCHK(hipMemcpyAsync(b->d_packets, packets, (size_t)nB * 8, hipMemcpyHostToDevice, b->stream));
+  DecodeArgs da = b->da;
+  da.packets = b->d_packets;
+  da.npackets = 1;
+  da.nstreams = nB;
+  da.st = b->d_state;
+  da.features = b->d_dfeat;
+  if (launch_decode(da, b->stream)) { set_err("decode kernel launch failed"); return -1; }
+  /* for (k=0;k<4;k++) lpcnet_synthesize(&st->lpcnet_state, features[k], &pcm[k*FRAME_SIZE], FRAME_SIZE) */
+  for (int f = 0; f < 4; f++)
+    if (launch_frame_step(b, b->d_dfeat + (size_t)f * nB * NF, b->d_lpc, true, b->d_dpcm + (size_t)f * nB * FRAME, FRAME, 0,
+                          -1, nB))
+      return -1;
+  std::vector<short> tmp((size_t)4 * nB * FRAME);
+  HIPCHK(hipMemcpyAsync(tmp.data(), b->d_dpcm, sizeof(short) * tmp.size(), hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  if (check_status(b)) return -1;
+  for (int k = 0; k < nB; k++)
+    for (int f = 0; f < 4; f++)
+      memcpy(pcm + ((size_t)k * 4 + f) * FRAME, &tmp[((size_t)f * nB + k) * FRAME], sizeof(short) * FRAME);
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_batch_decode(LPCNetBatch *b, const unsigned char *packets, short *pcm)
+{
+  return decode_first(b, b ? b->B : 0, packets, pcm);
+}
+
+LPCNET_EXPORT int lpcnet_batch_decode_frames(LPCNetBatch *b, const unsigned char *d_packets, short *d_pcm, int npackets)
+{
+  if (decode_ready(b)) return -1;
+  if (!d_packets || !d_pcm || npackets < 0) { set_err("bad arguments"); return -1; }
+  if (ensure_decode_bufs(b, false)) return -1;
+  for (int p0 = 0; p0 < npackets; p0 += DEC_MAX_PACKETS) {
+    const int np = std::min(DEC_MAX_PACKETS, npackets - p0);
+    DecodeArgs da = b->da;
+    da.packets = d_packets + (size_t)p0 * b->B * 8;
+    da.npackets = np;
+    da.nstreams = b->B;
+    da.st = b->d_state;
+    da.features = b->d_dfeat;
+    /* queued behind every kernel that still reads d_dfeat (the previous
+     * group's frame kernels precede the sample kernels on b->stream) */
+    if (launch_decode(da, b->stream)) { set_err("decode kernel launch failed"); return -1; }
+    if (lpcnet_batch_synthesize_frames(b, nullptr, b->d_dfeat, d_pcm + (size_t)4 * p0 * b->B * FRAME, 4 * np, FRAME))
+      return -1;
+  }
+  return 0;
+}
+
+/* lpcnet_synthesize_tail_impl on the first nB streams: the sample network on
+ * the conditioning and LPC already in the stream states, no frame network */
+static int tail_first(LPCNetBatch *b, int nB, short *pcm, int N, int preload)
+{
+  if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
+  if (N < 0 || N > FRAME || (N > 0 && !pcm) || preload < 0) { set_err("bad arguments"); return -1; }
+  if (N == 0) return 0;
+  if (b->set_device()) return -1;
+  if (ensure_trace(b, N)) return -1;
+  if (preload > 0) HIPCHK(hipMemcpyAsync(b->d_pcm, pcm, sizeof(short) * N * nB, hipMemcpyHostToDevice, b->stream));
+  if (launch_frame_step(b, nullptr, nullptr, false, b->d_pcm, N, preload, -1, nB, false, false)) return -1;
+  HIPCHK(hipMemcpyAsync(pcm, b->d_pcm, sizeof(short) * N * nB, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return check_status(b);
+}
+
+/* run_frame_network on the first nB streams (features [nB][NF]); keep_cond:
+ * into the caller's locals as run_frame_network_flush does (lpcnet.c:134-144),
+ * otherwise into the state's conditioning (lpcnet.c:275) */
+static int frame_first(LPCNetBatch *b, int nB, const float *features, bool keep_cond)
+{
+  if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
+  if (!features) { set_err("bad arguments"); return -1; }
+  if (b->set_device()) return -1;
+  HIPCHK(hipMemcpyAsync(b->d_feat, features, sizeof(float) * NF * nB, hipMemcpyHostToDevice, b->stream));
+  if (launch_frame_step(b, b->d_feat, b->d_lpc, true, nullptr, 0, 0, -1, nB, true, keep_cond)) return -1;
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return check_status(b);
+}
+
+LPCNET_EXPORT int lpcnet_batch_synthesize_tail_impl(LPCNetBatch *b, short *pcm, int N, int preload)
+{
+  return tail_first(b, b ? b->B : 0, pcm, N, preload);
+}
+
+LPCNET_EXPORT int lpcnet_batch_run_frame_network(LPCNetBatch *b, const float *features, int update_conditions)
+{
+  return frame_first(b, b ? b->B : 0, features, update_conditions == 0);
+}
+
+/* lpcnet.c:226-233 lpcnet_reset_signal on one stream */
+static void reset_signal(StreamState &s)
+{
+  s.deemph_mem = 0;
+  s.last_exc = host_lin2ulaw(0.f);
+  memset(s.last_sig, 0, sizeof(s.last_sig));
+  memset(s.gru_a_state, 0, sizeof(s.gru_a_state));
+  memset(s.gru_b_state, 0, sizeof(s.gru_b_state));
+}
+
+LPCNET_EXPORT int lpcnet_batch_reset_signal(LPCNetBatch *b, int stream)
+{
+  if (!b || stream < 0 || stream >= b->B) { set_err("bad arguments"); return -1; }
+  if (b->set_device()) return -1;
+  StreamState s;
+  HIPCHK(hipStreamSynchronize(b->stream));
+  HIPCHK(hipMemcpy(&s, &b->d_state[stream], sizeof(s), hipMemcpyDeviceToHost));
+  reset_signal(s);
+  HIPCHK(hipMemcpy(&b->d_state[stream], &s, sizeof(s), hipMemcpyHostToDevice));
+  return 0;
+}
+
 LPCNET_EXPORT int lpcnet_batch_state_size(void) { return (int)sizeof(StreamState); }
 
 LPCNET_EXPORT int lpcnet_batch_save_state(LPCNetBatch *b, int stream, void *buf)
@@ -2039,32 +2217,37 @@ LPCNET_EXPORT int lpcnet_batch_save_state(LPCNetBatch *b, int stream, void *buf)
   return 0;
 }
 
+/* A snapshot is restored only if it is one this engine can have produced. */
+static bool snapshot_ok(const void *buf)
+{
+  /* GRU states are convex combinations of earlier states and tanh outputs:
+   * |x| <= 1 (+ rounding) or NaN for every state the recurrence produces.
+   * The int8 kernels' state quantiser relies on |x| < 2^24 (quant_s8_state),
+   * so a snapshot outside that range is not one of ours: refuse it. */
+  StreamState tmp;
+  memcpy(&tmp, buf, sizeof(tmp));
+  auto bad = [](const float *v, int n) {
+    for (int k = 0; k < n; k++)
+      if (v[k] > 2.f || v[k] < -2.f) return true;
+    return false;
+  };
+  if (bad(tmp.gru_a_state, NA) || bad(tmp.gru_b_state, NB)) {
+    set_err("snapshot GRU state outside [-2, 2]: not a state this engine produced");
+    return false;
+  }
+  /* last_exc indexes the 256-row embedding tables (lpcnet.c:264: an
+   * excitation is a u-law byte) */
+  if (tmp.last_exc < 0 || tmp.last_exc > 255) {
+    set_err("snapshot last_exc outside [0, 255]: not a state this engine produced");
+    return false;
+  }
+  return true;
+}
+
 LPCNET_EXPORT int lpcnet_batch_restore_state(LPCNetBatch *b, int stream, const void *buf)
 {
   if (!b || stream < 0 || stream >= b->B || !buf || b->set_device()) return -1;
-  {
-    /* GRU states are convex combinations of earlier states and tanh outputs:
-     * |x| <= 1 (+ rounding) or NaN for every state the recurrence produces.
-     * The int8 kernels' state quantiser relies on |x| < 2^24 (quant_s8_state),
-     * so a snapshot outside that range is not one of ours: refuse it. */
-    StreamState tmp;
-    memcpy(&tmp, buf, sizeof(tmp));
-    auto bad = [](const float *v, int n) {
-      for (int k = 0; k < n; k++)
-        if (v[k] > 2.f || v[k] < -2.f) return true;
-      return false;
-    };
-    if (bad(tmp.gru_a_state, NA) || bad(tmp.gru_b_state, NB)) {
-      set_err("snapshot GRU state outside [-2, 2]: not a state this engine produced");
-      return -1;
-    }
-    /* last_exc indexes the 256-row embedding tables (lpcnet.c:264: an
-     * excitation is a u-law byte) */
-    if (tmp.last_exc < 0 || tmp.last_exc > 255) {
-      set_err("snapshot last_exc outside [0, 255]: not a state this engine produced");
-      return -1;
-    }
-  }
+  if (!snapshot_ok(buf)) return -1;
   HIPCHK(hipStreamSynchronize(b->stream));
   HIPCHK(hipMemcpy(&b->d_state[stream], buf, sizeof(StreamState), hipMemcpyHostToDevice));
   int fc;
@@ -2312,23 +2495,33 @@ LPCNET_EXPORT int lpcnet_batch_get_state(LPCNetBatch *b, int stream, float *gru_
 /* The drop-in handles share the GPU.  Every LPCNetState bound to the same
  * model (blob bytes, resolved model constants) on the same device is a slot
  * of one StatePool: one device copy of the model, the slots' stream states
- * in one device array, and one work batch.  Concurrent lpcnet_synthesize
- * calls on different handles coalesce into one launch (flat combining: the
- * first caller to find the pool idle runs every request pending at that
- * moment -- the slots' states are gathered into the work batch, one frame
- * step runs, the states are scattered back), so K reference-style callers
- * on K threads get batch-K launches instead of K batch-1 engines.  Each
- * handle's results are those of its own stream alone (streams of a batch
- * are independent), i.e. the reference's. */
+ * in one device array, and one work batch.  Concurrent calls on different
+ * handles coalesce into one launch (flat combining: the first caller to find
+ * the pool idle runs every request pending at that moment that has the same
+ * shape -- the slots' states are gathered into the work batch, one step
+ * runs, the states are scattered back), so K reference-style callers on K
+ * threads get batch-K launches instead of K batch-1 engines.  Each handle's
+ * results are those of its own stream alone (streams of a batch are
+ * independent), i.e. the reference's. */
 struct StatePool {
+  /* what a request runs on its slot */
+  enum Kind {
+    SYNTH = 0, /* lpcnet_synthesize_impl (lpcnet.c:273-277): frame + N samples, `preload` teacher-forced */
+    TAIL = 1,  /* lpcnet_synthesize_tail_impl (lpcnet.c:235-271): samples only */
+    FLUSH = 2, /* run_frame_network_flush (lpcnet.c:134-144): nfr frames, conditioning discarded */
+    DECODE = 3 /* lpcnet_decode (lpcnet.c:310-319): one 8-byte packet -> 4 frames */
+  };
   struct Req {
     int slot;
-    const float *feat;
-    short *out;
-    int N;
+    int kind;
+    const float *feat;           /* SYNTH [NF], FLUSH [nfr][NF] */
+    const unsigned char *packet; /* DECODE [8] */
+    short *out;                  /* SYNTH / TAIL [N] (the first `preload` are input), DECODE [4 * FRAME] */
+    int N, preload, nfr;
     bool done;
     int rc;
     std::string err;
+    bool same_shape(const Req &o) const { return kind == o.kind && N == o.N && preload == o.preload && nfr == o.nfr; }
   };
   uint64_t key = 0;
   int device = 0;
@@ -2337,7 +2530,7 @@ struct StatePool {
   StreamState *d_slots = nullptr;
   int cap = 0;
   std::vector<int> free_slots;
-  int refs = 0;
+  int refs = 0; /* handles bound + transient acquisitions; changed under g_pools_mu only */
   int *d_map = nullptr;
   int map_cap = 0;
   std::mutex mu;
@@ -2371,6 +2564,7 @@ static uint64_t pool_key(const unsigned char *data, int len)
 /* the pool of (blob, device), created with its model on first use; refs+1 */
 static StatePool *pool_acquire(const unsigned char *data, int len, int device)
 {
+  if (!data || len <= 0) { set_err("lpcnet_load_model: empty blob"); return nullptr; }
   const uint64_t key = pool_key(data, len);
   std::lock_guard<std::mutex> lk(g_pools_mu);
   auto it = g_pools.find({key, device});
@@ -2378,7 +2572,11 @@ static StatePool *pool_acquire(const unsigned char *data, int len, int device)
     it->second->refs++;
     return it->second;
   }
-  if (it != g_pools.end()) return nullptr; /* hash collision between different blobs: refuse rather than mix */
+  if (it != g_pools.end()) {
+    /* a different blob with the same 64-bit key: refuse rather than mix models */
+    set_err("lpcnet_load_model: model pool key collision between two different blobs");
+    return nullptr;
+  }
   LPCNetBatch *w = lpcnet_batch_create(1, device);
   if (!w) return nullptr;
   if (lpcnet_batch_load_model(w, data, len)) {
@@ -2397,19 +2595,23 @@ static StatePool *pool_acquire(const unsigned char *data, int len, int device)
   return p;
 }
 
+/* give back `slot` (if >= 0) and one reference; the last reference frees
+ * the pool.  refs changes under g_pools_mu only, the lock pool_acquire holds
+ * while it looks the pool up, so an acquisition and the last release can
+ * never both succeed. */
 static void pool_release(StatePool *p, int slot)
 {
-  bool last = false;
-  {
+  if (slot >= 0) {
     std::unique_lock<std::mutex> lk(p->mu);
     p->cv.wait(lk, [&] { return !p->busy; });
-    if (slot >= 0) p->free_slots.push_back(slot);
-    last = --p->refs == 0;
+    p->free_slots.push_back(slot);
   }
-  if (!last) return;
-  std::lock_guard<std::mutex> lk(g_pools_mu);
-  if (p->refs != 0) return; /* re-acquired meanwhile */
-  g_pools.erase({p->key, p->device});
+  {
+    std::lock_guard<std::mutex> lk(g_pools_mu);
+    if (--p->refs > 0) return;
+    g_pools.erase({p->key, p->device});
+  }
+  /* unreachable now: no handle holds it and the map no longer lists it */
   if (hipSetDevice(p->device) == hipSuccess) {
     (void)hipFree(p->d_slots);
     (void)hipFree(p->d_map);
@@ -2451,16 +2653,24 @@ static int pool_slot_io(StatePool *p, int slot, StreamState *get, const StreamSt
 {
   std::unique_lock<std::mutex> lk(p->mu);
   p->cv.wait(lk, [&] { return !p->busy; });
-  if (hipSetDevice(p->device) != hipSuccess) return -1;
-  if (get && hipMemcpy(get, &p->d_slots[slot], sizeof(*get), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  if (put && hipMemcpy(&p->d_slots[slot], put, sizeof(*put), hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (hipSetDevice(p->device) != hipSuccess) { set_err("hipSetDevice failed"); return -1; }
+  if (get && hipMemcpy(get, &p->d_slots[slot], sizeof(*get), hipMemcpyDeviceToHost) != hipSuccess) {
+    set_err("device copy failed");
+    return -1;
+  }
+  if (put && hipMemcpy(&p->d_slots[slot], put, sizeof(*put), hipMemcpyHostToDevice) != hipSuccess) {
+    set_err("device copy failed");
+    return -1;
+  }
   return 0;
 }
 
-/* one coalesced frame step for requests rq (all the same N) */
+/* one coalesced step for requests rq (all of the same shape) */
 static int pool_run(StatePool *p, const std::vector<StatePool::Req *> &rq)
 {
-  const int n = (int)rq.size(), N = rq[0]->N;
+  const int n = (int)rq.size();
+  const StatePool::Req &r0 = *rq[0];
+  const int N = r0.N;
   if (p->work->B < n) {
     int nb = 1;
     while (nb < n) nb *= 2;
@@ -2482,30 +2692,54 @@ static int pool_run(StatePool *p, const std::vector<StatePool::Req *> &rq)
     p->map_cap = w->B;
   }
   std::vector<int> map(n);
-  std::vector<float> feat((size_t)n * NF);
-  std::vector<short> pcm((size_t)n * std::max(N, 1));
-  for (int k = 0; k < n; k++) {
-    map[k] = rq[k]->slot;
-    memcpy(&feat[(size_t)k * NF], rq[k]->feat, sizeof(float) * NF);
-  }
+  for (int k = 0; k < n; k++) map[k] = rq[k]->slot;
   HIPCHK(hipMemcpyAsync(p->d_map, map.data(), sizeof(int) * n, hipMemcpyHostToDevice, w->stream));
   if (launch_state_copy(w->d_state, p->d_slots, nullptr, p->d_map, n, w->stream)) { set_err("state gather failed"); return -1; }
-  const int rc = synth_first(w, n, feat.data(), pcm.data(), N, 0);
+  /* every stream of the work batch is this call's: the multi-frame bound is its min */
+  w->min_fc = 0;
+  std::vector<float> feat((size_t)n * NF);
+  const int nout = r0.kind == StatePool::DECODE ? 4 * FRAME : N;
+  std::vector<short> pcm((size_t)n * std::max(nout, 1));
+  int rc = 0;
+  switch (r0.kind) {
+  case StatePool::SYNTH:
+  case StatePool::TAIL:
+    for (int k = 0; k < n; k++) {
+      if (r0.kind == StatePool::SYNTH) memcpy(&feat[(size_t)k * NF], rq[k]->feat, sizeof(float) * NF);
+      if (r0.preload > 0) memcpy(&pcm[(size_t)k * N], rq[k]->out, sizeof(short) * std::min(r0.preload, N));
+    }
+    rc = r0.kind == StatePool::SYNTH ? synth_first(w, n, feat.data(), pcm.data(), N, r0.preload)
+                                     : tail_first(w, n, pcm.data(), N, r0.preload);
+    break;
+  case StatePool::FLUSH:
+    for (int j = 0; j < r0.nfr && rc == 0; j++) {
+      for (int k = 0; k < n; k++) memcpy(&feat[(size_t)k * NF], rq[k]->feat + (size_t)j * NF, sizeof(float) * NF);
+      rc = frame_first(w, n, feat.data(), true);
+    }
+    break;
+  case StatePool::DECODE: {
+    std::vector<unsigned char> pk((size_t)n * 8);
+    for (int k = 0; k < n; k++) memcpy(&pk[(size_t)k * 8], rq[k]->packet, 8);
+    rc = decode_first(w, n, pk.data(), pcm.data());
+    break;
+  }
+  default:
+    set_err("bad request");
+    rc = -1;
+  }
   if (rc == 0) {
     if (launch_state_copy(p->d_slots, w->d_state, p->d_map, nullptr, n, w->stream)) { set_err("state scatter failed"); return -1; }
     HIPCHK(hipStreamSynchronize(w->stream));
     for (int k = 0; k < n; k++)
-      if (N > 0) memcpy(rq[k]->out, &pcm[(size_t)k * N], sizeof(short) * N);
+      if (nout > 0 && r0.kind != StatePool::FLUSH) memcpy(rq[k]->out, &pcm[(size_t)k * nout], sizeof(short) * nout);
   }
   p->launches++;
   p->requests += n;
   return rc;
 }
 
-static int pool_synthesize(StatePool *p, int slot, const float *features, short *out, int N)
+static int pool_submit(StatePool *p, StatePool::Req &r)
 {
-  if (N < 0 || N > FRAME || !features || (N > 0 && !out)) { set_err("bad arguments"); return -1; }
-  StatePool::Req r{slot, features, out, N, false, 0, std::string()};
   std::unique_lock<std::mutex> lk(p->mu);
   p->pending.push_back(&r);
   while (!r.done) {
@@ -2513,10 +2747,10 @@ static int pool_synthesize(StatePool *p, int slot, const float *features, short 
       p->cv.wait(lk);
       continue;
     }
-    /* combine: every pending request with the first one's N */
+    /* combine: every pending request with the first one's shape */
     p->busy = true;
     std::vector<StatePool::Req *> mine, rest;
-    for (StatePool::Req *q : p->pending) (q->N == p->pending[0]->N ? mine : rest).push_back(q);
+    for (StatePool::Req *q : p->pending) (q->same_shape(*p->pending[0]) ? mine : rest).push_back(q);
     p->pending.swap(rest);
     lk.unlock();
     const int rc = pool_run(p, mine);
@@ -2534,52 +2768,130 @@ static int pool_synthesize(StatePool *p, int slot, const float *features, short 
   return r.rc;
 }
 
+/* ---- handles -------------------------------------------------------------
+ * An LPCNetState is caller memory (lpcnet_get_size + malloc, calloc through
+ * lpcnet_create, or embedded in a larger struct as the reference's decoder
+ * and PLC states embed theirs).  It holds a magic word and a 64-bit token;
+ * everything else -- device, bound pool and slot, the deferred feature
+ * buffer -- lives in a Handle found through the registry, so nothing read
+ * from caller memory is ever dereferenced.  A registry entry whose token
+ * does not match the memory at its address is stale (the memory was freed
+ * without lpcnet_destroy / lpcnet_mi355x_deinit and reused): lpcnet_init
+ * there drops it, releasing its slot, and starts a fresh handle. */
 struct LPCNetState {
   uint32_t magic;
-  int device;
-  StatePool *pool; /* bound model (nullptr: none) */
-  int slot;
+  uint32_t reserved;
+  uint64_t token;
 };
 static const uint32_t kMagic = 0x4c50434eu; /* "LPCN" */
 
-LPCNET_EXPORT int lpcnet_get_size(void) { return (int)sizeof(LPCNetState); }
+constexpr int MAX_FEATURE_BUFFER = 4; /* lpcnet_private.h:26 MAX_FEATURE_BUFFER_SIZE */
 
-/* Handles initialised by lpcnet_init and not yet destroyed.  lpcnet_init is
- * called on raw caller memory (lpcnet_get_size + malloc, as the reference's
- * decoder does), so its contents are never trusted to tell a live handle
- * from garbage: only this registry does. */
+struct Handle {
+  uint64_t token = 0;
+  int device = 0;
+  StatePool *pool = nullptr; /* bound model (nullptr: none) */
+  int slot = -1;
+  /* run_frame_network_deferred's buffer (lpcnet_private.h:37-38, lpcnet.c:122-132) */
+  int fbuf_fill = 0;
+  float fbuf[MAX_FEATURE_BUFFER][NF] = {};
+};
+
+/* A handle's complete synthesis state: lpcnet_mi355x_state_save/restore, the
+ * replacement of the LPCNetState struct copies of lpcnet_plc.c:223,230. */
+struct HandleSnapshot {
+  StreamState s;
+  int fbuf_fill;
+  float fbuf[MAX_FEATURE_BUFFER][NF];
+};
+
 static std::mutex g_live_mu;
-static std::set<LPCNetState *> g_live;
+static std::unordered_map<const LPCNetState *, Handle *> g_live;
 
-static bool is_live(LPCNetState *st)
+static uint64_t new_token()
 {
-  std::lock_guard<std::mutex> lk(g_live_mu);
-  return st && g_live.count(st);
+  static std::atomic<uint64_t> ctr{0};
+  static const uint64_t salt = (uint64_t)(uintptr_t)&ctr ^ ((uint64_t)time(nullptr) << 20);
+  uint64_t z = (ctr.fetch_add(1) + 1) * 0x9E3779B97F4A7C15ull ^ salt; /* splitmix64 */
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z ? z : 1;
 }
+
+/* the live handle at st, or nullptr */
+static Handle *live_handle(const LPCNetState *st)
+{
+  if (!st) return nullptr;
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  auto it = g_live.find(st);
+  if (it == g_live.end() || st->magic != kMagic || st->token != it->second->token) return nullptr;
+  return it->second;
+}
+
+static void handle_free(Handle *h)
+{
+  if (h->pool) pool_release(h->pool, h->slot);
+  delete h;
+}
+
+/* unregister st (if live) and release its device resources */
+static void handle_deinit(LPCNetState *st)
+{
+  Handle *h = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    auto it = g_live.find(st);
+    if (it != g_live.end() && st->magic == kMagic && st->token == it->second->token) {
+      h = it->second;
+      g_live.erase(it);
+    }
+  }
+  if (h) handle_free(h);
+  /* a later malloc may hand this block out again: leave nothing that looks live */
+  st->magic = 0;
+  st->token = 0;
+}
+
+LPCNET_EXPORT int lpcnet_get_size(void) { return (int)sizeof(LPCNetState); }
 
 LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
 {
   if (!st) return -1;
-  /* src/lpcnet.c:184-200 ends with lpcnet_reset(): re-initialising a live
-   * handle (from lpcnet_create / an earlier lpcnet_init) resets its stream
-   * and keeps its device binding and model; anything else is a fresh handle */
+  Handle *stale = nullptr, *live = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_live_mu);
-    if (g_live.count(st)) {
-      if (st->pool) {
-        StreamState s;
-        host_reset_state(s);
-        pool_slot_io(st->pool, st->slot, nullptr, &s);
+    auto it = g_live.find(st);
+    if (it != g_live.end()) {
+      if (st->magic == kMagic && st->token == it->second->token) {
+        live = it->second;
+      } else {
+        stale = it->second;
+        g_live.erase(it);
       }
-      return 0;
     }
-    g_live.insert(st);
+    if (!live) {
+      Handle *h = new Handle();
+      h->token = new_token();
+      const char *d = getenv("LPCNET_DEVICE");
+      h->device = d ? atoi(d) : 0;
+      g_live[st] = h;
+      st->magic = kMagic;
+      st->reserved = 0;
+      st->token = h->token;
+    }
   }
-  st->magic = kMagic;
-  const char *d = getenv("LPCNET_DEVICE");
-  st->device = d ? atoi(d) : 0;
-  st->pool = nullptr;
-  st->slot = -1;
+  if (stale) handle_free(stale);
+  if (live) {
+    /* src/lpcnet.c:184-200 ends with lpcnet_reset(): re-initialising a live
+     * handle resets its stream and keeps its device binding and model */
+    live->fbuf_fill = 0;
+    if (live->pool) {
+      StreamState s;
+      host_reset_state(s);
+      if (pool_slot_io(live->pool, live->slot, nullptr, &s)) return -1;
+    }
+  }
   return 0;
 }
 
@@ -2593,78 +2905,242 @@ LPCNET_EXPORT LPCNetState *lpcnet_create(void)
 LPCNET_EXPORT void lpcnet_destroy(LPCNetState *st)
 {
   if (!st) return;
-  bool live;
-  {
-    std::lock_guard<std::mutex> lk(g_live_mu);
-    live = g_live.erase(st) > 0;
-  }
-  if (live && st->pool) pool_release(st->pool, st->slot);
-  /* a later malloc may hand this block out again: leave nothing that looks live */
-  st->magic = 0;
-  st->pool = nullptr;
+  handle_deinit(st);
   free(st);
+}
+
+LPCNET_EXPORT void lpcnet_mi355x_deinit(LPCNetState *st)
+{
+  if (st) handle_deinit(st);
 }
 
 LPCNET_EXPORT void lpcnet_reset(LPCNetState *st)
 {
-  if (!is_live(st) || !st->pool) return;
+  Handle *h = live_handle(st);
+  if (!h) return;
+  h->fbuf_fill = 0; /* lpcnet.c:177-179 clears from LPCNET_RESET_START, the feature buffer included */
+  if (!h->pool) return;
   StreamState s;
   host_reset_state(s);
-  pool_slot_io(st->pool, st->slot, nullptr, &s);
+  pool_slot_io(h->pool, h->slot, nullptr, &s);
 }
 
 LPCNET_EXPORT int lpcnet_load_model(LPCNetState *st, const unsigned char *data, int len)
 {
-  if (!is_live(st)) return -1;
-  StatePool *p = pool_acquire(data, len, st->device);
+  Handle *h = live_handle(st);
+  if (!h) { set_err("lpcnet_load_model: not an initialised LPCNetState"); return -1; }
+  StatePool *p = pool_acquire(data, len, h->device);
   if (!p) return -1;
-  if (p == st->pool) {
+  if (p == h->pool) {
     pool_release(p, -1); /* same model: keep the binding */
     return 0;
   }
   /* the model changes, the stream state stays (lpcnet.c:202-210 only binds arrays) */
   StreamState s;
-  bool have = st->pool && pool_slot_io(st->pool, st->slot, &s, nullptr) == 0;
+  bool have = h->pool && pool_slot_io(h->pool, h->slot, &s, nullptr) == 0;
   const int slot = pool_alloc_slot(p, have ? &s : nullptr);
   if (slot < 0) {
     pool_release(p, -1);
     return -1;
   }
-  if (st->pool) pool_release(st->pool, st->slot);
-  st->pool = p;
-  st->slot = slot;
+  if (h->pool) pool_release(h->pool, h->slot);
+  h->pool = p;
+  h->slot = slot;
   return 0;
+}
+
+/* run one request on st's slot; the void entry points report failure as the
+ * reference cannot: silence out, lpcnet_mi355x_last_error(), one stderr line */
+static int handle_run(LPCNetState *st, StatePool::Req r, const char *what)
+{
+  Handle *h = live_handle(st);
+  int rc;
+  if (!h || !h->pool) {
+    set_err(std::string(what) +
+            ": no model bound (call lpcnet_load_model first; liblpcnet_mi355x has no compiled-in model)");
+    rc = -1;
+  } else {
+    r.slot = h->slot;
+    rc = pool_submit(h->pool, r);
+  }
+  if (rc != 0) {
+    static std::atomic<bool> warned{false};
+    const int nout = r.kind == StatePool::DECODE ? 4 * FRAME : r.N;
+    if (r.out && nout > 0 && r.kind != StatePool::FLUSH) memset(r.out, 0, sizeof(short) * nout);
+    if (!warned.exchange(true)) fprintf(stderr, "liblpcnet_mi355x: %s\n", g_err.c_str());
+  }
+  return rc;
+}
+
+static bool req_args_ok(const float *features, const short *output, int N, int preload, bool need_features)
+{
+  if (N < 0 || N > FRAME || (need_features && !features) || (N > 0 && !output) || preload < 0) {
+    set_err("bad arguments");
+    return false;
+  }
+  return true;
+}
+
+LPCNET_EXPORT void lpcnet_synthesize_impl(LPCNetState *st, const float *features, short *output, int N, int preload)
+{
+  if (!req_args_ok(features, output, N, preload, true)) return;
+  StatePool::Req r{-1, StatePool::SYNTH, features, nullptr, output, N, std::min(preload, N), 0, false, 0, std::string()};
+  handle_run(st, r, "lpcnet_synthesize_impl");
 }
 
 LPCNET_EXPORT void lpcnet_synthesize(LPCNetState *st, const float *features, short *output, int N)
 {
-  /* void in the reference: a failed call (no model bound -- this library has
-   * no compiled-in model, so lpcnet_load_model is required -- or a device
-   * error) outputs silence, sets lpcnet_mi355x_last_error() and says so once
-   * on stderr */
-  static std::atomic<bool> warned{false};
-  int rc;
-  if (!is_live(st) || !st->pool) {
-    set_err("lpcnet_synthesize: no model bound (call lpcnet_load_model first; liblpcnet_mi355x has no compiled-in model)");
-    rc = -1;
-  } else {
-    rc = pool_synthesize(st->pool, st->slot, features, output, N);
+  if (!req_args_ok(features, output, N, 0, true)) {
+    if (output && N > 0 && N <= FRAME) memset(output, 0, sizeof(short) * N);
+    return;
   }
-  if (rc != 0) {
-    if (output && N > 0) memset(output, 0, sizeof(short) * N);
-    if (!warned.exchange(true)) fprintf(stderr, "liblpcnet_mi355x: %s\n", g_err.c_str());
+  StatePool::Req r{-1, StatePool::SYNTH, features, nullptr, output, N, 0, 0, false, 0, std::string()};
+  handle_run(st, r, "lpcnet_synthesize");
+}
+
+LPCNET_EXPORT void lpcnet_synthesize_tail_impl(LPCNetState *st, short *output, int N, int preload)
+{
+  if (!req_args_ok(nullptr, output, N, preload, false) || N == 0) return;
+  StatePool::Req r{-1, StatePool::TAIL, nullptr, nullptr, output, N, std::min(preload, N), 0, false, 0, std::string()};
+  handle_run(st, r, "lpcnet_synthesize_tail_impl");
+}
+
+/* lpcnet.c:122-132: keep the last kernel_size(conv1) + kernel_size(conv2) - 2
+ * frames (4 for the 3-tap convolutions of every LPCNet model) */
+LPCNET_EXPORT void run_frame_network_deferred(LPCNetState *st, const float *features)
+{
+  Handle *h = live_handle(st);
+  if (!h || !features) return;
+  if (h->fbuf_fill == MAX_FEATURE_BUFFER)
+    memmove(h->fbuf[0], h->fbuf[1], sizeof(float) * NF * (MAX_FEATURE_BUFFER - 1));
+  else
+    h->fbuf_fill++;
+  memcpy(h->fbuf[h->fbuf_fill - 1], features, sizeof(float) * NF);
+}
+
+/* lpcnet.c:134-144: the frame network of every buffered frame, outputs into
+ * locals (the state's conditioning and LPC stay), then an empty buffer */
+LPCNET_EXPORT void run_frame_network_flush(LPCNetState *st)
+{
+  Handle *h = live_handle(st);
+  if (!h || h->fbuf_fill == 0) return;
+  float f[MAX_FEATURE_BUFFER][NF];
+  memcpy(f, h->fbuf, sizeof(f));
+  StatePool::Req r{-1, StatePool::FLUSH, &f[0][0], nullptr, nullptr, 0, 0, h->fbuf_fill, false, 0, std::string()};
+  h->fbuf_fill = 0;
+  handle_run(st, r, "run_frame_network_flush");
+}
+
+/* lpcnet.c:226-233 */
+LPCNET_EXPORT void lpcnet_reset_signal(LPCNetState *st)
+{
+  Handle *h = live_handle(st);
+  if (!h || !h->pool) return;
+  StreamState s;
+  if (pool_slot_io(h->pool, h->slot, &s, nullptr)) return;
+  reset_signal(s);
+  pool_slot_io(h->pool, h->slot, nullptr, &s);
+}
+
+LPCNET_EXPORT int lpcnet_mi355x_state_size(void) { return (int)sizeof(HandleSnapshot); }
+
+LPCNET_EXPORT int lpcnet_mi355x_state_save(LPCNetState *st, void *buf)
+{
+  Handle *h = live_handle(st);
+  if (!h || !h->pool || !buf) { set_err("lpcnet_mi355x_state_save: no model bound or no buffer"); return -1; }
+  HandleSnapshot snap;
+  memset(&snap, 0, sizeof(snap));
+  if (pool_slot_io(h->pool, h->slot, &snap.s, nullptr)) return -1;
+  snap.fbuf_fill = h->fbuf_fill;
+  memcpy(snap.fbuf, h->fbuf, sizeof(snap.fbuf));
+  memcpy(buf, &snap, sizeof(snap));
+  return 0;
+}
+
+LPCNET_EXPORT int lpcnet_mi355x_state_restore(LPCNetState *st, const void *buf)
+{
+  Handle *h = live_handle(st);
+  if (!h || !h->pool || !buf) { set_err("lpcnet_mi355x_state_restore: no model bound or no buffer"); return -1; }
+  HandleSnapshot snap;
+  memcpy(&snap, buf, sizeof(snap));
+  if (!snapshot_ok(&snap.s)) return -1;
+  if (snap.fbuf_fill < 0 || snap.fbuf_fill > MAX_FEATURE_BUFFER) {
+    set_err("snapshot feature buffer fill outside [0, 4]: not a state this engine produced");
+    return -1;
   }
+  if (pool_slot_io(h->pool, h->slot, nullptr, &snap.s)) return -1;
+  h->fbuf_fill = snap.fbuf_fill;
+  memcpy(h->fbuf, snap.fbuf, sizeof(h->fbuf));
+  return 0;
 }
 
 LPCNET_EXPORT int lpcnet_mi355x_pool_stats(const LPCNetState *st, long *launches, long *requests, int *streams)
 {
-  LPCNetState *s = const_cast<LPCNetState *>(st);
-  if (!is_live(s) || !s->pool) return -1;
-  std::lock_guard<std::mutex> lk(s->pool->mu);
-  if (launches) *launches = s->pool->launches;
-  if (requests) *requests = s->pool->requests;
-  if (streams) *streams = s->pool->refs;
+  Handle *h = live_handle(st);
+  if (!h || !h->pool) return -1;
+  StatePool *p = h->pool;
+  {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (launches) *launches = p->launches;
+    if (requests) *requests = p->requests;
+  }
+  if (streams) {
+    std::lock_guard<std::mutex> lk(g_pools_mu);
+    *streams = p->refs;
+  }
   return 0;
+}
+
+/* ---- 1.6 kb/s decoder (include/lpcnet.h:63-100 of the reference) --------
+ * LPCNetDecState embeds an LPCNetState as the reference's does
+ * (lpcnet_private.h:50-53); vq_mem lives with the stream's device state. */
+struct LPCNetDecState {
+  LPCNetState lpcnet_state;
+};
+
+LPCNET_EXPORT int lpcnet_decoder_get_size(void) { return (int)sizeof(LPCNetDecState); }
+
+/* lpcnet.c:290-295: memset + lpcnet_init (a zeroed embedded handle is a
+ * fresh one; a live one at the same address is dropped as stale) */
+LPCNET_EXPORT int lpcnet_decoder_init(LPCNetDecState *st)
+{
+  if (!st) return -1;
+  memset(st, 0, sizeof(*st));
+  return lpcnet_init(&st->lpcnet_state);
+}
+
+LPCNET_EXPORT LPCNetDecState *lpcnet_decoder_create(void)
+{
+  LPCNetDecState *st = (LPCNetDecState *)malloc(sizeof(LPCNetDecState));
+  if (st) lpcnet_decoder_init(st);
+  return st;
+}
+
+LPCNET_EXPORT void lpcnet_decoder_destroy(LPCNetDecState *st)
+{
+  if (!st) return;
+  handle_deinit(&st->lpcnet_state);
+  free(st);
+}
+
+LPCNET_EXPORT int lpcnet_mi355x_decoder_load_model(LPCNetDecState *st, const unsigned char *data, int len)
+{
+  if (!st) return -1;
+  if (lpcnet_load_model(&st->lpcnet_state, data, len)) return -1;
+  Handle *h = live_handle(&st->lpcnet_state);
+  if (!h || !h->pool || !h->pool->work->has_codebooks) {
+    set_err("lpcnet_decode needs the ceps_codebook1/2/3 / ceps_codebook_diff4 records in the blob");
+    return -1;
+  }
+  return 0;
+}
+
+/* lpcnet.c:310-319: decode_packet, then lpcnet_synthesize of the 4 frames */
+LPCNET_EXPORT int lpcnet_decode(LPCNetDecState *st, const unsigned char *buf, short *pcm)
+{
+  if (!st || !buf || !pcm) { set_err("bad arguments"); return -1; }
+  StatePool::Req r{-1, StatePool::DECODE, nullptr, buf, pcm, 4 * FRAME, 0, 0, false, 0, std::string()};
+  return handle_run(&st->lpcnet_state, r, "lpcnet_decode") ? -1 : 0;
 }
 
 /* Host-only check of a weight blob against every rule lpcnet_load_model

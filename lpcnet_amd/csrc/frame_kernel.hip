@@ -271,7 +271,7 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
 #pragma unroll
       for (int k = 0; k < NS; k++) acc[k] = A.proj_b[row];
       chain_deep<COND, FK_PROJ, NS>(A.proj_w, row, xs, acc);
-      if (tid + p * FK_THREADS >= FK_PROJ) continue;
+      if (tid + p * FK_THREADS >= FK_PROJ || A.keep_cond) continue;
 #pragma unroll
       for (int k = 0; k < NS; k++) {
         const int sid = s0 + k;
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
    * lpc_from_cepstrum ring of FEATURES_DELAY frames (none at delay 0); then
    * lpc_weighting by LPC_GAMMA */
   if (A.mc.end2end) {
-    if (tid < NS && s0 + tid < A.nstreams) {
+    if (tid < NS && s0 + tid < A.nstreams && !A.keep_cond) {
       float rc[NLPC], l[NLPC];
 #pragma unroll
       for (int k = 0; k < NLPC; k++) rc[k] = ya[tid][k];
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(FK_THREADS) void frame_kernel(FrameArgs A)
       const float cur = D > 0 ? p->old_lpc[D - 1][k] : lpc_in;
       for (int j = D - 1; j > 0; j--) p->old_lpc[j][k] = p->old_lpc[j - 1][k];
       if (D > 0) p->old_lpc[0][k] = lpc_in;
-      p->lpc[k] = lpc_weight(cur, k, A.mc.lpc_gamma);
+      if (!A.keep_cond) p->lpc[k] = lpc_weight(cur, k, A.mc.lpc_gamma);
     }
   }
   __syncthreads();

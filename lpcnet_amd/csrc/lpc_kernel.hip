@@ -26,7 +26,7 @@ namespace lpcnet_mi355x {
 
 namespace {
 
-constexpr int NBANDS = LPC_NBANDS, WIN = LPC_WIN;
+constexpr int WIN = LPC_WIN; /* NBANDS (lpcnet_engine.h) == LPC_NBANDS */
 #ifndef LPC_WG_STREAMS
 #define LPC_WG_STREAMS 8
 #endif

@@ -20,6 +20,7 @@ constexpr int EP = 64;         /* pitch embedding */
 constexpr int FIN = NF + EP;   /* lpcnet.c:44 FRAME_INPUT_SIZE */
 constexpr int NLPC = 16;       /* LPC_ORDER */
 constexpr int FRAME = 160;     /* samples per frame */
+constexpr int NBANDS = 18;     /* freq.h:48 NB_BANDS (cepstral bands of the 1.6 kb/s decoder) */
 constexpr int GA_ROWS = 3 * NA;
 constexpr int GB_ROWS = 3 * NB;
 /* Model constants the reference bakes into the generated nnet_data.h
@@ -89,7 +90,11 @@ struct alignas(16) StreamState {
   int last_exc;
   int frame_count;
   uint32_t rng[4];
-  int pad[1];
+  /* LPCNetDecState::vq_mem (lpcnet_private.h:50-53): the previous packet's
+   * last cepstrum, read by decode_packet (lpcnet_dec.c:81-156); zero after
+   * a reset (lpcnet_decoder_init memsets the decoder state) */
+  float vq_mem[NBANDS];
+  int pad[3];
 };
 
 /* The device rcpps table holds t + kRcpBias (device_math.h rcp_x86_fix),
@@ -151,6 +156,10 @@ struct FrameArgs {
    * outputs of frame f into cond[f * B .. f * B + B) */
   int nframes;
   FrameCond *cond;
+  /* frame_kernel: 1 = run_frame_network into the caller's locals, as
+   * run_frame_network_flush does (lpcnet.c:134-144): conv memories, LPC ring
+   * and frame_count advance, the state's conditioning and lpc stay */
+  int keep_cond;
 };
 
 struct SampleArgs {
@@ -322,7 +331,7 @@ int launch_fp(const SampleArgs &a, void *stream);
  * (freq.c dct_table), the 320-point kiss FFT twiddles and input permutation
  * (kiss_fft.c, lpcnet_tables.c), the band index and interpolation fraction of
  * every spectrum bin (freq.c:202-216), the compensation factors (freq.c:50). */
-constexpr int LPC_NBANDS = 18;
+constexpr int LPC_NBANDS = NBANDS;
 constexpr int LPC_WIN = 320;
 constexpr int LPC_ORDER1 = NLPC + 1;
 constexpr int LPC_CHUNK = 32;     /* frames per batched lpc_kernel launch (lpcnet_batch_synthesize_frames) */
@@ -344,6 +353,21 @@ struct LpcTables {
 };
 /* features [nstreams][NF] -> lpc_out [nstreams][NLPC] */
 int launch_lpc(const float *features, float *lpc_out, int nstreams, const LpcTables *tables, void *stream);
+
+/* decode_packet (lpcnet_dec.c:81-156) on the device (decode_kernel.hip):
+ * packets [npackets][nstreams][8] -> features [4 npackets][nstreams][NF],
+ * each stream's vq_mem in st carried from packet to packet. */
+struct DecodeArgs {
+  const unsigned char *packets;
+  int npackets, nstreams;
+  StreamState *st;
+  const float *cb1, *cb2, *cb3; /* ceps_codebook1..3 [1024][NBANDS - 1] */
+  const float *cbd;             /* ceps_codebook_diff4 [4096][NBANDS] */
+  const float *pitch;           /* [64]: (float)(pow(2.f, m / 21.) * PITCH_MIN_PERIOD) (lpcnet_dec.c:118) */
+  float *features;
+};
+constexpr int DEC_MAX_PACKETS = LPC_CHUNK / 4; /* packets per decode launch (the frames of one chunk) */
+int launch_decode(const DecodeArgs &a, void *stream);
 
 }  // namespace lpcnet_mi355x
 

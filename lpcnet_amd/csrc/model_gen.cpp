@@ -287,6 +287,27 @@ extern "C" LPCNET_EXPORT int lpcnet_mi355x_synthetic_model(unsigned seed, int va
     blob.addf("sparse_gru_a_bias", bias);
     blob.addf("sparse_gru_a_subias", subias);
   }
+  /* flags bit 2: the 1.6 kb/s decoder's codebooks (lpcnet_private.h:109-112;
+   * sizes from lpcnet_enc.c:109-119, 709), drawn from their own generator so
+   * every other array is identical with or without them.  Scales follow the
+   * synthetic features' cepstra (0.6/k on band k): stage 1 carries most of
+   * it, stages 2 and 3 refine, the difference codebook is a residual. */
+  if (flags & 4) {
+    Rng c;
+    c.seed("lpcnet-mi355x-synthetic-codebooks", seed);
+    const float stage[3] = {1.f, 0.35f, 0.15f};
+    const char *names[3] = {"ceps_codebook1", "ceps_codebook2", "ceps_codebook3"};
+    for (int k = 0; k < 3; k++) {
+      std::vector<float> cb((size_t)1024 * 17);
+      for (int e = 0; e < 1024; e++)
+        for (int i = 0; i < 17; i++) cb[(size_t)e * 17 + i] = stage[k] * (0.6f / (i + 1)) * c.gauss();
+      blob.addf(names[k], cb);
+    }
+    std::vector<float> d((size_t)4096 * 18);
+    for (int e = 0; e < 4096; e++)
+      for (int i = 0; i < 18; i++) d[(size_t)e * 18 + i] = (i == 0 ? 0.5f : 0.25f / i) * c.gauss();
+    blob.addf("ceps_codebook_diff4", d);
+  }
   int size = (int)blob.data.size();
   if (buf && cap >= size) memcpy(buf, blob.data.data(), size);
   return size;

@@ -30,6 +30,10 @@
 #define FRAME_SIZE 160
 #define PREEMPH 0.85f /* lpcnet.c:40 */
 #define NLEVELS 256
+#define MAX_FEATURE_BUFFER_SIZE 4 /* lpcnet_private.h:26 */
+#define NB_BANDS 18               /* freq.h:48 */
+#define NB_BANDS_1 (NB_BANDS - 1) /* freq.h:49 */
+#define NB_TOTAL_FEATURES 36      /* include/lpcnet.h:46 */
 
 /* ------------------------------------------------------------------------ */
 /* rcpps emulation.  The table holds _mm256_rcp_ps(1.m) for the 2048 values of
@@ -587,10 +591,16 @@ struct OracleState {
   int frame_count;
   float deemph_mem;
   float lpc[LPC_ORDER];
+  float feature_buffer[NB_FEATURES * MAX_FEATURE_BUFFER_SIZE]; /* lpcnet_private.h:37-38 */
+  int feature_buffer_fill;
   /* trace */
   float *t_logits;
   int *t_exc;
   uint32_t *t_rng;
+  /* 1.6 kb/s decoder: codebooks (generated ceps_codebooks.c in the
+   * reference, optional blob records here) and LPCNetDecState::vq_mem */
+  const float *cb1, *cb2, *cb3, *cbd;
+  float vq_mem[NB_BANDS];
 };
 
 OracleState *oracle_create(const unsigned char *blob, int len, int variant, const oracle_kernels *k)
@@ -638,6 +648,11 @@ OracleState *oracle_create(const unsigned char *blob, int len, int variant, cons
   F(st->fc_w, "dual_fc_weights", NB * 2 * NLEVELS);
   F(st->fc_factor, "dual_fc_factor", 2 * NLEVELS);
 #undef F
+  /* optional decoder codebooks (lpcnet_private.h:109-112; sizes lpcnet_enc.c:109-119, 709) */
+  st->cb1 = (const float *)find_arr(list, n, "ceps_codebook1", 1024 * NB_BANDS_1 * 4);
+  st->cb2 = (const float *)find_arr(list, n, "ceps_codebook2", 1024 * NB_BANDS_1 * 4);
+  st->cb3 = (const float *)find_arr(list, n, "ceps_codebook3", 1024 * NB_BANDS_1 * 4);
+  st->cbd = (const float *)find_arr(list, n, "ceps_codebook_diff4", 4096 * NB_BANDS * 4);
   st->lpc_gamma = 1.f;
   st->delay = FEATURES_DELAY;
   st->end2end = 0;
@@ -733,7 +748,8 @@ static void rc2lpc(float *lpc, const float *rc)
 }
 
 /* lpcnet.c:82-120 run_frame_network */
-static void run_frame_network(OracleState *st, const float *features)
+static void run_frame_network(OracleState *st, float *gru_a_condition, float *gru_b_condition, float *lpc,
+                              const float *features)
 {
   float in[FRAME_INPUT], conv1_out[COND], conv2_out[COND], dense1_out[COND], condition[COND];
   int pitch = (int)floor(.1 + 50 * features[18] + 100);
@@ -746,18 +762,18 @@ static void run_frame_network(OracleState *st, const float *features)
   if (st->frame_count < st->delay) memset(conv2_out, 0, sizeof(conv2_out));
   dense(st, dense1_out, st->dense1_w, st->dense1_b, COND, COND, 1, conv2_out);
   dense(st, condition, st->dense2_w, st->dense2_b, COND, COND, 1, dense1_out);
-  dense(st, st->gru_a_cond, st->gadf_w, st->gadf_b, COND, 3 * NA, 0, condition);
-  dense(st, st->gru_b_cond, st->gbdf_w, st->gbdf_b, COND, 3 * NB, 0, condition);
+  dense(st, gru_a_condition, st->gadf_w, st->gadf_b, COND, 3 * NA, 0, condition);
+  dense(st, gru_b_condition, st->gbdf_w, st->gbdf_b, COND, 3 * NB, 0, condition);
   if (st->end2end) {
-    rc2lpc(st->lpc, condition); /* lpcnet.c:104,107-108: rc = condition[0..LPC_ORDER) */
+    rc2lpc(lpc, condition); /* lpcnet.c:104,107-108: rc = condition[0..LPC_ORDER) */
   } else if (st->delay > 0) {   /* lpcnet.c:109-112 */
-    memcpy(st->lpc, st->old_lpc[st->delay - 1], sizeof(st->lpc));
+    memcpy(lpc, st->old_lpc[st->delay - 1], LPC_ORDER * sizeof(float));
     memmove(st->old_lpc[1], st->old_lpc[0], (st->delay - 1) * LPC_ORDER * sizeof(float));
     st->k->lpc_from_cepstrum(st->old_lpc[0], features);
   } else {                      /* lpcnet.c:113-114 */
-    st->k->lpc_from_cepstrum(st->lpc, features);
+    st->k->lpc_from_cepstrum(lpc, features);
   }
-  st->k->lpc_weighting(st->lpc, st->lpc_gamma); /* lpcnet.c:116-118 */
+  st->k->lpc_weighting(lpc, st->lpc_gamma); /* lpcnet.c:116-118 */
   if (st->frame_count < 1000) st->frame_count++;
 }
 
@@ -882,6 +898,160 @@ static void synthesize_tail(OracleState *st, short *output, int N, int preload)
 /* lpcnet.c:273-277 */
 void oracle_synthesize(OracleState *st, const float *features, short *output, int N, int preload)
 {
-  run_frame_network(st, features);
+  run_frame_network(st, st->gru_a_cond, st->gru_b_cond, st->lpc, features);
   synthesize_tail(st, output, N, preload);
+}
+
+void oracle_synthesize_tail(OracleState *st, short *output, int N, int preload)
+{
+  synthesize_tail(st, output, N, preload);
+}
+
+/* lpcnet.c:122-132 run_frame_network_deferred; max_buffer_size = the two
+ * 3-tap convolutions' kernel_size - 1 each = 4 */
+void oracle_frame_deferred(OracleState *st, const float *features)
+{
+  const int max_buffer_size = (CONV_K - 1) + (CONV_K - 1);
+  if (st->feature_buffer_fill == max_buffer_size)
+    memmove(st->feature_buffer, &st->feature_buffer[NB_FEATURES], (max_buffer_size - 1) * NB_FEATURES * sizeof(float));
+  else
+    st->feature_buffer_fill++;
+  memcpy(&st->feature_buffer[(st->feature_buffer_fill - 1) * NB_FEATURES], features, NB_FEATURES * sizeof(float));
+}
+
+/* lpcnet.c:134-144 run_frame_network_flush: outputs into locals */
+void oracle_frame_flush(OracleState *st)
+{
+  for (int i = 0; i < st->feature_buffer_fill; i++) {
+    float lpc[LPC_ORDER], gru_a_condition[3 * NA], gru_b_condition[3 * NB];
+    run_frame_network(st, gru_a_condition, gru_b_condition, lpc, &st->feature_buffer[i * NB_FEATURES]);
+  }
+  st->feature_buffer_fill = 0;
+}
+
+/* lpcnet.c:226-233 lpcnet_reset_signal */
+void oracle_reset_signal(OracleState *st)
+{
+  st->deemph_mem = 0;
+  st->last_exc = st->k->lin2ulaw(0.f);
+  memset(st->last_sig, 0, sizeof(st->last_sig));
+  memset(st->gru_a_state, 0, sizeof(st->gru_a_state));
+  memset(st->gru_b_state, 0, sizeof(st->gru_b_state));
+}
+
+/* The PLC's struct copies (lpcnet_plc.c:223,230): a snapshot of the whole
+ * state into / out of caller memory of oracle_state_size() bytes. */
+int oracle_state_size(void) { return (int)sizeof(OracleState); }
+void oracle_state_save(const OracleState *st, void *buf) { memcpy(buf, st, sizeof(OracleState)); }
+void oracle_state_restore(OracleState *st, const void *buf) { memcpy(st, buf, sizeof(OracleState)); }
+
+/* ------------------------------------------------------------------------ */
+/* 1.6 kb/s decoder.  Parity unpinned by a reference build: lpcnet_dec.c and
+ * common.c include lpcnet_private.h -> the generated nnet_data.h, and the
+ * codebooks are generated data (ceps_codebooks.c) absent from the tree. */
+
+typedef struct {
+  int byte_pos, bit_pos, max_bytes;
+  const unsigned char *chars;
+} unpacker;
+
+/* lpcnet_dec.c:52-72 bits_unpack */
+static unsigned bits_unpack(unpacker *bits, int nb_bits)
+{
+  unsigned d = 0;
+  while (nb_bits) {
+    if (bits->byte_pos == bits->max_bytes) return 0;
+    d <<= 1;
+    d |= (bits->chars[bits->byte_pos] >> (8 - 1 - bits->bit_pos)) & 1;
+    bits->bit_pos++;
+    if (bits->bit_pos == 8) {
+      bits->bit_pos = 0;
+      bits->byte_pos++;
+    }
+    nb_bits--;
+  }
+  return d;
+}
+
+/* common.c:36-56 single_interp */
+static void single_interp(float *x, const float *left, const float *right, int id)
+{
+  float pred[3 * NB_BANDS];
+  for (int i = 0; i < NB_BANDS; i++) pred[i] = .5f * (left[i] + right[i]);
+  for (int i = 0; i < NB_BANDS; i++) pred[NB_BANDS + i] = left[i];
+  for (int i = 0; i < NB_BANDS; i++) pred[2 * NB_BANDS + i] = right[i];
+  for (int i = 0; i < NB_BANDS; i++) x[i] = pred[id * NB_BANDS + i];
+}
+
+/* common.c:58-65 perform_double_interp */
+static void perform_double_interp(float features[4][NB_TOTAL_FEATURES], const float *mem, int best_id)
+{
+  best_id += (best_id >= 7); /* FORBIDDEN_INTERP, lpcnet_private.h:23 */
+  int id0 = best_id / 3, id1 = best_id % 3;
+  single_interp(features[0], mem, features[1], id0);
+  single_interp(features[2], features[1], features[3], id1);
+}
+
+/* lpcnet_dec.c:81-156 decode_packet.  -1 if the model has no codebooks. */
+int oracle_decode_packet(OracleState *st, const unsigned char *buf, float *feat /* [4][NB_TOTAL_FEATURES] */)
+{
+  float(*features)[NB_TOTAL_FEATURES] = (float(*)[NB_TOTAL_FEATURES])feat;
+  if (!st->cb1 || !st->cb2 || !st->cb3 || !st->cbd) return -1;
+  unpacker bits = {0, 0, 8, buf};
+  int c0_id = bits_unpack(&bits, 7);
+  int main_pitch = bits_unpack(&bits, 6);
+  int modulation = bits_unpack(&bits, 3);
+  int corr_id = bits_unpack(&bits, 2);
+  int vq_end[3];
+  vq_end[0] = bits_unpack(&bits, 10);
+  vq_end[1] = bits_unpack(&bits, 10);
+  vq_end[2] = bits_unpack(&bits, 10);
+  int vq_mid = bits_unpack(&bits, 13);
+  int interp_id = bits_unpack(&bits, 3);
+  int voiced = 1;
+  float frame_corr, sign;
+  for (int i = 0; i < 4; i++) memset(features[i], 0, NB_TOTAL_FEATURES * sizeof(float));
+  modulation -= 4;
+  if (modulation == -4) {
+    voiced = 0;
+    modulation = 0;
+  }
+  if (voiced) frame_corr = 0.3875f + .175f * corr_id;
+  else frame_corr = 0.0375f + .075f * corr_id;
+  for (int sub = 0; sub < 4; sub++) {
+    float p = pow(2.f, main_pitch / 21.) * 32; /* PITCH_MIN_PERIOD, lpcnet_private.h:14 */
+    p *= 1.f + modulation / 16.f / 7.f * (2 * sub - 3);
+    p = (255 < (33 > p ? 33 : p) ? 255 : (33 > p ? 33 : p)); /* MIN16(255, MAX16(33, p)) */
+    features[sub][NB_BANDS] = .02f * (p - 100.f);
+    features[sub][NB_BANDS + 1] = frame_corr - .5f;
+  }
+  features[3][0] = (c0_id - 64) / 4.f;
+  for (int i = 0; i < NB_BANDS_1; i++)
+    features[3][i + 1] = st->cb1[vq_end[0] * NB_BANDS_1 + i] + st->cb2[vq_end[1] * NB_BANDS_1 + i] +
+                         st->cb3[vq_end[2] * NB_BANDS_1 + i];
+  sign = 1;
+  if (vq_mid >= 4096) {
+    vq_mid -= 4096;
+    sign = -1;
+  }
+  for (int i = 0; i < NB_BANDS; i++) features[1][i] = sign * st->cbd[vq_mid * NB_BANDS + i];
+  if ((vq_mid & 3) < 2) {
+    for (int i = 0; i < NB_BANDS; i++) features[1][i] += .5f * (st->vq_mem[i] + features[3][i]);
+  } else if ((vq_mid & 3) == 2) {
+    for (int i = 0; i < NB_BANDS; i++) features[1][i] += st->vq_mem[i];
+  } else {
+    for (int i = 0; i < NB_BANDS; i++) features[1][i] += features[3][i];
+  }
+  perform_double_interp(features, st->vq_mem, interp_id);
+  memcpy(st->vq_mem, &features[3][0], NB_BANDS * sizeof(float));
+  return 0;
+}
+
+/* lpcnet.c:310-319 lpcnet_decode */
+int oracle_decode(OracleState *st, const unsigned char *buf, short *pcm /* [4 * FRAME_SIZE] */)
+{
+  float features[4][NB_TOTAL_FEATURES];
+  if (oracle_decode_packet(st, buf, &features[0][0])) return -1;
+  for (int k = 0; k < 4; k++) oracle_synthesize(st, features[k], &pcm[k * FRAME_SIZE], FRAME_SIZE, 0);
+  return 0;
 }

@@ -88,6 +88,23 @@ void oracle_reset(OracleState *st);
 /* lpcnet.c:273-277 lpcnet_synthesize_impl(st, features, output, N, preload) */
 void oracle_synthesize(OracleState *st, const float *features, short *output, int N, int preload);
 
+/* lpcnet.c:235-271 lpcnet_synthesize_tail_impl */
+void oracle_synthesize_tail(OracleState *st, short *output, int N, int preload);
+/* lpcnet.c:122-144 run_frame_network_deferred / _flush */
+void oracle_frame_deferred(OracleState *st, const float *features);
+void oracle_frame_flush(OracleState *st);
+/* lpcnet.c:226-233 lpcnet_reset_signal */
+void oracle_reset_signal(OracleState *st);
+/* whole-state snapshot (the PLC's LPCNetState struct copies) */
+int oracle_state_size(void);
+void oracle_state_save(const OracleState *st, void *buf);
+void oracle_state_restore(OracleState *st, const void *buf);
+/* lpcnet_dec.c:81-156 decode_packet (features [4][36]) and lpcnet.c:310-319
+ * lpcnet_decode (pcm [640]); -1 if the blob had no codebooks.  The decoder's
+ * vq_mem starts at zero (lpcnet_decoder_init). */
+int oracle_decode_packet(OracleState *st, const unsigned char *buf, float *features);
+int oracle_decode(OracleState *st, const unsigned char *buf, short *pcm);
+
 /* Model constants the reference compiles in from nnet_data.h
  * (dump_lpcnet.py:423-446): LPC_GAMMA, FEATURES_DELAY (0..4), END2END.
  * Defaults 1.0, 2, 0.  Returns -1 for an unsupported value. */

@@ -19,10 +19,11 @@ def ensure_built():
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
 
 
+ORACLE_AVX2_SO = os.path.join(ROOT, "oracle", "liblpcnet_oracle_avx2.so")
+
 ensure_built()
-_ora = C.CDLL(ORACLE_SO)
 _vp, _i = C.c_void_p, C.c_int
-for name, res, args in [
+_SIGS = [
     ("oracle_port_kernels", _vp, []),
     ("oracle_set_rcp_table", None, [_vp]),
     ("oracle_rcp", C.c_float, [C.c_float]),
@@ -38,14 +39,38 @@ for name, res, args in [
     ("oracle_get_frame", None, [_vp, _vp, _vp, _vp]),
     ("oracle_frame_count", _i, [_vp]),
     ("oracle_get_state", None, [_vp, _vp, _vp]),
-]:
-    fn = getattr(_ora, name)
-    fn.restype = res
-    fn.argtypes = args
-
+    ("oracle_synthesize_tail", None, [_vp, _vp, _i, _i]),
+    ("oracle_frame_deferred", None, [_vp, _vp]),
+    ("oracle_frame_flush", None, [_vp]),
+    ("oracle_reset_signal", None, [_vp]),
+    ("oracle_state_size", _i, []),
+    ("oracle_state_save", None, [_vp, _vp]),
+    ("oracle_state_restore", None, [_vp, _vp]),
+    ("oracle_decode_packet", _i, [_vp, _vp, _vp]),
+    ("oracle_decode", _i, [_vp, _vp, _vp]),
+]
 RCP_TABLE = np.fromfile(os.path.join(GOLDEN, "rcp_x86.bin"), dtype=np.uint32)
 assert RCP_TABLE.size == 2048
-_ora.oracle_set_rcp_table(RCP_TABLE.ctypes.data)
+
+
+def _bind(path):
+    lib = C.CDLL(path)
+    for name, res, args in _SIGS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    lib.oracle_set_rcp_table(RCP_TABLE.ctypes.data)
+    return lib
+
+
+_ora = _bind(ORACLE_SO)
+# the same restatement under the reference's -O3 -mavx2 -mfma flags: the CPU
+# baseline's build (bench.py cpu_baseline), bit-identical (tests/test_oracle.py)
+_ora_avx2 = _bind(ORACLE_AVX2_SO) if os.path.exists(ORACLE_AVX2_SO) else None
+
+
+def have_avx2_build() -> bool:
+    return _ora_avx2 is not None
 
 _ref = None
 if os.path.exists(REF_SO):
@@ -101,15 +126,18 @@ def kernel_table(k: C.c_void_p):
 class Oracle:
     """One reference-semantics synthesis stream on the CPU."""
 
-    def __init__(self, blob: bytes, variant: int = 0, kernels=None, constants=None):
+    def __init__(self, blob: bytes, variant: int = 0, kernels=None, constants=None, avx2_build: bool = False):
         """constants: (LPC_GAMMA, FEATURES_DELAY, END2END) of the model, the
-        #defines the reference compiles in from nnet_data.h; default (1.0, 2, 0)."""
-        self._st = _ora.oracle_create(blob, len(blob), variant, kernels or port_kernels())
+        #defines the reference compiles in from nnet_data.h; default (1.0, 2, 0).
+        avx2_build: the -O3 -mavx2 -mfma build of the restatement (CPU baseline)."""
+        lib = _ora_avx2 if avx2_build and _ora_avx2 is not None else _ora
+        self._lib = lib
+        self._st = lib.oracle_create(blob, len(blob), variant, kernels or lib.oracle_port_kernels())
         if not self._st:
             raise ValueError("oracle_create: blob rejected")
         if constants is not None:
             g, d, e = constants
-            if _ora.oracle_set_constants(self._st, g, int(d), int(e)) != 0:
+            if self._lib.oracle_set_constants(self._st, g, int(d), int(e)) != 0:
                 raise ValueError("oracle_set_constants: unsupported value")
 
     def synthesize(self, features: np.ndarray, n: int = 160, preload: np.ndarray | None = None,
@@ -123,36 +151,74 @@ class Oracle:
             lg = np.zeros((n, 8), np.float32)
             ex = np.zeros(n, np.int32)
             rw = np.zeros((n, 2), np.uint32)
-            _ora.oracle_set_trace(self._st, lg.ctypes.data, ex.ctypes.data, rw.ctypes.data)
-        _ora.oracle_synthesize(self._st, f.ctypes.data, out.ctypes.data, n, npre)
+            self._lib.oracle_set_trace(self._st, lg.ctypes.data, ex.ctypes.data, rw.ctypes.data)
+        self._lib.oracle_synthesize(self._st, f.ctypes.data, out.ctypes.data, n, npre)
         out = out[:n]
         if trace:
-            _ora.oracle_set_trace(self._st, None, None, None)
+            self._lib.oracle_set_trace(self._st, None, None, None)
             return out, lg, ex, rw
+        return out
+
+    def synthesize_tail(self, pcm: np.ndarray, preload: int = 0) -> np.ndarray:
+        """lpcnet_synthesize_tail_impl: pcm [N] (first ``preload`` teacher-forced)."""
+        out = np.ascontiguousarray(pcm, np.int16).copy()
+        self._lib.oracle_synthesize_tail(self._st, out.ctypes.data, out.size, preload)
+        return out
+
+    def frame_deferred(self, features: np.ndarray) -> None:
+        f = np.ascontiguousarray(np.asarray(features, np.float32)[:20])
+        self._lib.oracle_frame_deferred(self._st, f.ctypes.data)
+
+    def frame_flush(self) -> None:
+        self._lib.oracle_frame_flush(self._st)
+
+    def reset_signal(self) -> None:
+        self._lib.oracle_reset_signal(self._st)
+
+    def save(self) -> bytes:
+        buf = C.create_string_buffer(self._lib.oracle_state_size())
+        self._lib.oracle_state_save(self._st, buf)
+        return buf.raw
+
+    def restore(self, state: bytes) -> None:
+        self._lib.oracle_state_restore(self._st, state)
+
+    def decode_packet(self, packet: bytes) -> np.ndarray:
+        """decode_packet (lpcnet_dec.c:81-156): 8 bytes -> features [4, 36]."""
+        f = np.zeros((4, 36), np.float32)
+        if self._lib.oracle_decode_packet(self._st, bytes(packet), f.ctypes.data) != 0:
+            raise ValueError("blob has no codebooks")
+        return f
+
+    def decode(self, packet: bytes) -> np.ndarray:
+        """lpcnet_decode (lpcnet.c:310-319): 8 bytes -> pcm [640]."""
+        out = np.zeros(640, np.int16)
+        if self._lib.oracle_decode(self._st, bytes(packet), out.ctypes.data) != 0:
+            raise ValueError("blob has no codebooks")
         return out
 
     def frame(self):
         a = np.zeros(1152, np.float32)
         b = np.zeros(48, np.float32)
         lpc = np.zeros(16, np.float32)
-        _ora.oracle_get_frame(self._st, a.ctypes.data, b.ctypes.data, lpc.ctypes.data)
+        self._lib.oracle_get_frame(self._st, a.ctypes.data, b.ctypes.data, lpc.ctypes.data)
         return a, b, lpc
 
     def state(self):
         a = np.zeros(384, np.float32)
         b = np.zeros(16, np.float32)
-        _ora.oracle_get_state(self._st, a.ctypes.data, b.ctypes.data)
+        self._lib.oracle_get_state(self._st, a.ctypes.data, b.ctypes.data)
         return a, b
 
     def frame_count(self) -> int:
-        return _ora.oracle_frame_count(self._st)
+        return self._lib.oracle_frame_count(self._st)
 
     def reset(self):
-        _ora.oracle_reset(self._st)
+        self._lib.oracle_reset(self._st)
 
     def __del__(self):
         try:
-            _ora.oracle_destroy(self._st)
+            self._lib.oracle_destroy(self._st)
         except Exception:
             pass
 

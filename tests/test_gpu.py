@@ -408,9 +408,10 @@ def test_restore_refuses_out_of_range_last_exc(require_gpu, blobs):
     for f in range(3):
         b.synthesize(allf[f])
     snap = bytes(b.save_state(7))
-    # StreamState ends ..., deemph_mem, last_exc, frame_count (= 3 now), rng[4], pad
+    # StreamState ends ..., deemph_mem, last_exc, frame_count (= 3 now), rng[4], vq_mem[18] (0), pad[3]
     i32 = lambda o: struct.unpack_from("<i", snap, o)[0]  # noqa: E731
-    offs = [o for o in range(len(snap) - 64, len(snap) - 8, 4) if i32(o + 4) == 3 and 0 <= i32(o) <= 255]
+    offs = [o for o in range(len(snap) - 160, len(snap) - 8, 4)
+            if i32(o + 4) == 3 and 0 <= i32(o) <= 255 and snap[o + 24:o + 24 + 72] == bytes(72)]
     assert len(offs) == 1, offs
     off = offs[0]
     for v in (256, -1, 1 << 20):

@@ -111,3 +111,52 @@ def test_device_numerics_rejects_bad_arguments():
     assert L.lib.lpcnet_mi355x_device_numerics(0, 99, None, None, 1) == -1
     assert L.lib.lpcnet_mi355x_device_numerics(0, 0, None, None, 4) == -1
     assert L.lib.lpcnet_mi355x_device_numerics(0, 0, None, None, 0) == 0
+
+
+def test_stale_registry_entry_is_dropped():
+    """An LPCNetState embedded in caller memory that is freed without
+    lpcnet_destroy leaves a registry entry; memory reused at that address
+    (garbage, or another handle's bytes) must start a fresh handle -- the
+    registry's record, never the memory, says what to release."""
+    import ctypes as C
+    n = L.lib.lpcnet_get_size()
+    raw = (C.c_ubyte * n)()
+    p = C.cast(raw, C.c_void_p)
+    assert L.lib.lpcnet_init(p) == 0
+    snap = bytes(raw)
+    C.memmove(raw, b"\x5a" * n, n)  # the block reused for something else
+    assert L.lib.lpcnet_init(p) == 0  # stale entry dropped, fresh handle
+    assert bytes(raw) != snap  # a new token
+    C.memmove(raw, snap, n)  # the old handle's bytes: not the live token any more
+    assert L.lib.lpcnet_init(p) == 0
+    L.lib.lpcnet_mi355x_deinit(p)
+    assert bytes(raw[:4]) == b"\0\0\0\0"
+    L.lib.lpcnet_mi355x_deinit(p)  # idempotent
+    # an embedded decoder state: init / destroy without a device
+    d = L.lib.lpcnet_decoder_create()
+    assert d and L.lib.lpcnet_decoder_init(d) == 0
+    L.lib.lpcnet_decoder_destroy(d)
+
+
+def test_handle_entry_points_fail_cleanly_without_model():
+    """The reference-internal entry points on a handle with no model bound:
+    silence out, no crash, no device work."""
+    import ctypes as C
+    st = L.lib.lpcnet_create()
+    out = np.full(160, 7, np.int16)
+    f = np.zeros(20, np.float32)
+    L.lib.lpcnet_synthesize_impl(st, f.ctypes.data, out.ctypes.data, 160, 10)
+    assert np.all(out == 0)
+    out[:] = 7
+    L.lib.lpcnet_synthesize_tail_impl(st, out.ctypes.data, 160, 0)
+    assert np.all(out == 0)
+    L.lib.run_frame_network_deferred(st, f.ctypes.data)
+    L.lib.run_frame_network_flush(st)
+    L.lib.lpcnet_reset_signal(st)
+    buf = C.create_string_buffer(L.lib.lpcnet_mi355x_state_size())
+    assert L.lib.lpcnet_mi355x_state_save(st, buf) == -1
+    d = L.lib.lpcnet_decoder_create()
+    pcm = np.full(640, 3, np.int16)
+    assert L.lib.lpcnet_decode(d, bytes(8), pcm.ctypes.data) == -1 and np.all(pcm == 0)
+    L.lib.lpcnet_decoder_destroy(d)
+    L.lib.lpcnet_destroy(st)

@@ -7,6 +7,12 @@ cd "$R"
 mkdir -p gpurun_out
 STEPS=${STEPS:-20}
 TAG=${TAG:-run}
+if [ -n "$FIRST" ]; then
+  # the tests of this change first (fail fast), then the whole suite
+  timeout -k 10 ${TEST_TIMEOUT:-780} python -u -m pytest $FIRST -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread > gpurun_out/pt_first_$TAG.log 2>&1
+  rc=$?; echo "pytest(first) rc=$rc"; tail -4 gpurun_out/pt_first_$TAG.log
+  [ $rc -eq 0 ] || exit $rc
+fi
 if [ -z "$NOTEST" ]; then
   timeout -k 10 ${TEST_TIMEOUT:-780} python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread ${K:+-k "$K"} > gpurun_out/pt_$TAG.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pt_$TAG.log
