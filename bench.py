@@ -292,26 +292,53 @@ def cpu_model():
     return "unknown"
 
 
+def physical_cores():
+    """Distinct (physical id, core id) pairs of /proc/cpuinfo (SMT siblings
+    counted once); os.cpu_count() if unreadable."""
+    ids, phys = set(), None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                ids.add((phys, line.split(":", 1)[1].strip()))
+    except OSError:
+        pass
+    return len(ids) or os.cpu_count()
+
+
+# BASELINE.md section 3: the calibration of this baseline against the
+# compiled reference, measured in the build container (tools/cpu_calibrate.py)
+CPU_CALIBRATION = ("restatement glue at the reference's -O3 -mavx2 -mfma flags + the reference's own kernels: "
+                   "189-233 K samples/s/core on the build container's Xeon = 0.88-1.09x the survey's "
+                   "-O2 -mavx2 -mfma reference build (214 K) and 0.65-0.80x its -O3 -march=native build (290 K), "
+                   "two runs of best-of-6 alternating rounds (BASELINE.md section 3, profiles/r04/cpu_calibration.json)")
+
+
 def cpu_baseline(seconds, variant=0):
     """The reference's own AVX2 kernels (oracle/_ref, compiled from the
-    reference sources) driven by the oracle's lpcnet.c/nnet.c restatement,
-    one stream per worker thread, one worker pinned per host core this
-    process may use.  On the GPU box that is the harness's CPU share for one
-    GPU (OMP_NUM_THREADS = 16 there; the affinity mask shows the whole
-    machine), so `per_core` is the number to scale to a node.  variant 1:
-    the reference's --disable-dot-product build (fp32 GRU weights,
+    reference sources) driven by the oracle's lpcnet.c/nnet.c restatement
+    built with the reference's optimisation flags (oracle/Makefile
+    BASE_CFLAGS: -O3 -mavx2 -mfma -ffp-contract=off; bit-identical to the
+    portable build), one stream per worker thread, one worker pinned per host
+    core this process may use.  On the GPU box that is the harness's CPU
+    share for one GPU (OMP_NUM_THREADS = 16 there; the affinity mask shows
+    the whole machine), so `per_core` is the number to scale to a node
+    (`node_extrapolated`: per_core x the machine's physical cores).
+    variant 1: the reference's --disable-dot-product build (fp32 GRU weights,
     vec_avx.h:861-904 compiled with DISABLE_DOT_PROD), beside configs[1]'s
     batch1_fp32 line."""
     import lpcnet_amd as L
     import oracle_lib as O
     kind = "reference" if O.have_ref() else "port"
     kernels = O.ref_kernels() if O.have_ref() else None
+    avx2 = O.have_avx2_build()
     blob = L.synthetic_model(1, variant)
     cpus = sorted(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     threads = max(1, min(len(cpus), share) if share > 0 else len(cpus))
     # warm the lazily built tables on one thread first
-    O.Oracle(blob, variant, kernels).synthesize(L.synthetic_features(0, 1)[0])
+    O.Oracle(blob, variant, kernels, avx2_build=avx2).synthesize(L.synthetic_features(0, 1)[0])
     frames_done = [0] * threads
     stop = [False]
 
@@ -320,7 +347,7 @@ def cpu_baseline(seconds, variant=0):
             os.sched_setaffinity(threading.get_native_id(), {cpus[t % len(cpus)]})
         except OSError:
             pass
-        o = O.Oracle(blob, variant, kernels)
+        o = O.Oracle(blob, variant, kernels, avx2_build=avx2)
         f = L.synthetic_features(1000 + t, 64)
         k = 0
         while not stop[0]:
@@ -339,14 +366,16 @@ def cpu_baseline(seconds, variant=0):
     dt = time.perf_counter() - t0
     frames = sum(frames_done)
     value = frames * 160 / dt
+    pc = physical_cores()
     return {"value": value, "unit": "samples/s", "cores": threads, "kind": kind,
-            "per_core": value / threads, "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-            "affinity_cpus": len(cpus),
+            "per_core": value / threads, "physical_cores": pc, "node_extrapolated": value / threads * pc,
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": len(cpus),
+            "glue_build": "-O3 -mavx2 -mfma -ffp-contract=off" if avx2 else "-O2 portable",
             "sample": f"{threads} pinned threads x 1 stream each (one per core of this process's CPU share), "
                       f"{'fp32 (--disable-dot-product)' if variant else 'int8'} "
                       f"synthetic model, {frames} frames in {dt:.1f}s "
                       f"({'reference vec_avx.h/kiss99/freq.c kernels compiled from /root/reference/src' if kind == 'reference' else 'portable oracle'}"
-                      f" + oracle restatement of lpcnet.c/nnet.c; restatement/reference speed ratio: BASELINE.md section 3)"}
+                      f" + oracle restatement of lpcnet.c/nnet.c; calibration: {CPU_CALIBRATION})"}
 
 
 def side_line(L, blob, B, args, config, variant_name):

@@ -123,6 +123,22 @@ def test_oracle_stream_golden(name, variant):
             assert np.array_equal(bits(np.concatenate([a, b, lpc])), bits(G["frame_cond"][fr]))
 
 
+@pytest.mark.parametrize("name,variant", [("streams_int8", 0), ("streams_fp32", 1), ("streams_int8_sat", 0)])
+def test_baseline_build_bit_identical(name, variant):
+    """The CPU baseline's build of the restatement (-O3 -mavx2 -mfma
+    -ffp-contract=off, oracle/Makefile BASE_CFLAGS) with the reference's
+    compiled kernels reproduces the golden PCM: the flags change speed only."""
+    import lpcnet_amd as L
+    if not O.have_avx2_build():
+        pytest.skip("liblpcnet_oracle_avx2.so not built")
+    G = np.load(os.path.join(O.GOLDEN, name + ".npz"))
+    blob = L.synthetic_model(1, variant, name.endswith("_sat"))
+    for kernels in ([None, O.ref_kernels()] if O.have_ref() else [None]):
+        o = O.Oracle(blob, variant, kernels, avx2_build=True)
+        for fr in range(10):
+            assert np.array_equal(o.synthesize(G["features"][1, fr]), G["pcm"][1, fr]), fr
+
+
 CONST_FIXTURES = ["streams_int8_g092_d3", "streams_int8_g095_d0", "streams_int8_e2e_g09_d1", "streams_fp32_g092_d4"]
 
 
