@@ -124,7 +124,8 @@ def max_over_ranks(dist, x):
     return float(t.item())
 
 
-def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1, preheat_ms=0.0, kernel=0):
+def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1, preheat_ms=0.0, kernel=0,
+              rcp_table=None):
     """Returns (seconds for `steps` frames, kernel ms / launches, info, pcm).
     The timed region carries HIP events around each sample-kernel launch
     (timers=1; 2 adds the frame kernel); the frame kernel's own time comes
@@ -137,6 +138,8 @@ def run_batch(L, blob, B, stream_base, warmup, steps, timed_dist=None, timers=1,
     b = L.LPCNetBatch(B, int(os.environ.get("LOCAL_RANK", "0")) % ndev, blob)
     if kernel:
         b.set_kernel(kernel)
+    if rcp_table is not None:
+        b.set_rcp_table(rcp_table)
     d_feat = b.device_alloc(feats.nbytes)
     d_pcm = b.device_alloc((F + extra) * B * 160 * 2)
     b.h2d(d_feat, feats)
@@ -441,9 +444,27 @@ def skewed_lines(L, args):
     its throughput at the three batch sizes of the default-model lines."""
     blob = L.synthetic_model(1, L.VARIANT_INT8, skewed=True)
     out = {}
-    for B in (1, 256, 1024):
+    for B in (1, 256, 1024, 2048, 8192):
         nf = max(args.steps, 20)
         dt, (k, n, kf, _, _), info, _ = run_batch(L, blob, B, 0, args.warmup, nf, None, args.timers, args.preheat_ms)
+        out[f"b{B}"] = {"samples_per_s": B * nf * 160 / dt, "sample_kernel_ms_per_frame": k / max(kf, 1),
+                        "kernel": info.kernel_name, "quad_path": info.quad_path}
+    return out
+
+
+def host_rcpps_lines(L, args):
+    """Same-box numerics: the engine with THIS host's rcpps table
+    (lpcnet_batch_set_rcp_table; LPCNET_RCP=host for the drop-in API), i.e.
+    the PCM the reference prints on this CPU (vec_avx.h:408,437), beside the
+    default (Intel-table) numerics of the headline, at 1 and 1024 streams:
+    the fast kernels' table-only forms."""
+    tab, bad = L.host_rcp_table()
+    out = {"host_table_exact": bad == 0}
+    blob = L.synthetic_model(1, L.VARIANT_INT8)
+    for B in (1, 1024):
+        nf = max(args.steps, 20)
+        dt, (k, n, kf, _, _), info, _ = run_batch(L, blob, B, 0, args.warmup, nf, None, args.timers, args.preheat_ms,
+                                                  rcp_table=tab)
         out[f"b{B}"] = {"samples_per_s": B * nf * 160 / dt, "sample_kernel_ms_per_frame": k / max(kf, 1),
                         "kernel": info.kernel_name, "quad_path": info.quad_path}
     return out
@@ -526,8 +547,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_batch1:
         out["skewed_int8"] = skewed_lines(L, args)
         out["lockstep"] = lockstep_lines(L, args)
+        out["host_rcpps"] = host_rcpps_lines(L, args)
     if rank == 0 and world == 1 and not args.no_capacity:
         out["capacity"] = capacity(L, blob, args)
+        # the same ladder on the trained-like (Sparsify) sparsity pattern
+        out["capacity_skewed"] = capacity(L, L.synthetic_model(1, L.VARIANT_INT8, skewed=True), args)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         # beside batch1_fp32 (configs[1]): the reference's fp32 build on the same cores

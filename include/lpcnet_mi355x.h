@@ -282,6 +282,7 @@ LPCNET_EXPORT void lpcnet_reset_signal(LPCNetState *st);
 /* A handle's whole synthesis state (device stream state + the deferred
  * feature buffer): buf holds lpcnet_mi355x_state_size() bytes.  Restore
  * refuses a buffer this engine cannot have produced.  0 / -1. */
+#define LPCNET_MI355X_STATE_MAX 16384 /* >= lpcnet_mi355x_state_size() (stack buffers) */
 LPCNET_EXPORT int lpcnet_mi355x_state_size(void);
 LPCNET_EXPORT int lpcnet_mi355x_state_save(LPCNetState *st, void *buf);
 LPCNET_EXPORT int lpcnet_mi355x_state_restore(LPCNetState *st, const void *buf);

@@ -145,7 +145,7 @@ class ModelInfo(C.Structure):
         if self.quad_path == 4:
             return f"mf_kernel<{self.streams_per_workgroup}, 0, {lr}>"
         if self.quad_path == 6:
-            return "mf2_kernel<4>"
+            return f"mf2_kernel<4, {lr}>"
         if self.quad_path == 5:
             return f"fp_kernel<0, {lr}>"
         quad = "true" if self.quad_path == 1 else "false"

@@ -107,7 +107,7 @@ __device__ __forceinline__ void ck_tile(const float *__restrict__ W, const float
  * (lpcnet.c:119: incremented while below 1000) */
 __device__ __forceinline__ int ck_fc(int fc0, int f) { return fc0 >= 1000 ? fc0 : min(fc0 + f, 1000); }
 
-template <int NFR, int SC>
+template <int NFR, int SC, bool HWR>
 __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
 {
   using G = CkGeom<NFR, SC>;
@@ -180,10 +180,10 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   for (int j = 0; j < NCT; j++) {
     const bool clr = ck_fc(fcs[cs[j]], cf[j]) < 1;
     float4 t;
-    t.x = clr ? 0.f : tanh_x86<true>(acc[j][0], rcp);
-    t.y = clr ? 0.f : tanh_x86<true>(acc[j][1], rcp);
-    t.z = clr ? 0.f : tanh_x86<true>(acc[j][2], rcp);
-    t.w = clr ? 0.f : tanh_x86<true>(acc[j][3], rcp);
+    t.x = clr ? 0.f : tanh_x86<HWR>(acc[j][0], rcp);
+    t.y = clr ? 0.f : tanh_x86<HWR>(acc[j][1], rcp);
+    t.z = clr ? 0.f : tanh_x86<HWR>(acc[j][2], rcp);
+    t.w = clr ? 0.f : tanh_x86<HWR>(acc[j][3], rcp);
     *(float4 *)&c1[cs[j] * G::C1_SS + (cf[j] + 2) * CK_RS + 16 * wave + 4 * g] = t;
   }
   __syncthreads();
@@ -201,10 +201,10 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   for (int j = 0; j < NCT; j++) {
     const bool clr = ck_fc(fcs[cs[j]], cf[j]) < D;
     float4 t;
-    t.x = clr ? 0.f : tanh_x86<true>(acc[j][0], rcp);
-    t.y = clr ? 0.f : tanh_x86<true>(acc[j][1], rcp);
-    t.z = clr ? 0.f : tanh_x86<true>(acc[j][2], rcp);
-    t.w = clr ? 0.f : tanh_x86<true>(acc[j][3], rcp);
+    t.x = clr ? 0.f : tanh_x86<HWR>(acc[j][0], rcp);
+    t.y = clr ? 0.f : tanh_x86<HWR>(acc[j][1], rcp);
+    t.z = clr ? 0.f : tanh_x86<HWR>(acc[j][2], rcp);
+    t.w = clr ? 0.f : tanh_x86<HWR>(acc[j][3], rcp);
     *(float4 *)&ya[(16 * j + r) * CK_RS + 16 * wave + 4 * g] = t;
   }
   __syncthreads();
@@ -216,15 +216,15 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
 #pragma unroll
   for (int j = 0; j < NCT; j++)
     *(float4 *)&yb[(16 * j + r) * CK_RS + 16 * wave + 4 * g] =
-        make_float4(tanh_x86<true>(acc[j][0], rcp), tanh_x86<true>(acc[j][1], rcp), tanh_x86<true>(acc[j][2], rcp),
-                    tanh_x86<true>(acc[j][3], rcp));
+        make_float4(tanh_x86<HWR>(acc[j][0], rcp), tanh_x86<HWR>(acc[j][1], rcp), tanh_x86<HWR>(acc[j][2], rcp),
+                    tanh_x86<HWR>(acc[j][3], rcp));
   __syncthreads();
   ck_tile<COND, COND, COND, CK_RS>(A.dense2_w, A.dense2_b, wave, yb, xb, acc);
 #pragma unroll
   for (int j = 0; j < NCT; j++)
     *(float4 *)&ya[(16 * j + r) * CK_RS + 16 * wave + 4 * g] =
-        make_float4(tanh_x86<true>(acc[j][0], rcp), tanh_x86<true>(acc[j][1], rcp), tanh_x86<true>(acc[j][2], rcp),
-                    tanh_x86<true>(acc[j][3], rcp));
+        make_float4(tanh_x86<HWR>(acc[j][0], rcp), tanh_x86<HWR>(acc[j][1], rcp), tanh_x86<HWR>(acc[j][2], rcp),
+                    tanh_x86<HWR>(acc[j][3], rcp));
   __syncthreads();
 
   /* END2END models (lpcnet.c:104,107-108): each frame's LPC = rc2lpc of the
@@ -309,20 +309,20 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   if (tid < G::SC && s0 + tid < B) A.st[s0 + tid].frame_count = ck_fc(fcs[tid], n);
 }
 
-template <int NFR, int SC>
+template <int NFR, int SC, bool HWR>
 static int launch_chunk_t(const FrameArgs &a, void *stream)
 {
   using G = CkGeom<NFR, SC>;
   const int bytes = G::FLOATS * 4;
-  if (ensure_dyn_lds((const void *)chunk_kernel<NFR, SC>, bytes)) return -1;
+  if (ensure_dyn_lds((const void *)chunk_kernel<NFR, SC, HWR>, bytes)) return -1;
   const int grid = (a.nstreams + G::SC - 1) / G::SC;
-  hipLaunchKernelGGL((chunk_kernel<NFR, SC>), dim3(grid), dim3(CK_THREADS), bytes, (hipStream_t)stream, a);
+  hipLaunchKernelGGL((chunk_kernel<NFR, SC, HWR>), dim3(grid), dim3(CK_THREADS), bytes, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_chunk(const FrameArgs &a, void *stream)
+template <bool HWR>
+static int launch_chunk_h(const FrameArgs &a, void *stream)
 {
-  if (a.nframes < 1 || a.nframes > LPC_CHUNK || !a.cond) return -1;
   /* a workgroup's time grows with its column tiles, and the grid runs in
    * rounds of one workgroup per CU: 17..24 frames as 20 or 24 frames x 4
    * streams (5 or 6 column tiles) when that turns two rounds of 32 x 2 into
@@ -330,11 +330,19 @@ int launch_chunk(const FrameArgs &a, void *stream)
   const int cus = current_device_cus();
   /* estimated time: rounds of workgroups x column tiles per workgroup */
   auto cost = [&](int sc, int nct) { return ((a.nstreams + sc - 1) / sc + cus - 1) / cus * nct; };
-  if (a.nframes <= 8) return launch_chunk_t<8, 8>(a, stream);
-  if (a.nframes <= 16) return launch_chunk_t<16, 4>(a, stream);
-  if (a.nframes <= 20 && cost(4, 5) < cost(2, 4)) return launch_chunk_t<20, 4>(a, stream);
-  if (a.nframes <= 24 && cost(4, 6) < cost(2, 4)) return launch_chunk_t<24, 4>(a, stream);
-  return launch_chunk_t<32, 2>(a, stream);
+  if (a.nframes <= 8) return launch_chunk_t<8, 8, HWR>(a, stream);
+  if (a.nframes <= 16) return launch_chunk_t<16, 4, HWR>(a, stream);
+  if (a.nframes <= 20 && cost(4, 5) < cost(2, 4)) return launch_chunk_t<20, 4, HWR>(a, stream);
+  if (a.nframes <= 24 && cost(4, 6) < cost(2, 4)) return launch_chunk_t<24, 4, HWR>(a, stream);
+  return launch_chunk_t<32, 2, HWR>(a, stream);
+}
+
+int launch_chunk(const FrameArgs &a, void *stream)
+{
+  if (a.nframes < 1 || a.nframes > LPC_CHUNK || !a.cond) return -1;
+  /* tanh through the hardware reciprocal, or through the LDS table when the
+   * batch carries another host's rcpps (same-box parity) */
+  return a.rcp_hw ? launch_chunk_h<true>(a, stream) : launch_chunk_h<false>(a, stream);
 }
 
 }  // namespace lpcnet_mi355x

@@ -439,9 +439,10 @@ void choose_kernel(LPCNetBatch *b)
   b->info.mfma_ops_per_group_sample = 0;
   int mode = b->kernel_mode;
   if (mode == 0) mode = b->fp_ok ? 5 : (b->mf_ok ? 4 : 1);
-  /* a custom rcpps table: every activation through the table (the fast
-   * kernels' hardware-reciprocal shortcut is proven for the Intel table only) */
-  if (b->rcp_custom) mode = 1;
+  /* a custom rcpps table (another host's, same-box parity): the fast
+   * kernels run their table-only forms (the hardware-reciprocal shortcut is
+   * proven for the Intel table only) */
+  b->sa.rcp_hw = b->fa.rcp_hw = b->rcp_custom ? 0 : 1;
   if (mode == 5 && b->fp_ok && fp_lds_bytes() <= 160 * 1024) {
     b->fp = true;
     b->info.streams_per_workgroup = 1;
@@ -459,11 +460,11 @@ void choose_kernel(LPCNetBatch *b)
      * (LPCNET_MF2=0 off, =1 at any batch size) */
     const char *e2 = getenv("LPCNET_MF2");
     const bool want2 = e2 ? atoi(e2) != 0 : b->B >= MF2_MIN_STREAMS;
-    if (want2 && !b->sa.mf_split && mf2_lds_bytes(4) <= 160 * 1024) {
+    if (want2 && mf2_lds_bytes(4, b->sa.mf_split) <= 160 * 1024) {
       b->mf2 = true;
       b->info.mfma_ops_per_group_sample = 2 * (b->mf_ga_ops + b->mf_gb_ops);
       b->info.streams_per_workgroup = 8;
-      b->info.lds_bytes = mf2_lds_bytes(4);
+      b->info.lds_bytes = mf2_lds_bytes(4, b->sa.mf_split);
       b->info.quad_path = 6;
     }
     return;
@@ -662,6 +663,7 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
     P.pieces[g].clear();
     for (int u = 0; u < NUB; u++) {
       const int K = (int)ga[g * NUB + u].size();
+      if (K > T[g] && (F[g] <= 0 || (K - T[g] + F[g] - 1) / F[g] > 15)) return -1; /* the owner word counts 4 bits of pieces */
       for (int t0 = T[g]; t0 < K; t0 += F[g]) P.pieces[g].push_back(MfPiece{u, t0, std::min(K, t0 + F[g])});
     }
     if ((int)P.pieces[g].size() > NLG) return -1;
@@ -1168,8 +1170,9 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     const std::vector<int> &perm = plan.perm;
     mft.assign((size_t)SAMPLE_WAVES * MF_LANE_U32 * 64, 0);
     mf_units.assign((size_t)SAMPLE_WAVES * 64, 0);
-    mf_frow.assign((size_t)3 * SAMPLE_WAVES * 64, NA); /* NA: no hosted piece (a dummy row) */
+    mf_frow.assign((size_t)2 * SAMPLE_WAVES * 64, 0); /* [host word][owner word] per lane (mf_common.h) */
     sa.mf_split = plan.split ? 1 : 0;
+    for (int w = 0; w < SAMPLE_WAVES; w++) sa.mf_kmax[w] = 0;
     for (int w = 0; w < SAMPLE_WAVES; w++) {
       auto word = [&](int k, int l) -> uint32_t & { return mft[((size_t)w * MF_LANE_U32 + k) * 64 + l]; };
       sa.mf_nzr[w] = plan.nzr[w];
@@ -1201,7 +1204,8 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
                 rbk[k] = g * (NA / 8) + pc.unit;
                 t0k[k] = pc.t0;
                 t1 = pc.t1;
-                for (int r = 0; r < 8; r++) mf_frow[((size_t)g * SAMPLE_WAVES + w) * 64 + 8 * (4 * half + k) + r] = 8 * pc.unit + r;
+                for (int r = 0; r < 8; r++)
+                  mf_frow[(size_t)w * 64 + 8 * (4 * half + k) + r] |= (uint32_t)(plan.host[g][lg] | 64) << (7 * g);
               }
               if (rbk[k] >= 0) lists[k].assign(ga_blocks[rbk[k]].begin() + t0k[k], ga_blocks[rbk[k]].begin() + t1);
             }
@@ -1222,13 +1226,26 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
         }
       }
     }
-    /* bit 16 of a lane's entry of gate g: its own row (unit mf_units[lane])
-     * has hosted pieces there, whose sums it merges after barrier X */
+    /* owner word of a lane: per gate the first piece of its own row
+     * (unit mf_units[lane]) and their number -- a row's pieces are
+     * consecutive (mf_layout emits them row by row) */
     for (int g = 0; g < 3; g++) {
-      std::vector<char> has(NA / 8, 0);
-      for (const MfPiece &pc : plan.pieces[g]) has[pc.unit] = 1;
-      for (int t = 0; t < SAMPLE_WAVES * 64; t++)
-        if (has[mf_units[t] / 8]) mf_frow[(size_t)g * SAMPLE_WAVES * 64 + t] |= 1 << 16;
+      std::vector<int> first(NA / 8, -1), cnt(NA / 8, 0);
+      for (int p = 0; p < (int)plan.pieces[g].size(); p++) {
+        const int u = plan.pieces[g][p].unit;
+        if (first[u] < 0) first[u] = p;
+        cnt[u]++;
+      }
+      for (int t = 0; t < SAMPLE_WAVES * 64; t++) {
+        const int u = mf_units[t] / 8;
+        if (cnt[u]) mf_frow[(size_t)SAMPLE_WAVES * 64 + t] |= (uint32_t)(first[u] | cnt[u] << 6) << (10 * g);
+      }
+      /* per wave: the most pieces any of its rows has (the merge's trip count) */
+      for (int w = 0; w < SAMPLE_WAVES; w++) {
+        int m = 0;
+        for (int j = 0; j < 8; j++) m = std::max(m, cnt[perm[8 * w + j]]);
+        sa.mf_kmax[w] |= m << (4 * g);
+      }
     }
     /* GRU_B: dense A tiles, lane l = row 16g + l%16, k = 64kt + 16(l/16) + byte */
     std::vector<int8_t> dense((size_t)GB_ROWS * NA, 0), drec((size_t)GB_ROWS * NB, 0);
@@ -2805,6 +2822,8 @@ struct HandleSnapshot {
   float fbuf[MAX_FEATURE_BUFFER][NF];
 };
 
+static_assert(sizeof(HandleSnapshot) <= LPCNET_MI355X_STATE_MAX, "LPCNET_MI355X_STATE_MAX too small");
+
 static std::mutex g_live_mu;
 static std::unordered_map<const LPCNetState *, Handle *> g_live;
 
@@ -3148,7 +3167,9 @@ LPCNET_EXPORT int lpcnet_decode(LPCNetDecState *st, const unsigned char *buf, sh
 LPCNET_EXPORT int lpcnet_mi355x_validate_model(const unsigned char *data, int len)
 {
   LPCNetBatch tmp;
-  tmp.B = 1;
+  /* diagnostics: the batch size whose kernel plan to build (LPCNET_VERBOSE prints it) */
+  const char *v = getenv("LPCNET_VALIDATE_STREAMS");
+  tmp.B = v ? std::max(1, atoi(v)) : 1;
   return load_model(&tmp, data, len, false);
 }
 

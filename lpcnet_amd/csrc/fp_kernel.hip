@@ -249,7 +249,7 @@ __device__ __forceinline__ float h_chain_stream(const float4 *hw /* lane's slot 
 
 /* DIAG: 0 the production kernel, 1 with the logit / excitation trace, 2
  * with the s_memtime phase stamps (mf_kernel.hip) */
-template <int DIAG, bool LONG>
+template <int DIAG, bool LONG, bool HWR>
 __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
 {
   constexpr bool TRACE = DIAG == 1;
@@ -423,9 +423,9 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
       stamp(2);
       /* compute_sparse_gru elementwise (nnet.c:442-447) */
       float zr2[2] = {acc.x, acc.y};
-      sigmoid_x86_n<2, true>(zr2, rcp);
+      sigmoid_x86_n<2, HWR>(zr2, rcp);
       float hv[1] = {hpre * zr2[1] + inh};
-      tanh_x86_n<1, true>(hv, rcp);
+      tanh_x86_n<1, HWR>(hv, rcp);
       st = zr2[0] * st + (1.f - zr2[0]) * hv[0];
       ((float *)xn)[i] = st;
       if (lane == 0) flag_publish(done + g, n + 1);
@@ -571,9 +571,9 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
         const float hin = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(y), __float_as_uint(y), false, false)[1]);
         const float hrec = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(y2), __float_as_uint(y2), false, false)[1]);
         float zr2[2] = {zin, rin};
-        sigmoid_x86_n<2, true>(zr2, rcp);
+        sigmoid_x86_n<2, HWR>(zr2, rcp);
         float hh[1] = {hin + hrec * zr2[1]};
-        tanh_x86_n<1, true>(hh, rcp);
+        tanh_x86_n<1, HWR>(hh, rcp);
         sbv = zr2[0] * sbv + (1.f - zr2[0]) * hh[0];
         if (lane < NB) sbuf[lane] = sbv;
       }
@@ -587,7 +587,7 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
         }
       }
       stamp(3);
-      const WalkOut R = dual_fc_walk_p<TRACE>(F, t03, t47, xv, pred, lpd, lpr, n < A.preload ? pcmbuf + n : nullptr, deemph);
+      const WalkOut R = dual_fc_walk_p<TRACE, false, HWR>(F, t03, t47, xv, pred, lpd, lpr, n < A.preload ? pcmbuf + n : nullptr, deemph);
       if (n + 1 < A.N && lane == 0) {
         *(int4 *)ix = make_int4(R.su, R.pu, R.exc, 0);
         flag_publish(ixseq, n + 2);
@@ -632,17 +632,24 @@ __global__ __launch_bounds__(FP_THREADS) void fp_kernel(SampleArgs A)
   }
 }
 
-template <int DIAG, bool LONG>
+template <int DIAG, bool LONG, bool HWR = true>
 static int launch_fp_t(const SampleArgs &a, hipStream_t stream)
 {
-  if (ensure_dyn_lds((const void *)fp_kernel<DIAG, LONG>, 160 * 1024 - IMG_VAR)) return -1;
-  hipLaunchKernelGGL((fp_kernel<DIAG, LONG>), dim3(warm_grid(a.nstreams, a.nstreams)), dim3(FP_THREADS), fp_lds_bytes() - IMG_VAR, stream, a);
+  if (ensure_dyn_lds((const void *)fp_kernel<DIAG, LONG, HWR>, 160 * 1024 - IMG_VAR)) return -1;
+  hipLaunchKernelGGL((fp_kernel<DIAG, LONG, HWR>), dim3(warm_grid(a.nstreams, a.nstreams)), dim3(FP_THREADS), fp_lds_bytes() - IMG_VAR, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_fp(const SampleArgs &a, void *stream)
 {
   hipStream_t st = (hipStream_t)stream;
+  if (!a.rcp_hw) {
+    /* another host's rcpps table: every activation through it (production
+     * and trace forms; no stamped build) */
+    if (a.stamps) return -1;
+    if (a.fp_long) return a.trace_logits ? launch_fp_t<1, true, false>(a, st) : launch_fp_t<0, true, false>(a, st);
+    return a.trace_logits ? launch_fp_t<1, false, false>(a, st) : launch_fp_t<0, false, false>(a, st);
+  }
   if (a.fp_long)
     return a.trace_logits ? launch_fp_t<1, true>(a, st) : a.stamps ? launch_fp_t<2, true>(a, st) : launch_fp_t<0, true>(a, st);
   return a.trace_logits ? launch_fp_t<1, false>(a, st) : a.stamps ? launch_fp_t<2, false>(a, st) : launch_fp_t<0, false>(a, st);

@@ -160,6 +160,7 @@ struct FrameArgs {
    * run_frame_network_flush does (lpcnet.c:134-144): conv memories, LPC ring
    * and frame_count advance, the state's conditioning and lpc stay */
   int keep_cond;
+  int rcp_hw; /* chunk_kernel: hardware-reciprocal tanh allowed (see SampleArgs::rcp_hw) */
 };
 
 struct SampleArgs {
@@ -219,7 +220,8 @@ struct SampleArgs {
   int mf_split;
   int mf_nfzr[SAMPLE_WAVES];
   int mf_nfh[SAMPLE_WAVES];
-  const int *mf_frow;
+  const int *mf_frow;                /* [2][SAMPLE_THREADS]: host / owner words (mf_common.h) */
+  int mf_kmax[SAMPLE_WAVES];         /* per GRU_A wave: its lanes' maximum pieces per row, 4 bits per gate */
   const uint4 *mf_gb;
   const float4 *fp_zr, *fp_h, *fp_gb; /* fp_kernel tables (see FP_ZF) */
   const uint32_t *fp_off;
@@ -238,6 +240,9 @@ struct SampleArgs {
   unsigned long long *stamps; /* optional diagnostics [grid][STAMP_WAVES][16] s_memtime sums */
   float *trace_logits;   /* optional [B][N][8] */
   int *trace_exc;        /* optional [B][N] */
+  int rcp_hw;            /* 1: the latency chains may use the hardware-reciprocal rcpps (equal to the
+                            default Intel table only); 0: every activation through the LDS table
+                            (lpcnet_batch_set_rcp_table with another host's table) */
   int *status;           /* device view of the batch's pinned status word: a
                             kernel that aborts sets bits (STATUS_*), the host
                             checks after every sync */
@@ -317,9 +322,9 @@ constexpr int CHUNK_MIN_FRAMES = 4; /* shorter runs use the per-frame kernel */
 int mf_lds_bytes(int S, int split);
 int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream);
 /* Large batches: two groups of S streams per workgroup, half a sample
- * apart (mf2_kernel.hip); no preload / trace / stamps / split models. */
+ * apart (mf2_kernel.hip); no preload / trace / stamps. */
 constexpr int MF2_MIN_STREAMS = 2048; /* automatic choice of mf2_kernel from this batch size */
-int mf2_lds_bytes(int S);
+int mf2_lds_bytes(int S, int split);
 int launch_mf2(const SampleArgs &a, int S, void *stream);
 /* fp32 latency kernel: one stream per workgroup, LDS flags instead of
  * workgroup barriers (fp32 models within the FP_* limits, dense GRU_B). */

@@ -19,8 +19,8 @@
  *               samplers:    GRU_B + walk of A's sample t -> ix_A(t+1)
  * one workgroup barrier per phase, so both roles work in every phase and the
  * GRU_A register tables and GRU_B tiles serve 2S streams.  Used for batches
- * of >= 2048 streams (a launch still fills every CU); preload, trace, stamps
- * and split models take mf_kernel.  Samples t run over all frames of a
+ * of >= 2048 streams (a launch still fills every CU); preload, trace and
+ * stamps take mf_kernel.  Samples t run over all frames of a
  * multi-frame launch (SampleArgs::nframes); the samplers write each output
  * sample straight to global memory.
  */
@@ -49,11 +49,21 @@ struct Mf2Lds {
   static constexpr int okw = 2 * 2 * 8 * 4;         /* range words [frame parity][group][GRU_A wave] */
   static constexpr int gbw = 3 * 64 * 16;           /* GRU_B recurrent A tiles [3][64] */
   static constexpr int total = x + xb + sb + ix + lpc + cnd + gbs + gbr + okw + gbw;
+  static constexpr int part = 2 * MfHs<S>::ints * 4; /* split models: hosted-sum slots per group (mf_common.h) */
 };
 
-int mf2_lds_bytes(int S) { return IMG_VAR + (S == 4 ? Mf2Lds<4>::total : Mf2Lds<2>::total); }
+int mf2_lds_bytes(int S, int split)
+{
+  return IMG_VAR + (S == 4 ? Mf2Lds<4>::total + (split ? Mf2Lds<4>::part : 0)
+                           : Mf2Lds<2>::total + (split ? Mf2Lds<2>::part : 0));
+}
 
-template <int S>
+/* SPLIT: models with block rows beyond the register tables (trained
+ * Sparsify masks, engine.cpp mf_plan) -- each lane group also runs a hosted
+ * piece of another row, whose partial sums reach the row's owner through
+ * private LDS slots (mf_common.h): one set per group, written by the group's
+ * recurrent product and read by its next elementwise step, a barrier apart */
+template <int S, bool SPLIT, bool HWR>
 __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
 {
   extern __shared__ uint4 lds4[];
@@ -70,6 +80,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
   int *gbr = gbs + 2 * 2 * S * GB_ROWS;
   int *okw = gbr + GB_ROWS;
   v4i *gbw = (v4i *)(okw + 32);
+  int *hs = (int *)(gbw + 3 * 64); /* SPLIT: [2 groups][hosted-sum slots] */
   __shared__ uint4 img_s[IMG_VAR / 16];
   unsigned char *img = (unsigned char *)img_s;
 
@@ -158,14 +169,27 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
       for (int t = 0; t < MF_HMAX / 2; t++) oh[t] = off(2 * MF_ZMAX + 2 * t) | (off(2 * MF_ZMAX + 2 * t + 1) << 16);
     }
     const int nzr = A.mf_nzr[wv], nh = A.mf_nh[wv];
+    const int nfzr = SPLIT ? A.mf_nfzr[wv] : 0, nfh = SPLIT ? A.mf_nfh[wv] : 0;
+    /* split models: this lane's hosted pieces and its own row's pieces (mf_common.h) */
+    uint32_t fhost = 0, fown = 0;
+    if constexpr (SPLIT) {
+      fhost = (uint32_t)A.mf_frow[tid];
+      fown = (uint32_t)A.mf_frow[SAMPLE_THREADS + tid];
+    }
     __syncthreads(); /* image in LDS */
     for (int g = 0; g < 2; g++)
       for (int s = 0; s < S; s++) xa[(g * S + s) * MF_XSTR + i] = (unsigned char)quant_s8_state(st[g][s]);
+    if constexpr (SPLIT) /* the never-written zero slots of both groups (mf_common.h) */
+      for (int e = tid; e < 2 * 3 * 8 * S; e += SAMPLE_THREADS) {
+        const int g = e / (3 * 8 * S), q = e % (3 * 8 * S);
+        hs[g * MfHs<S>::ints + ((q / (8 * S)) * (MF_MAX_PIECES + 1) + MF_MAX_PIECES) * 8 * S + q % (8 * S)] = 0;
+      }
     __syncthreads(); /* initial q(h_A) of both groups, ix of both groups, seeds */
 
     /* one group's recurrent terms, for its next elementwise step */
     float az[S], ar[S]; /* the recurrent sums as exact floats (ga_elementwise) */
     float tz[S], tr[S], hpre[S];
+    int iaz[S], iar[S], iah[S]; /* SPLIT: the own sums as int32 until the hosted partial sums are merged */
     auto recurrent = [&](auto gc) {
       constexpr int g = decltype(gc)::value;
       const unsigned char *xg = xa + g * S * MF_XSTR;
@@ -173,6 +197,29 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
       mf_opaque(oz);
       mf_opaque(orr);
       mf_opaque(oh);
+      if constexpr (SPLIT) {
+        /* own groups into v*, the hosted piece into f*, to the owner of its
+         * row through this group's private LDS slots (exact int32 adds) */
+        v4i fz = {0, 0, 0, 0}, fr = {0, 0, 0, 0}, fh[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+        uint32_t xz[4], xr[4], xh[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          xz[k] = mf_x(xg, oz, k);
+          xr[k] = mf_x(xg, orr, k);
+          xh[k] = mf_x(xg, oh, k);
+        }
+        mf_zr_split(xg, wz, wr, oz, orr, nzr, nfzr, xz, xr, vz[0], vr[0], fz, fr);
+        mf_h_split(xg, wh, oh, nh, nfh, xh, vh, fh);
+        mf_host_store<S>(hs + g * MfHs<S>::ints, fhost, tid & 7, fz, fr, fh);
+        for (int s = 0; s < S; s++) {
+          iaz[s] = vz[0][s];
+          iar[s] = vr[0][s];
+          iah[s] = (vh[0][s] + vh[1][s]) + cvt_rne((bh + dh * st[g][s]) * kScale); /* int32 sums associate */
+          tz[s] = bz + dz * st[g][s];
+          tr[s] = br + dr * st[g][s];
+        }
+        return;
+      }
       switch (nzr * 16 + nh) {
 #define MF_CASE(Z, H)                                 \
   case Z * 16 + H:                                    \
@@ -215,6 +262,18 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
           e[s][q] = *(const float *)(b1 + o1 + q * NA * 4u);
           e[s][3 + q] = *(const float *)(b2 + o2 + q * NA * 4u);
           e[s][6 + q] = *(const float *)(b3 + o3 + q * NA * 4u);
+        }
+      }
+      if constexpr (SPLIT) {
+        /* the hosted pieces' partial sums of this thread's row (stored by
+         * the group's recurrent product a barrier ago) */
+        int hadd[S];
+        for (int s = 0; s < S; s++) hadd[s] = 0;
+        mf_owner_merge<S>(hs + g * MfHs<S>::ints, fown, A.mf_kmax[wv], tid & 7, iaz, iar, hadd);
+        for (int s = 0; s < S; s++) {
+          hpre[s] = (float)(iah[s] + hadd[s]) * kScale1;
+          az[s] = (float)iaz[s];
+          ar[s] = (float)iar[s];
         }
       }
       int stub = 0;
@@ -370,9 +429,9 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
       for (int kt = 0; kt < 6; kt++) acc[2] = mfma16(xk[kt], wt[12 + kt], acc[2]);
       float zrb[2] = {(float)acc[0][0] * kScale1 + (float)accr[0][0] * kScale1,
                       (float)acc[1][0] * kScale1 + (float)accr[1][0] * kScale1};
-      sigmoid_x86_fin_n<2, true>(zrb, rcp);
+      sigmoid_x86_fin_n<2, HWR>(zrb, rcp);
       float hh[1] = {(float)acc[2][0] * kScale1 + ((float)accr[2][0] * kScale1) * zrb[1]};
-      tanh_x86_fin_n<1, true>(hh, rcp); /* |hh| < 2^19: int32 sums x 2^-14 */
+      tanh_x86_fin_n<1, HWR>(hh, rcp); /* |hh| < 2^19: int32 sums x 2^-14 */
       sbv[g] = zrb[0] * sbv[g] + (1.f - zrb[0]) * hh[0];
       if (gown) sbuf[(g * S + gs) * NB + gu] = sbv[g];
       __builtin_amdgcn_wave_barrier();
@@ -395,7 +454,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
         }
       }
       /* (the select-free walk of mf_kernel measured 1 % slower here) */
-      const WalkOut R = dual_fc_walk<false>(F, t03, t47, xv, pred[g], lsr[g], lpr, nullptr, deemph[g]);
+      const WalkOut R = dual_fc_walk<false, false, HWR>(F, t03, t47, xv, pred[g], lsr[g], lpr, nullptr, deemph[g]);
       if (samp_w && hl == 0) *(int4 *)(ix + (g * S + ms) * 4) = ix_word(R.su, R.pu, R.exc);
       /* bookkeeping (lpcnet.c:262-269) and the output sample */
 #pragma unroll
@@ -445,19 +504,26 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
   }
 }
 
-template <int S>
+template <int S, bool SPLIT, bool HWR>
 static int launch_mf2_t(const SampleArgs &a, hipStream_t stream)
 {
-  if (ensure_dyn_lds((const void *)mf2_kernel<S>, 160 * 1024 - IMG_VAR)) return -1;
+  if (ensure_dyn_lds((const void *)mf2_kernel<S, SPLIT, HWR>, 160 * 1024 - IMG_VAR)) return -1;
   const int grid = (a.nstreams + 2 * S - 1) / (2 * S);
-  hipLaunchKernelGGL((mf2_kernel<S>), dim3(grid), dim3(MF_THREADS), mf2_lds_bytes(S) - IMG_VAR, stream, a);
+  hipLaunchKernelGGL((mf2_kernel<S, SPLIT, HWR>), dim3(grid), dim3(MF_THREADS), mf2_lds_bytes(S, SPLIT) - IMG_VAR, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <bool HWR>
+static int launch_mf2_h(const SampleArgs &a, int S, hipStream_t st)
+{
+  if (a.mf_split) return S == 4 ? launch_mf2_t<4, true, HWR>(a, st) : launch_mf2_t<2, true, HWR>(a, st);
+  return S == 4 ? launch_mf2_t<4, false, HWR>(a, st) : launch_mf2_t<2, false, HWR>(a, st);
 }
 
 int launch_mf2(const SampleArgs &a, int S, void *stream)
 {
   hipStream_t st = (hipStream_t)stream;
-  return S == 4 ? launch_mf2_t<4>(a, st) : launch_mf2_t<2>(a, st);
+  return a.rcp_hw ? launch_mf2_h<true>(a, S, st) : launch_mf2_h<false>(a, S, st);
 }
 
 }  // namespace lpcnet_mi355x

@@ -48,24 +48,26 @@ struct FcLane {
    * (nnet.c:196-205: sum1 + sum2 through DPP quad_perm [1,0,3,2]).  FIN:
    * the node sum is known finite and below 2^60 (SampleArgs::fc_fin and
    * GRU_B states within [-2, 2]), tanh without its flush and NaN selects */
-  template <bool FIN = false>
+  template <bool FIN = false, bool HW = true>
   __device__ __forceinline__ float node_logit(float bias, float factor, const float *w, const float (&xv)[NB]) const
   {
     float sum = bias;
 #pragma unroll
     for (int j = 0; j < NB; j++) sum = sum + w[j] * xv[j];
-    return node_logit_tail<FIN>(sum, factor);
+    return node_logit_tail<FIN, HW>(sum, factor);
   }
 
   /* the same from the finished dot product sum */
-  template <bool FIN = false>
+  /* HW: the hardware-reciprocal rcpps (proven equal to the Intel table
+   * only); false: the LDS table (any host's rcpps, same-box parity) */
+  template <bool FIN = false, bool HW = true>
   __device__ __forceinline__ float node_logit_tail(float sum, float factor) const
   {
     float v[1] = {sum};
     if constexpr (FIN)
-      tanh_x86_fin_n<1, true>(v, rcp);
+      tanh_x86_fin_n<1, HW>(v, rcp);
     else
-      tanh_x86_n<1, true>(v, rcp);
+      tanh_x86_n<1, HW>(v, rcp);
     const float vv = factor * v[0];
     const float o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(vv), 0xB1, 0xF, 0xF, false));
     return ch2 ? o + vv : vv + o;
@@ -136,7 +138,7 @@ struct WalkNoStamp {
  * reference multiplies and subtracts separately (no FMA), so a product
  * computed ahead -- before barrier Y, off the sampler chain -- is the same
  * float */
-template <bool TRACE, bool FIN = false, class ST = WalkNoStamp>
+template <bool TRACE, bool FIN = false, bool HW = true, class ST = WalkNoStamp>
 __device__ __forceinline__ WalkOut dual_fc_walk_p(const FcLane &F, float t03, float t47, const float (&xv)[NB], float pred,
                                                   const float (&lprod)[NLPC], const float (&lpr)[NLPC], const short *teach,
                                                   float deemph, ST st = ST())
@@ -144,7 +146,7 @@ __device__ __forceinline__ WalkOut dual_fc_walk_p(const FcLane &F, float t03, fl
   WalkOut R;
   int val;
   {
-    const float l = F.node_logit<FIN>(F.b03, F.f03, F.w03, xv);
+    const float l = F.node_logit<FIN, HW>(F.b03, F.f03, F.w03, xv);
     st(2, l);
     val = walk_round(half_bits(__ballot(t03 < l), F.half));
     if (TRACE) {
@@ -197,7 +199,7 @@ __device__ __forceinline__ WalkOut dual_fc_walk_p(const FcLane &F, float t03, fl
   int sp_u = lin2ulaw_x86(F.hl < 16 ? sp_pcm : sp_pred);
   int low;
   {
-    const float l = F.node_logit_tail<FIN>(sum, f47);
+    const float l = F.node_logit_tail<FIN, HW>(sum, f47);
     st(15, l);
     /* the speculation is needed only when not teaching: pin it before the
      * ballot, or the compiler sinks it into that branch, after the round */
@@ -241,7 +243,7 @@ __device__ __forceinline__ WalkOut dual_fc_walk_p(const FcLane &F, float t03, fl
 }
 
 /* the same with the products formed here, beside round 1's dependent chain */
-template <bool TRACE, bool FIN = false, class ST = WalkNoStamp>
+template <bool TRACE, bool FIN = false, bool HW = true, class ST = WalkNoStamp>
 __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, float t47, const float (&xv)[NB], float pred,
                                                 const float (&lsr)[NLPC], const float (&lpr)[NLPC], const short *teach,
                                                 float deemph, ST st = ST())
@@ -250,7 +252,7 @@ __device__ __forceinline__ WalkOut dual_fc_walk(const FcLane &F, float t03, floa
   lprod[0] = 0.f;
 #pragma unroll
   for (int j = 1; j < NLPC; j++) lprod[j] = lsr[j - 1] * lpr[j];
-  return dual_fc_walk_p<TRACE, FIN, ST>(F, t03, t47, xv, pred, lprod, lpr, teach, deemph, st);
+  return dual_fc_walk_p<TRACE, FIN, HW, ST>(F, t03, t47, xv, pred, lprod, lpr, teach, deemph, st);
 }
 
 }  // namespace lpcnet_mi355x

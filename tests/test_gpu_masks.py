@@ -137,3 +137,47 @@ def test_skewed_other_kernels(require_gpu, variant, sat, kernel, B):
     for s in (0, B - 1):
         exp = O.synth_stream(blob, allf[:, s], variant)
         assert np.array_equal(out[:, s], exp), s
+
+
+def test_forced_split_mf2_matches_golden(require_gpu, monkeypatch):
+    """mf2_kernel's split form (two staggered groups, one hosted-sum buffer
+    per group) on the default model, every row split, at the fixture's three
+    streams (LPCNET_MF2=1 takes mf2 at any batch): PCM and final GRU states
+    == the golden fixture."""
+    monkeypatch.setenv("LPCNET_MF_FORCE_SPLIT", "1")
+    monkeypatch.setenv("LPCNET_MF2", "1")
+    G = np.load(os.path.join(O.GOLDEN, "streams_int8.npz"))
+    b = L.LPCNetBatch(len(G["streams"]), 0, L.synthetic_model(1, 0))
+    info = b.info()
+    assert info.quad_path == 6 and info.long_rows == 1, (info.quad_path, info.long_rows)
+    for fr in range(G["pcm"].shape[1]):
+        assert np.array_equal(b.synthesize(G["features"][:, fr, :20]), G["pcm"][:, fr]), fr
+    for s in range(len(G["streams"])):
+        st = b.get_state(s)
+        if s == 0:
+            assert np.array_equal(bits(st["gru_a_state"]), bits(G["final_gru_a_state"]))
+            assert np.array_equal(bits(st["gru_b_state"]), bits(G["final_gru_b_state"]))
+
+
+@pytest.mark.parametrize("B,check", [(2048, (0, 1031, 2047)), (8192, (0, 4099, 8191))])
+def test_skewed_int8_on_mf2(require_gpu, B, check):
+    """Skewed (trained-like) int8 model at mf2_kernel's batch sizes: the
+    automatic kernel is mf2_kernel's split form; host frames then the
+    chunked multi-frame device path, PCM and final states against the
+    oracle."""
+    F = 7
+    blob = L.synthetic_model(1, 0, skewed=True)
+    b = L.LPCNetBatch(B, 0, blob)
+    info = b.info()
+    assert info.quad_path == 6 and info.long_rows == 1, info.quad_path
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    out = np.concatenate([np.stack([b.synthesize(allf[f]) for f in range(3)]), _frames(b, allf, 3, F)], 0)
+    assert np.abs(out[3:].astype(np.float64)).mean() > 100
+    for s in check:
+        o = O.Oracle(blob, 0)
+        exp = np.stack([o.synthesize(allf[f, s]) for f in range(F)])
+        assert np.array_equal(out[:, s], exp), s
+        a, g = o.state()
+        st = b.get_state(s)
+        assert np.array_equal(bits(st["gru_a_state"]), bits(a)), s
+        assert np.array_equal(bits(st["gru_b_state"]), bits(g)), s

@@ -32,8 +32,8 @@ def test_engine_with_host_rcpps_matches_live_reference(require_gpu, variant):
     allf = np.stack([feats(s, F) for s in range(B)], 1)
     b = L.LPCNetBatch(B, 0, blob)
     b.set_rcp_table(tab)
-    if not intel:
-        assert b.info().quad_path in (0, 1)  # every activation through the table
+    # the fast kernels in their table-only form (every activation through the table)
+    assert b.info().quad_path == (5 if variant else 4)
     refs = [O.Oracle(blob, variant, O.ref_kernels()) for _ in range(B)]  # live reference kernels, this CPU
     ports = [O.Oracle(blob, variant) for _ in range(B)]                  # the Intel table (golden numerics)
     differ = 0
@@ -53,3 +53,33 @@ def test_engine_with_host_rcpps_matches_live_reference(require_gpu, variant):
     # back to the default table: the Intel-table numerics of the golden fixtures
     b.set_rcp_table(None)
     assert b.info().quad_path in ((5,) if variant else (4,))
+
+
+@pytest.mark.skipif(not O.have_ref(), reason="oracle/_ref (the reference's compiled kernels) not built")
+@pytest.mark.parametrize("B,check", [(1024, (0, 513, 1023)), (2048, (0, 1031, 2047))])
+def test_host_rcpps_fast_kernels_at_scale(require_gpu, B, check):
+    """The table-only forms of the batched path with this host's rcpps:
+    chunked frame network (chunk_kernel, LDS-table tanh), multi-frame
+    mf_kernel<4> at 1024 streams and mf2_kernel at 2048, against the
+    reference's kernels running live on this CPU (three streams each)."""
+    tab, bad = L.host_rcp_table()
+    assert bad == 0
+    blob = L.synthetic_model(1, 0)
+    F = 8
+    allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
+    b = L.LPCNetBatch(B, 0, blob)
+    b.set_rcp_table(tab)
+    assert b.info().quad_path == (6 if B >= 2048 else 4)
+    df = b.device_alloc(allf.nbytes)
+    dp = b.device_alloc(F * B * 160 * 2)
+    b.h2d(df, allf)
+    b.synthesize_frames(allf, df, dp, F)
+    b.sync()
+    out = np.zeros((F, B, 160), np.int16)
+    b.d2h(out, dp)
+    b.device_free(df)
+    b.device_free(dp)
+    for s in check:
+        ref = O.Oracle(blob, 0, O.ref_kernels())
+        exp = np.stack([ref.synthesize(allf[f, s]) for f in range(F)])
+        assert np.array_equal(out[:, s], exp), s

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Throughput of the default and the skewed (trained-mask-like) int8 model at
-1, 256 and 1024 streams through bench.run_batch (the bench's own timed path),
+1, 256 and 1024 streams (or the comma list argv[1]) through bench.run_batch (the bench's own timed path),
 and the skewed/default ratio: gpurun_out/skew_tput.json."""
 import json
 import os
@@ -12,7 +12,7 @@ import bench  # noqa: E402
 import lpcnet_amd as L  # noqa: E402
 
 out = {}
-for B in (1, 256, 1024):
+for B in ([int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else (1, 256, 1024)):
     row = {}
     for name, skew in (("default", False), ("skewed", True)):
         blob = L.synthetic_model(1, L.VARIANT_INT8, skewed=skew)
@@ -22,4 +22,5 @@ for B in (1, 256, 1024):
     row["skewed_over_default"] = row["skewed"]["samples_per_s"] / row["default"]["samples_per_s"]
     out[f"b{B}"] = row
     print(f"b{B}", json.dumps(row), flush=True)
-json.dump(out, open(os.path.join(ROOT, "gpurun_out", "skew_tput.json"), "w"), indent=1)
+json.dump(out, open(os.path.join(ROOT, "gpurun_out", "skew_tput%s.json" % os.environ.get("LPCNET_LIB_VARIANT", "")), "w"),
+          indent=1)
