@@ -18,8 +18,9 @@ COMMON := $(EXTRA) -O3 -fPIC -ffp-contract=off -fno-fast-math -std=c++17 -Iinclu
 OBJS := $(BUILD)/kernels.o $(BUILD)/mf_kernel.o $(BUILD)/mf2_kernel.o $(BUILD)/fp_kernel.o $(BUILD)/selftest.o $(BUILD)/frame_kernel.o $(BUILD)/engine.o $(BUILD)/lpc_kernel.o $(BUILD)/chunk_kernel.o $(BUILD)/model_gen.o $(BUILD)/host_rcpps.o $(BUILD)/decode_kernel.o
 
 SYNTH := tools/lpcnet_synth
+DROPIN := tools/dropin_bench
 
-all: lib synth oracle
+all: lib synth dropin oracle
 
 lib: $(LIB)
 
@@ -29,6 +30,12 @@ synth: $(SYNTH)
 
 $(SYNTH): tools/lpcnet_synth.c include/lpcnet.h $(LIB)
 	$(CC) -std=c99 -O2 -Wall -Wextra -pedantic -Werror -Iinclude -o $@ $< -Llpcnet_amd -llpcnet_mi355x -Wl,-rpath,'$$ORIGIN/../lpcnet_amd'
+
+# pthread C driver of the drop-in API (many handles at once) against the batch API
+dropin: $(DROPIN)
+
+$(DROPIN): tools/dropin_bench.c include/lpcnet.h include/lpcnet_mi355x.h $(LIB)
+	$(CC) -std=c99 -O2 -Wall -Wextra -Werror -Iinclude -o $@ $< -Llpcnet_amd -llpcnet_mi355x -lpthread -Wl,-rpath,'$$ORIGIN/../lpcnet_amd'
 
 $(BUILD):
 	mkdir -p $(BUILD)
@@ -79,7 +86,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(SYNTH)
+	rm -rf $(BUILD) $(LIB) $(SYNTH) $(DROPIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib synth oracle clean
+.PHONY: all lib synth dropin oracle clean

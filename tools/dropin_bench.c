@@ -1,0 +1,140 @@
+/*
+ * dropin_bench.c -- aggregate throughput of the drop-in API from C threads.
+ *
+ *   dropin_bench <threads> <frames>
+ *
+ * T pthreads, one LPCNetState each (include/lpcnet.h: lpcnet_create,
+ * lpcnet_load_model, lpcnet_synthesize -- the reference's own calling
+ * pattern, src/lpcnet.c:213-219, 279-281), all synthesising F frames at
+ * once; the library's shared pool coalesces their calls into batched
+ * launches.  Beside it, the same T streams through one LPCNetBatch with host
+ * I/O frame by frame (lpcnet_batch_synthesize) and device-resident
+ * (lpcnet_batch_synthesize_frames).  One JSON object on stdout.  The C
+ * driver separates the pool's own cost from a Python caller's turnaround.
+ */
+#define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "lpcnet_mi355x.h"
+
+static int T, F;
+static unsigned char *blob;
+static int blob_len;
+static float *feats; /* [T][F][NB_TOTAL_FEATURES] */
+static LPCNetState **nets;
+static pthread_barrier_t go;
+
+static double now(void)
+{
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+static void *run(void *arg)
+{
+  const int t = (int)(size_t)arg;
+  short pcm[LPCNET_FRAME_SIZE];
+  pthread_barrier_wait(&go);
+  for (int f = 0; f < F; f++)
+    lpcnet_synthesize(nets[t], &feats[((size_t)t * F + f) * NB_TOTAL_FEATURES], pcm, LPCNET_FRAME_SIZE);
+  return NULL;
+}
+
+int main(int argc, char **argv)
+{
+  if (argc < 3) {
+    fprintf(stderr, "usage: %s <threads> <frames>\n", argv[0]);
+    return 2;
+  }
+  T = atoi(argv[1]);
+  F = atoi(argv[2]);
+  if (T < 1 || F < 1) return 2;
+  blob_len = lpcnet_mi355x_synthetic_model(1, LPCNET_VARIANT_INT8, 0, NULL, 0);
+  blob = malloc(blob_len);
+  lpcnet_mi355x_synthetic_model(1, LPCNET_VARIANT_INT8, 0, blob, blob_len);
+  feats = malloc(sizeof(float) * T * F * NB_TOTAL_FEATURES);
+  for (int t = 0; t < T; t++) lpcnet_mi355x_synthetic_features(t, F, &feats[(size_t)t * F * NB_TOTAL_FEATURES]);
+
+  /* drop-in handles, one per thread; one warm call each (pool, work batch) */
+  nets = malloc(sizeof(*nets) * T);
+  short warm[LPCNET_FRAME_SIZE];
+  for (int t = 0; t < T; t++) {
+    nets[t] = lpcnet_create();
+    if (!nets[t] || lpcnet_load_model(nets[t], blob, blob_len)) {
+      fprintf(stderr, "load failed: %s\n", lpcnet_mi355x_last_error());
+      return 1;
+    }
+  }
+  pthread_t *th = malloc(sizeof(*th) * T);
+  /* warm-up round: every thread one frame at once (sizes the work batch) */
+  {
+    int saveF = F;
+    F = 1;
+    pthread_barrier_init(&go, NULL, T + 1);
+    for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, run, (void *)(size_t)t);
+    pthread_barrier_wait(&go);
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    pthread_barrier_destroy(&go);
+    F = saveF;
+    for (int t = 0; t < T; t++) lpcnet_reset(nets[t]);
+  }
+  (void)warm;
+  long la0 = 0, rq0 = 0;
+  int ns = 0;
+  lpcnet_mi355x_pool_stats(nets[0], &la0, &rq0, &ns);
+  pthread_barrier_init(&go, NULL, T + 1);
+  for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, run, (void *)(size_t)t);
+  pthread_barrier_wait(&go);
+  const double t0 = now();
+  for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+  const double dt_pool = now() - t0;
+  long la = 0, rq = 0;
+  lpcnet_mi355x_pool_stats(nets[0], &la, &rq, &ns);
+  la -= la0;
+  rq -= rq0;
+  for (int t = 0; t < T; t++) lpcnet_destroy(nets[t]);
+
+  /* the same streams through one batch: host I/O frame by frame */
+  LPCNetBatch *b = lpcnet_batch_create(T, 0);
+  if (!b || lpcnet_batch_load_model(b, blob, blob_len)) {
+    fprintf(stderr, "batch failed: %s\n", lpcnet_mi355x_last_error());
+    return 1;
+  }
+  float *ff = malloc(sizeof(float) * (size_t)F * T * NB_FEATURES); /* [F][T][20] */
+  for (int f = 0; f < F; f++)
+    for (int t = 0; t < T; t++)
+      memcpy(&ff[((size_t)f * T + t) * NB_FEATURES], &feats[((size_t)t * F + f) * NB_TOTAL_FEATURES], sizeof(float) * NB_FEATURES);
+  short *pcm = malloc(sizeof(short) * (size_t)T * LPCNET_FRAME_SIZE * F);
+  lpcnet_batch_synthesize(b, ff, pcm, LPCNET_FRAME_SIZE);
+  lpcnet_batch_reset(b);
+  double t1 = now();
+  for (int f = 0; f < F; f++) lpcnet_batch_synthesize(b, &ff[(size_t)f * T * NB_FEATURES], pcm, LPCNET_FRAME_SIZE);
+  const double dt_host = now() - t1;
+  /* device-resident, all frames enqueued at once */
+  float *d_f = lpcnet_batch_device_alloc(b, sizeof(float) * (size_t)F * T * NB_FEATURES);
+  short *d_p = lpcnet_batch_device_alloc(b, sizeof(short) * (size_t)F * T * LPCNET_FRAME_SIZE);
+  lpcnet_batch_memcpy_h2d(b, d_f, ff, sizeof(float) * (size_t)F * T * NB_FEATURES);
+  lpcnet_batch_reset(b);
+  lpcnet_batch_sync(b);
+  t1 = now();
+  lpcnet_batch_synthesize_frames(b, NULL, d_f, d_p, F, LPCNET_FRAME_SIZE);
+  lpcnet_batch_sync(b);
+  const double dt_dev = now() - t1;
+  lpcnet_batch_device_free(b, d_f);
+  lpcnet_batch_device_free(b, d_p);
+  lpcnet_batch_destroy(b);
+
+  const double samples = (double)T * F * LPCNET_FRAME_SIZE;
+  printf("{\"threads\": %d, \"frames\": %d, \"dropin_c_threads\": {\"samples_per_s\": %.1f, \"launches\": %ld, "
+         "\"requests\": %ld, \"mean_coalesced_streams\": %.2f, \"ms_per_launch\": %.4f}, "
+         "\"batch_host_io\": {\"samples_per_s\": %.1f, \"ms_per_frame\": %.4f}, "
+         "\"batch_device\": {\"samples_per_s\": %.1f, \"ms_per_frame\": %.4f}}\n",
+         T, F, samples / dt_pool, la, rq, (double)rq / (la > 0 ? la : 1), 1e3 * dt_pool / (la > 0 ? la : 1),
+         samples / dt_host, 1e3 * dt_host / F, samples / dt_dev, 1e3 * dt_dev / F);
+  return 0;
+}
