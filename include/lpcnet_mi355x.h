@@ -268,6 +268,10 @@ LPCNET_EXPORT int lpcnet_mi355x_device_count(void);
  * the pool `st` belongs to: coalesced launches, handled requests, handles
  * bound.  -1 if st is not bound. */
 LPCNET_EXPORT int lpcnet_mi355x_pool_stats(const LPCNetState *st, long *launches, long *requests, int *streams);
+/* Milliseconds the pool of `st` has spent inside its coalesced launches
+ * (host I/O, state moves and kernels of each launch; the rest of a caller's
+ * wait is hand-off and thread wake-up).  -1 if st is not bound. */
+LPCNET_EXPORT double lpcnet_mi355x_pool_run_ms(const LPCNetState *st);
 /* ---- reference-internal entry points on a drop-in handle ----------------
  * The reference's PLC (lpcnet_plc.c:188-337) drives one LPCNetState through
  * these functions of lpcnet_private.h:126-132; they are exported here under

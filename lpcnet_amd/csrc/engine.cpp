@@ -25,13 +25,17 @@
 #include <cmath>
 #include <cstddef>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "lpcnet_engine.h"
@@ -663,7 +667,7 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
     P.pieces[g].clear();
     for (int u = 0; u < NUB; u++) {
       const int K = (int)ga[g * NUB + u].size();
-      if (K > T[g] && (F[g] <= 0 || (K - T[g] + F[g] - 1) / F[g] > 15)) return -1; /* the owner word counts 4 bits of pieces */
+      if (K > T[g] && F[g] <= 0) return -1;
       for (int t0 = T[g]; t0 < K; t0 += F[g]) P.pieces[g].push_back(MfPiece{u, t0, std::min(K, t0 + F[g])});
     }
     if ((int)P.pieces[g].size() > NLG) return -1;
@@ -1170,9 +1174,8 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     const std::vector<int> &perm = plan.perm;
     mft.assign((size_t)SAMPLE_WAVES * MF_LANE_U32 * 64, 0);
     mf_units.assign((size_t)SAMPLE_WAVES * 64, 0);
-    mf_frow.assign((size_t)2 * SAMPLE_WAVES * 64, 0); /* [host word][owner word] per lane (mf_common.h) */
+    mf_frow.assign((size_t)3 * SAMPLE_WAVES * 64, NA); /* NA: no hosted piece (a dummy row) */
     sa.mf_split = plan.split ? 1 : 0;
-    for (int w = 0; w < SAMPLE_WAVES; w++) sa.mf_kmax[w] = 0;
     for (int w = 0; w < SAMPLE_WAVES; w++) {
       auto word = [&](int k, int l) -> uint32_t & { return mft[((size_t)w * MF_LANE_U32 + k) * 64 + l]; };
       sa.mf_nzr[w] = plan.nzr[w];
@@ -1204,8 +1207,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
                 rbk[k] = g * (NA / 8) + pc.unit;
                 t0k[k] = pc.t0;
                 t1 = pc.t1;
-                for (int r = 0; r < 8; r++)
-                  mf_frow[(size_t)w * 64 + 8 * (4 * half + k) + r] |= (uint32_t)(plan.host[g][lg] | 64) << (7 * g);
+                for (int r = 0; r < 8; r++) mf_frow[((size_t)g * SAMPLE_WAVES + w) * 64 + 8 * (4 * half + k) + r] = 8 * pc.unit + r;
               }
               if (rbk[k] >= 0) lists[k].assign(ga_blocks[rbk[k]].begin() + t0k[k], ga_blocks[rbk[k]].begin() + t1);
             }
@@ -1226,26 +1228,13 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
         }
       }
     }
-    /* owner word of a lane: per gate the first piece of its own row
-     * (unit mf_units[lane]) and their number -- a row's pieces are
-     * consecutive (mf_layout emits them row by row) */
+    /* bit 16 of a lane's entry of gate g: its own row (unit mf_units[lane])
+     * has hosted pieces there, whose sums it merges after barrier X */
     for (int g = 0; g < 3; g++) {
-      std::vector<int> first(NA / 8, -1), cnt(NA / 8, 0);
-      for (int p = 0; p < (int)plan.pieces[g].size(); p++) {
-        const int u = plan.pieces[g][p].unit;
-        if (first[u] < 0) first[u] = p;
-        cnt[u]++;
-      }
-      for (int t = 0; t < SAMPLE_WAVES * 64; t++) {
-        const int u = mf_units[t] / 8;
-        if (cnt[u]) mf_frow[(size_t)SAMPLE_WAVES * 64 + t] |= (uint32_t)(first[u] | cnt[u] << 6) << (10 * g);
-      }
-      /* per wave: the most pieces any of its rows has (the merge's trip count) */
-      for (int w = 0; w < SAMPLE_WAVES; w++) {
-        int m = 0;
-        for (int j = 0; j < 8; j++) m = std::max(m, cnt[perm[8 * w + j]]);
-        sa.mf_kmax[w] |= m << (4 * g);
-      }
+      std::vector<char> has(NA / 8, 0);
+      for (const MfPiece &pc : plan.pieces[g]) has[pc.unit] = 1;
+      for (int t = 0; t < SAMPLE_WAVES * 64; t++)
+        if (has[mf_units[t] / 8]) mf_frow[(size_t)g * SAMPLE_WAVES * 64 + t] |= 1 << 16;
     }
     /* GRU_B: dense A tiles, lane l = row 16g + l%16, k = 64kt + 16(l/16) + byte */
     std::vector<int8_t> dense((size_t)GB_ROWS * NA, 0), drec((size_t)GB_ROWS * NB, 0);
@@ -2535,31 +2524,69 @@ struct StatePool {
     const unsigned char *packet; /* DECODE [8] */
     short *out;                  /* SYNTH / TAIL [N] (the first `preload` are input), DECODE [4 * FRAME] */
     int N, preload, nfr;
-    bool done;
-    int rc;
+    bool done = false;
+    int rc = 0;
     std::string err;
+    int lane = -1;                /* >= 0: this caller combines on that lane (taken, or handed over) */
+    uint64_t group = 0;           /* the launch this caller's previous request completed in */
+    std::thread::id tid = std::this_thread::get_id();
+    std::mutex m;                 /* guards done / lane once the caller waits: the notifier */
+    std::condition_variable cv;   /* holds it while notifying, so the caller outlives the notify */
     bool same_shape(const Req &o) const { return kind == o.kind && N == o.N && preload == o.preload && nfr == o.nfr; }
+  };
+  /* a lane: one work batch (its own HIP stream) driven by one combiner at a
+   * time; launches on different lanes run concurrently */
+  struct Lane {
+    LPCNetBatch *work = nullptr; /* work->B >= the largest coalesced call on this lane */
+    int *d_map = nullptr;        /* [map_cap] work-batch stream -> slot */
+    int map_cap = 0;
   };
   uint64_t key = 0;
   int device = 0;
   std::vector<unsigned char> blob;
-  LPCNetBatch *work = nullptr; /* work->B >= the largest coalesced call */
+  bool has_codebooks = false;
+  std::vector<Lane> lanes; /* fixed at creation */
+  std::vector<int> free_lanes;
   StreamState *d_slots = nullptr;
   int cap = 0;
   std::vector<int> free_slots;
   int refs = 0; /* handles bound + transient acquisitions; changed under g_pools_mu only */
-  int *d_map = nullptr;
-  int map_cap = 0;
   std::mutex mu;
-  std::condition_variable cv;
-  bool busy = false;
+  std::condition_variable cv;      /* no launch runs (slot I/O waiters) */
+  std::condition_variable cv_comb; /* a launch's callers are all back (gather windows) */
+  int nbusy = 0;                   /* lanes with a combiner */
+  int io_waiting = 0; /* slot I/O callers waiting for an idle pool: no new combiner then */
   std::vector<Req *> pending;
+  /* gather window: the callers of each recent launch that have not come back */
+  std::unordered_map<std::thread::id, uint64_t> last_group; /* caller -> launch its last request completed in */
+  std::unordered_map<uint64_t, int> group_away;             /* launch -> its callers not back yet */
+  std::unordered_set<uint64_t> gathering;                   /* launches a combiner is waiting for */
+  uint64_t groups = 0;
+  int window_us = 0; /* LPCNET_POOL_WINDOW_US */
   /* statistics (tests / diagnostics) */
   long launches = 0, requests = 0;
+  double run_us = 0; /* time inside pool_run (the launches themselves) */
 };
 
 static std::mutex g_pools_mu;
 static std::map<std::pair<uint64_t, int>, StatePool *> g_pools;
+
+/* Gather window of a combiner: before its launch it waits up to this long
+ * for the other callers of the launch its own previous request ran in (a
+ * thread calling lpcnet_synthesize in a loop is back within microseconds), so
+ * K looping callers keep launching together instead of fragmenting into
+ * ever smaller launches.  A launch whose callers do not all come back in time
+ * is forgotten: a caller that stopped costs one window once. */
+#ifndef POOL_WINDOW_US_DEFAULT
+#define POOL_WINDOW_US_DEFAULT 200
+#endif
+/* Lanes per pool (LPCNET_POOL_LANES): concurrent launches.  A frame step of
+ * a few hundred streams is latency-bound (a few percent of the CUs), and the
+ * wake-ups of one launch's callers take about as long as the launch, so two
+ * lanes keep the GPU busy while each group is woken and gathers again. */
+#ifndef POOL_LANES_DEFAULT
+#define POOL_LANES_DEFAULT 2
+#endif
 
 static uint64_t pool_key(const unsigned char *data, int len)
 {
@@ -2606,11 +2633,49 @@ static StatePool *pool_acquire(const unsigned char *data, int len, int device)
   p->key = key;
   p->device = device;
   p->blob.assign(data, data + len);
-  p->work = w;
+  p->has_codebooks = w->has_codebooks;
+  int nl = POOL_LANES_DEFAULT;
+  if (const char *v = getenv("LPCNET_POOL_LANES")) nl = std::min(8, std::max(1, atoi(v)));
+  p->lanes.resize(nl);
+  p->lanes[0].work = w; /* the others load the model on first use */
+  for (int k = nl - 1; k >= 0; k--) p->free_lanes.push_back(k);
   p->refs = 1;
+  if (const char *v = getenv("LPCNET_POOL_WINDOW_US")) p->window_us = std::max(0, atoi(v));
+  else p->window_us = POOL_WINDOW_US_DEFAULT;
   g_pools[{key, device}] = p;
   return p;
 }
+
+/* (lock held) free lanes and pending requests: the oldest requests' callers
+ * become combiners (each takes its lane through the hand-off) */
+static void pool_kick(StatePool *p)
+{
+  while (!p->io_waiting && !p->free_lanes.empty() && !p->pending.empty()) {
+    StatePool::Req *q = p->pending.front();
+    p->pending.erase(p->pending.begin());
+    const int lane = p->free_lanes.back();
+    p->free_lanes.pop_back();
+    p->nbusy++;
+    std::lock_guard<std::mutex> g(q->m);
+    q->lane = lane;
+    q->cv.notify_one();
+  }
+}
+
+/* Slot I/O on an idle pool: waits (lock held) until no launch runs --
+ * meanwhile the combiner does not hand its role on, so a stream of synthesis
+ * calls cannot starve it -- and on scope exit hands the pool to any pending
+ * requests */
+struct PoolIdle {
+  StatePool *p;
+  PoolIdle(StatePool *p_, std::unique_lock<std::mutex> &lk) : p(p_)
+  {
+    p->io_waiting++;
+    p->cv.wait(lk, [&] { return p->nbusy == 0; });
+    p->io_waiting--;
+  }
+  ~PoolIdle() { pool_kick(p); }
+};
 
 /* give back `slot` (if >= 0) and one reference; the last reference frees
  * the pool.  refs changes under g_pools_mu only, the lock pool_acquire holds
@@ -2620,7 +2685,7 @@ static void pool_release(StatePool *p, int slot)
 {
   if (slot >= 0) {
     std::unique_lock<std::mutex> lk(p->mu);
-    p->cv.wait(lk, [&] { return !p->busy; });
+    PoolIdle idle(p, lk);
     p->free_slots.push_back(slot);
   }
   {
@@ -2631,9 +2696,10 @@ static void pool_release(StatePool *p, int slot)
   /* unreachable now: no handle holds it and the map no longer lists it */
   if (hipSetDevice(p->device) == hipSuccess) {
     (void)hipFree(p->d_slots);
-    (void)hipFree(p->d_map);
+    for (StatePool::Lane &l : p->lanes) (void)hipFree(l.d_map);
   }
-  lpcnet_batch_destroy(p->work);
+  for (StatePool::Lane &l : p->lanes)
+    if (l.work) lpcnet_batch_destroy(l.work);
   delete p;
 }
 
@@ -2641,7 +2707,7 @@ static void pool_release(StatePool *p, int slot)
 static int pool_alloc_slot(StatePool *p, const StreamState *init)
 {
   std::unique_lock<std::mutex> lk(p->mu);
-  p->cv.wait(lk, [&] { return !p->busy; });
+  PoolIdle idle(p, lk);
   if (hipSetDevice(p->device) != hipSuccess) { set_err("hipSetDevice failed"); return -1; }
   if (p->free_slots.empty()) {
     const int ncap = std::max(4, 2 * p->cap);
@@ -2669,7 +2735,7 @@ static int pool_alloc_slot(StatePool *p, const StreamState *init)
 static int pool_slot_io(StatePool *p, int slot, StreamState *get, const StreamState *put)
 {
   std::unique_lock<std::mutex> lk(p->mu);
-  p->cv.wait(lk, [&] { return !p->busy; });
+  PoolIdle idle(p, lk);
   if (hipSetDevice(p->device) != hipSuccess) { set_err("hipSetDevice failed"); return -1; }
   if (get && hipMemcpy(get, &p->d_slots[slot], sizeof(*get), hipMemcpyDeviceToHost) != hipSuccess) {
     set_err("device copy failed");
@@ -2682,13 +2748,14 @@ static int pool_slot_io(StatePool *p, int slot, StreamState *get, const StreamSt
   return 0;
 }
 
-/* one coalesced step for requests rq (all of the same shape) */
-static int pool_run(StatePool *p, const std::vector<StatePool::Req *> &rq)
+/* one coalesced step for requests rq (all of the same shape) on lane L
+ * (only L's combiner touches L) */
+static int pool_run(StatePool *p, StatePool::Lane &L, const std::vector<StatePool::Req *> &rq)
 {
   const int n = (int)rq.size();
   const StatePool::Req &r0 = *rq[0];
   const int N = r0.N;
-  if (p->work->B < n) {
+  if (!L.work || L.work->B < n) {
     int nb = 1;
     while (nb < n) nb *= 2;
     LPCNetBatch *w = lpcnet_batch_create(nb, p->device);
@@ -2697,21 +2764,21 @@ static int pool_run(StatePool *p, const std::vector<StatePool::Req *> &rq)
       lpcnet_batch_destroy(w);
       return -1;
     }
-    lpcnet_batch_destroy(p->work);
-    p->work = w;
+    if (L.work) lpcnet_batch_destroy(L.work);
+    L.work = w;
   }
-  LPCNetBatch *w = p->work;
+  LPCNetBatch *w = L.work;
   if (w->set_device()) return -1;
-  if (p->map_cap < n) {
-    (void)hipFree(p->d_map);
-    p->d_map = nullptr;
-    HIPCHK(hipMalloc(&p->d_map, sizeof(int) * (size_t)w->B));
-    p->map_cap = w->B;
+  if (L.map_cap < n) {
+    (void)hipFree(L.d_map);
+    L.d_map = nullptr;
+    HIPCHK(hipMalloc(&L.d_map, sizeof(int) * (size_t)w->B));
+    L.map_cap = w->B;
   }
   std::vector<int> map(n);
   for (int k = 0; k < n; k++) map[k] = rq[k]->slot;
-  HIPCHK(hipMemcpyAsync(p->d_map, map.data(), sizeof(int) * n, hipMemcpyHostToDevice, w->stream));
-  if (launch_state_copy(w->d_state, p->d_slots, nullptr, p->d_map, n, w->stream)) { set_err("state gather failed"); return -1; }
+  HIPCHK(hipMemcpyAsync(L.d_map, map.data(), sizeof(int) * n, hipMemcpyHostToDevice, w->stream));
+  if (launch_state_copy(w->d_state, p->d_slots, nullptr, L.d_map, n, w->stream)) { set_err("state gather failed"); return -1; }
   /* every stream of the work batch is this call's: the multi-frame bound is its min */
   w->min_fc = 0;
   std::vector<float> feat((size_t)n * NF);
@@ -2745,44 +2812,112 @@ static int pool_run(StatePool *p, const std::vector<StatePool::Req *> &rq)
     rc = -1;
   }
   if (rc == 0) {
-    if (launch_state_copy(p->d_slots, w->d_state, p->d_map, nullptr, n, w->stream)) { set_err("state scatter failed"); return -1; }
+    if (launch_state_copy(p->d_slots, w->d_state, L.d_map, nullptr, n, w->stream)) { set_err("state scatter failed"); return -1; }
     HIPCHK(hipStreamSynchronize(w->stream));
     for (int k = 0; k < n; k++)
       if (nout > 0 && r0.kind != StatePool::FLUSH) memcpy(rq[k]->out, &pcm[(size_t)k * nout], sizeof(short) * nout);
   }
-  p->launches++;
-  p->requests += n;
   return rc;
 }
 
+/* (lock held) `tid` is back: its previous launch has one caller less away;
+ * that launch's id (0: none, or its window gave up) */
+static uint64_t pool_back(StatePool *p, std::thread::id tid)
+{
+  auto it = p->last_group.find(tid);
+  if (it == p->last_group.end()) return 0;
+  const uint64_t g = it->second;
+  p->last_group.erase(it);
+  auto ga = p->group_away.find(g);
+  if (ga == p->group_away.end()) return 0; /* that launch's window already gave up */
+  if (--ga->second == 0) {
+    p->group_away.erase(ga);
+    p->cv_comb.notify_all();
+  }
+  return g;
+}
+
+/* Flat combining over lanes with a hand-off: a caller that finds a lane free
+ * takes it, waits (the gather window) for the rest of its previous launch's
+ * callers, and runs itself plus every pending request of its shape; when it
+ * is done it hands free lanes to the oldest pending requests' callers first
+ * (the GPU idles until they launch) and then wakes exactly the callers whose
+ * requests completed -- no wake-up of every waiting thread per launch (with
+ * 256 C threads that herd on one mutex cost more than the launch) */
 static int pool_submit(StatePool *p, StatePool::Req &r)
 {
   std::unique_lock<std::mutex> lk(p->mu);
-  p->pending.push_back(&r);
-  while (!r.done) {
-    if (p->busy) {
-      p->cv.wait(lk);
-      continue;
-    }
-    /* combine: every pending request with the first one's shape */
-    p->busy = true;
-    std::vector<StatePool::Req *> mine, rest;
-    for (StatePool::Req *q : p->pending) (q->same_shape(*p->pending[0]) ? mine : rest).push_back(q);
-    p->pending.swap(rest);
+  r.group = pool_back(p, r.tid);
+  /* a caller whose launch-mates are being gathered by a combiner joins it */
+  if (p->free_lanes.empty() || p->io_waiting || (r.group && p->gathering.count(r.group))) {
+    p->pending.push_back(&r);
+    /* wait on this request's own lock (taken before the pool's is released,
+     * so a completion or hand-off cannot slip in between) */
+    std::unique_lock<std::mutex> rl(r.m);
     lk.unlock();
-    const int rc = pool_run(p, mine);
-    const std::string e = rc ? g_err : std::string();
-    lk.lock();
-    for (StatePool::Req *q : mine) {
-      q->rc = rc;
-      q->err = e;
-      q->done = true;
+    r.cv.wait(rl, [&] { return r.done || r.lane >= 0; });
+    if (r.done) {
+      rl.unlock();
+      if (r.rc) set_err(r.err);
+      return r.rc;
     }
-    p->busy = false;
-    p->cv.notify_all();
+    rl.unlock();
+    lk.lock();
+  } else {
+    r.lane = p->free_lanes.back();
+    p->free_lanes.pop_back();
+    p->nbusy++;
   }
-  if (r.rc) set_err(r.err);
-  return r.rc;
+  if (p->window_us > 0 && r.group && p->group_away.count(r.group)) {
+    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(p->window_us);
+    p->gathering.insert(r.group);
+    while (p->group_away.count(r.group))
+      if (p->cv_comb.wait_until(lk, until) == std::cv_status::timeout) {
+        /* gave up on the stragglers: forget that launch */
+        p->group_away.erase(r.group);
+        for (auto it = p->last_group.begin(); it != p->last_group.end();)
+          it = it->second == r.group ? p->last_group.erase(it) : std::next(it);
+      }
+    p->gathering.erase(r.group);
+  }
+  /* combine: this request and every pending one of its shape */
+  std::vector<StatePool::Req *> mine{&r}, rest;
+  for (StatePool::Req *q : p->pending) (q->same_shape(r) ? mine : rest).push_back(q);
+  p->pending.swap(rest);
+  StatePool::Lane &L = p->lanes[r.lane];
+  lk.unlock();
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = pool_run(p, L, mine);
+  const std::string e = rc ? g_err : std::string();
+  lk.lock();
+  p->run_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  p->launches++;
+  p->requests += (long)mine.size();
+  const uint64_t g = ++p->groups;
+  p->group_away[g] = (int)mine.size();
+  for (StatePool::Req *q : mine) {
+    q->rc = rc;
+    q->err = e;
+    if (p->last_group.count(q->tid)) pool_back(p, q->tid);
+    p->last_group[q->tid] = g;
+  }
+  p->free_lanes.push_back(r.lane);
+  p->nbusy--;
+  if (p->io_waiting) {
+    if (p->nbusy == 0) p->cv.notify_all(); /* slot I/O first; it hands the pool on when done */
+  } else {
+    pool_kick(p);
+  }
+  lk.unlock();
+  /* the wake-ups, after the hand-off: one futex call per completed caller */
+  for (size_t k = 1; k < mine.size(); k++) {
+    StatePool::Req *q = mine[k];
+    std::lock_guard<std::mutex> gq(q->m);
+    q->done = true;
+    q->cv.notify_one();
+  }
+  if (rc) set_err(e);
+  return rc;
 }
 
 /* ---- handles -------------------------------------------------------------
@@ -2970,7 +3105,7 @@ LPCNET_EXPORT int lpcnet_load_model(LPCNetState *st, const unsigned char *data, 
 
 /* run one request on st's slot; the void entry points report failure as the
  * reference cannot: silence out, lpcnet_mi355x_last_error(), one stderr line */
-static int handle_run(LPCNetState *st, StatePool::Req r, const char *what)
+static int handle_run(LPCNetState *st, StatePool::Req &r, const char *what)
 {
   Handle *h = live_handle(st);
   int rc;
@@ -3093,6 +3228,14 @@ LPCNET_EXPORT int lpcnet_mi355x_state_restore(LPCNetState *st, const void *buf)
   return 0;
 }
 
+LPCNET_EXPORT double lpcnet_mi355x_pool_run_ms(const LPCNetState *st)
+{
+  Handle *h = live_handle(st);
+  if (!h || !h->pool) return -1.0;
+  std::lock_guard<std::mutex> lk(h->pool->mu);
+  return h->pool->run_us * 1e-3;
+}
+
 LPCNET_EXPORT int lpcnet_mi355x_pool_stats(const LPCNetState *st, long *launches, long *requests, int *streams)
 {
   Handle *h = live_handle(st);
@@ -3147,7 +3290,7 @@ LPCNET_EXPORT int lpcnet_mi355x_decoder_load_model(LPCNetDecState *st, const uns
   if (!st) return -1;
   if (lpcnet_load_model(&st->lpcnet_state, data, len)) return -1;
   Handle *h = live_handle(&st->lpcnet_state);
-  if (!h || !h->pool || !h->pool->work->has_codebooks) {
+  if (!h || !h->pool || !h->pool->has_codebooks) {
     set_err("lpcnet_decode needs the ceps_codebook1/2/3 / ceps_codebook_diff4 records in the blob");
     return -1;
   }

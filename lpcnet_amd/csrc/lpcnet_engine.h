@@ -220,8 +220,7 @@ struct SampleArgs {
   int mf_split;
   int mf_nfzr[SAMPLE_WAVES];
   int mf_nfh[SAMPLE_WAVES];
-  const int *mf_frow;                /* [2][SAMPLE_THREADS]: host / owner words (mf_common.h) */
-  int mf_kmax[SAMPLE_WAVES];         /* per GRU_A wave: its lanes' maximum pieces per row, 4 bits per gate */
+  const int *mf_frow;
   const uint4 *mf_gb;
   const float4 *fp_zr, *fp_h, *fp_gb; /* fp_kernel tables (see FP_ZF) */
   const uint32_t *fp_off;

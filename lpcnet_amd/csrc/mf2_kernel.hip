@@ -49,7 +49,7 @@ struct Mf2Lds {
   static constexpr int okw = 2 * 2 * 8 * 4;         /* range words [frame parity][group][GRU_A wave] */
   static constexpr int gbw = 3 * 64 * 16;           /* GRU_B recurrent A tiles [3][64] */
   static constexpr int total = x + xb + sb + ix + lpc + cnd + gbs + gbr + okw + gbw;
-  static constexpr int part = 2 * MfHs<S>::ints * 4; /* split models: hosted-sum slots per group (mf_common.h) */
+  static constexpr int part = 2 * 3 * (NA + 1) * S * 4; /* split models: hosted partial sums [group][3][S][NA + 1] */
 };
 
 int mf2_lds_bytes(int S, int split)
@@ -61,8 +61,8 @@ int mf2_lds_bytes(int S, int split)
 /* SPLIT: models with block rows beyond the register tables (trained
  * Sparsify masks, engine.cpp mf_plan) -- each lane group also runs a hosted
  * piece of another row, whose partial sums reach the row's owner through
- * private LDS slots (mf_common.h): one set per group, written by the group's
- * recurrent product and read by its next elementwise step, a barrier apart */
+ * LDS: one buffer per group, added into by the group's recurrent product and
+ * merged (then cleared) by its next elementwise step, a barrier apart */
 template <int S, bool SPLIT, bool HWR>
 __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
 {
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
   int *gbr = gbs + 2 * 2 * S * GB_ROWS;
   int *okw = gbr + GB_ROWS;
   v4i *gbw = (v4i *)(okw + 32);
-  int *hs = (int *)(gbw + 3 * 64); /* SPLIT: [2 groups][hosted-sum slots] */
+  int *part = (int *)(gbw + 3 * 64); /* SPLIT: [2 groups][3][S][NA + 1] */
   __shared__ uint4 img_s[IMG_VAR / 16];
   unsigned char *img = (unsigned char *)img_s;
 
@@ -170,20 +170,21 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
     }
     const int nzr = A.mf_nzr[wv], nh = A.mf_nh[wv];
     const int nfzr = SPLIT ? A.mf_nfzr[wv] : 0, nfh = SPLIT ? A.mf_nfh[wv] : 0;
-    /* split models: this lane's hosted pieces and its own row's pieces (mf_common.h) */
-    uint32_t fhost = 0, fown = 0;
+    /* split models: the rows of this lane's hosted pieces (9 bits per gate,
+     * NA: none) and whether this thread's own unit has pieces to merge (bits
+     * 27..29), as in mf_kernel */
+    uint32_t frow = 0;
     if constexpr (SPLIT) {
-      fhost = (uint32_t)A.mf_frow[tid];
-      fown = (uint32_t)A.mf_frow[SAMPLE_THREADS + tid];
+      const uint32_t *fro = (const uint32_t *)A.mf_frow + tid;
+      const uint32_t e0 = fro[0], e1 = fro[SAMPLE_THREADS], e2 = fro[2 * SAMPLE_THREADS];
+      frow = (e0 & 0x1FF) | (e1 & 0x1FF) << 9 | (e2 & 0x1FF) << 18 | (e0 >> 16 & 1) << 27 | (e1 >> 16 & 1) << 28 |
+             (e2 >> 16 & 1) << 29;
     }
     __syncthreads(); /* image in LDS */
     for (int g = 0; g < 2; g++)
       for (int s = 0; s < S; s++) xa[(g * S + s) * MF_XSTR + i] = (unsigned char)quant_s8_state(st[g][s]);
-    if constexpr (SPLIT) /* the never-written zero slots of both groups (mf_common.h) */
-      for (int e = tid; e < 2 * 3 * 8 * S; e += SAMPLE_THREADS) {
-        const int g = e / (3 * 8 * S), q = e % (3 * 8 * S);
-        hs[g * MfHs<S>::ints + ((q / (8 * S)) * (MF_MAX_PIECES + 1) + MF_MAX_PIECES) * 8 * S + q % (8 * S)] = 0;
-      }
+    if constexpr (SPLIT)
+      for (int e = tid; e < 2 * 3 * (NA + 1) * S; e += SAMPLE_THREADS) part[e] = 0;
     __syncthreads(); /* initial q(h_A) of both groups, ix of both groups, seeds */
 
     /* one group's recurrent terms, for its next elementwise step */
@@ -198,8 +199,8 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
       mf_opaque(orr);
       mf_opaque(oh);
       if constexpr (SPLIT) {
-        /* own groups into v*, the hosted piece into f*, to the owner of its
-         * row through this group's private LDS slots (exact int32 adds) */
+        /* own groups into v*, the hosted piece into f*, added into the
+         * owner's row through this group's LDS buffer (exact int32 adds) */
         v4i fz = {0, 0, 0, 0}, fr = {0, 0, 0, 0}, fh[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
         uint32_t xz[4], xr[4], xh[4];
 #pragma unroll
@@ -210,7 +211,15 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
         }
         mf_zr_split(xg, wz, wr, oz, orr, nzr, nfzr, xz, xr, vz[0], vr[0], fz, fr);
         mf_h_split(xg, wh, oh, nh, nfh, xh, vh, fh);
-        mf_host_store<S>(hs + g * MfHs<S>::ints, fhost, tid & 7, fz, fr, fh);
+        uint32_t fp = frow;
+        asm volatile("" : "+v"(fp));
+        const int frz = (int)(fp & 0x1FF), frr = (int)((fp >> 9) & 0x1FF), frh = (int)((fp >> 18) & 0x1FF);
+        int *pg = part + g * 3 * (NA + 1) * S;
+        for (int s = 0; s < S; s++) {
+          if (frz != NA) atomicAdd(&pg[(0 * S + s) * (NA + 1) + frz], fz[s]);
+          if (frr != NA) atomicAdd(&pg[(1 * S + s) * (NA + 1) + frr], fr[s]);
+          if (frh != NA) atomicAdd(&pg[(2 * S + s) * (NA + 1) + frh], fh[0][s] + fh[1][s]);
+        }
         for (int s = 0; s < S; s++) {
           iaz[s] = vz[0][s];
           iar[s] = vr[0][s];
@@ -265,11 +274,31 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
         }
       }
       if constexpr (SPLIT) {
-        /* the hosted pieces' partial sums of this thread's row (stored by
-         * the group's recurrent product a barrier ago) */
+        /* the hosted pieces' partial sums of this thread's rows (added by
+         * the group's recurrent product a barrier ago), then cleared */
+        uint32_t fp = frow;
+        asm volatile("" : "+v"(fp));
+        int *pg = part + g * 3 * (NA + 1) * S;
+        if (fp >> 27 & 1)
+          for (int s = 0; s < S; s++) {
+            int *pz = &pg[(0 * S + s) * (NA + 1) + i];
+            iaz[s] += *pz;
+            *pz = 0;
+          }
+        if (fp >> 28 & 1)
+          for (int s = 0; s < S; s++) {
+            int *pr = &pg[(1 * S + s) * (NA + 1) + i];
+            iar[s] += *pr;
+            *pr = 0;
+          }
         int hadd[S];
         for (int s = 0; s < S; s++) hadd[s] = 0;
-        mf_owner_merge<S>(hs + g * MfHs<S>::ints, fown, A.mf_kmax[wv], tid & 7, iaz, iar, hadd);
+        if (fp >> 29 & 1)
+          for (int s = 0; s < S; s++) {
+            int *ph = &pg[(2 * S + s) * (NA + 1) + i];
+            hadd[s] = *ph;
+            *ph = 0;
+          }
         for (int s = 0; s < S; s++) {
           hpre[s] = (float)(iah[s] + hadd[s]) * kScale1;
           az[s] = (float)iaz[s];

@@ -223,105 +223,6 @@ __device__ __forceinline__ void mf_h_split(const unsigned char *lds, const uint3
   }
 }
 
-/* Split models: hosted partial sums travel through private LDS slots, one
- * per (gate, piece, row): the lane group hosting piece p of a gate stores its
- * S int32 sums of row r at hs[gate][p][r][0..S) (no two lanes share a slot:
- * plain vector stores, no atomics), and the owner of the piece's row adds the
- * slots of its row's pieces, which the plan (engine.cpp mf_plan) numbers
- * consecutively.  Per-lane words (SampleArgs::mf_frow):
- *   host  bits 7g .. 7g+5: piece index of gate g, bit 7g+6: hosts one
- *   owner bits 10g .. 10g+5: first piece of this lane's row in gate g,
- *         bits 10g+6 .. 10g+9: its number of pieces */
-constexpr int MF_MAX_PIECES = SAMPLE_WAVES * 8; /* per gate: one per lane group */
-constexpr int MF_MAX_ROW_PIECES = 15;
-/* slot MF_MAX_PIECES of each gate stays zero: the batched merge reads it
- * where a lane has fewer pieces than its wave's maximum */
-template <int S>
-struct MfHs {
-  static constexpr int ints = 3 * (MF_MAX_PIECES + 1) * 8 * S;
-};
-
-template <int S>
-__device__ __forceinline__ void mf_hs_store(int *q, const v4i &v)
-{
-  if constexpr (S == 4) *(v4i *)q = v;
-  else if constexpr (S == 2) *(int2 *)q = make_int2(v[0], v[1]);
-  else *q = v[0];
-}
-
-template <int S>
-__device__ __forceinline__ void mf_hs_add(const int *q, int (&a)[S])
-{
-  if constexpr (S == 4) {
-    const v4i v = *(const v4i *)q;
-    a[0] += v[0]; a[1] += v[1]; a[2] += v[2]; a[3] += v[3];
-  } else if constexpr (S == 2) {
-    const int2 v = *(const int2 *)q;
-    a[0] += v.x; a[1] += v.y;
-  } else {
-    a[0] += *q;
-  }
-}
-
-/* host side, after the recurrent product: this lane's hosted sums (row r of
- * its pieces) into their slots */
-template <int S>
-__device__ __forceinline__ void mf_host_store(int *hs, uint32_t host, int r, const v4i &fz, const v4i &fr, const v4i (&fh)[2])
-{
-  constexpr int G = (MF_MAX_PIECES + 1) * 8 * S; /* ints per gate */
-  asm volatile("" : "+v"(host));
-  if (host >> 6 & 1) mf_hs_store<S>(hs + 0 * G + ((int)(host & 63) * 8 + r) * S, fz);
-  if (host >> 13 & 1) mf_hs_store<S>(hs + 1 * G + ((int)(host >> 7 & 63) * 8 + r) * S, fr);
-  if (host >> 20 & 1) mf_hs_store<S>(hs + 2 * G + ((int)(host >> 14 & 63) * 8 + r) * S, fh[0] + fh[1]);
-}
-
-/* the k slots from piece p0 of one gate (hs_g) into a: loads in batches of
- * four issued before their adds (one LDS round trip per batch, not per
- * slot), over the wave's maximum K; slots past this lane's k read the zero
- * slot */
-template <int S>
-__device__ __forceinline__ void mf_merge_gate(const int *hs_g, int p0, int k, int K, int r, int (&a)[S])
-{
-  for (int j = 0; j < K; j += 4) {
-    int v[4][S];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int p = j + u < k ? p0 + j + u : MF_MAX_PIECES;
-      const int *q = hs_g + (p * 8 + r) * S;
-      if constexpr (S == 4) {
-        const v4i t = *(const v4i *)q;
-        v[u][0] = t[0]; v[u][1] = t[1]; v[u][2] = t[2]; v[u][3] = t[3];
-      } else if constexpr (S == 2) {
-        const int2 t = *(const int2 *)q;
-        v[u][0] = t.x; v[u][1] = t.y;
-      } else {
-        v[u][0] = *q;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++)
-#pragma unroll
-      for (int s = 0; s < S; s++) a[s] += v[u][s];
-  }
-}
-
-/* owner side, a barrier later: the slots of this lane's row's pieces into
- * its own sums (int32, exact in any order); kmax: the wave's maximum piece
- * counts (4 bits per gate, SampleArgs::mf_kmax) */
-template <int S>
-__device__ __forceinline__ void mf_owner_merge(const int *hs, uint32_t own, int kmax, int r, int (&az)[S], int (&ar)[S],
-                                               int (&ah)[S])
-{
-  constexpr int G = (MF_MAX_PIECES + 1) * 8 * S;
-  asm volatile("" : "+v"(own));
-  const int z0 = (int)(own & 63), nz = (int)(own >> 6 & 15);
-  const int r0 = (int)(own >> 10 & 63), nr = (int)(own >> 16 & 15);
-  const int h0 = (int)(own >> 20 & 63), nh = (int)(own >> 26 & 15);
-  mf_merge_gate<S>(hs + 0 * G, z0, nz, kmax & 15, r, az);
-  mf_merge_gate<S>(hs + 1 * G, r0, nr, kmax >> 4 & 15, r, ar);
-  mf_merge_gate<S>(hs + 2 * G, h0, nh, kmax >> 8 & 15, r, ah);
-}
-
 /* compute_sparse_gru elementwise (nnet.c:431-447) of one GRU_A unit for S
  * streams, from the gathered rows e (nnet.c:484-491 sums in the reference's
  * order), the recurrent sums faz/far, the state terms tz/tr and the recurrent

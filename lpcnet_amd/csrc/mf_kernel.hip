@@ -49,7 +49,7 @@ struct MfLds {
   static constexpr int okw = 8 * 4;           /* per-GRU_A-wave "inputs in range" words */
   static constexpr int gbw = 3 * 64 * 16;     /* GRU_B recurrent A tiles [3][64 lanes] (LDS, not registers) */
   static constexpr int total = x + xb + sb + ix + pcm + cnd + gbs + gbr + okw + gbw;
-  static constexpr int part = MfHs<S>::ints * 4; /* split models: hosted-sum slots (mf_common.h) */
+  static constexpr int part = 3 * (NA + 1) * S * 4; /* split models: hosted partial sums [3][S][NA + 1] (row NA: none) */
 };
 
 int mf_lds_bytes(int S, int split)
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   int *gbr = gbs + S * GB_ROWS;
   int *okw = gbr + GB_ROWS;
   v4i *gbw = (v4i *)(okw + 8);
-  int *hs = (int *)(gbw + 3 * 64); /* SPLIT: hosted-sum slots [3][MF_MAX_PIECES][8][S] (mf_common.h) */
+  int *part = (int *)(gbw + 3 * 64); /* SPLIT: [3][S][NA + 1] (rows contiguous: a lane group's 8 rows on 8 banks) */
   /* fixed image sections (rcpps / u-law / logit tables, dual_fc) in static
    * LDS: addresses into dynamic LDS carry an extra add of its base per
    * access, on the activation and walk chains */
@@ -216,20 +216,23 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     /* split models: this lane's hosted groups and the rows their partial
      * sums belong to (NA: none) */
     const int nfzr = SPLIT ? A.mf_nfzr[wv] : 0, nfh = SPLIT ? A.mf_nfh[wv] : 0;
-    /* split models: this lane's hosted pieces and its own row's pieces
-     * (mf_common.h), for the whole launch */
-    uint32_t fhost = 0, fown = 0;
+    /* split models: the rows this lane's hosted pieces belong to (NA: none),
+     * 9 bits per gate, and per gate whether this thread's own unit has
+     * hosted pieces to merge (bits 27..29), in one register for the whole
+     * launch */
+    uint32_t frow = 0;
     if constexpr (SPLIT) {
-      fhost = (uint32_t)A.mf_frow[tid];
-      fown = (uint32_t)A.mf_frow[SAMPLE_THREADS + tid];
+      const uint32_t *fro = (const uint32_t *)A.mf_frow + tid;
+      const uint32_t e0 = fro[0], e1 = fro[SAMPLE_THREADS], e2 = fro[2 * SAMPLE_THREADS];
+      frow = (e0 & 0x1FF) | (e1 & 0x1FF) << 9 | (e2 & 0x1FF) << 18 | (e0 >> 16 & 1) << 27 | (e1 >> 16 & 1) << 28 |
+             (e2 >> 16 & 1) << 29;
     }
 
     __syncthreads(); /* image in LDS */
     bool fast = true;
     for (int s = 0; s < S; s++) xa[s * MF_XSTR + i] = (unsigned char)quant_s8_state(st[s]);
-    if constexpr (SPLIT) /* the never-written zero slots (mf_common.h) */
-      for (int e = tid; e < 3 * 8 * S; e += SAMPLE_THREADS)
-        hs[((e / (8 * S)) * (MF_MAX_PIECES + 1) + MF_MAX_PIECES) * 8 * S + e % (8 * S)] = 0;
+    if constexpr (SPLIT)
+      for (int e = tid; e < 3 * (NA + 1) * S; e += SAMPLE_THREADS) part[e] = 0;
     __syncthreads(); /* initial q(h_A), q(h_B), ix, seeds */
     stamp_start();
 #ifdef MF_PRIO45
@@ -252,8 +255,8 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
       mf_opaque(oh);
       if constexpr (SPLIT) {
         /* own groups into v*, the hosted piece into f*, whose partial sums
-         * go to their row's owner through private LDS slots (exact int32
-         * adds, any order); the owners add them after barrier X.  Group 0's x words of both
+         * go to their row's owner through LDS (exact int32 adds, any order);
+         * the owners add them after barrier X.  Group 0's x words of both
          * products are read first: the h product's are in flight while the
          * z/r MFMAs run (the two switches break the prefetch chain) */
         v4i fz = {0, 0, 0, 0}, fr = {0, 0, 0, 0}, fh[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -266,10 +269,16 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         }
         mf_zr_split(lds, wz, wr, oz, orr, nzr, nfzr, xz, xr, vz[0], vr[0], fz, fr);
         mf_h_split(lds, wh, oh, nh, nfh, xh, vh, fh);
-        /* one vector store per hosted gate into the piece's private slot
-         * (with LDS atomics into shared row slots: ~580 more cycles per
-         * sample at 1024 skewed streams, profiles/r04) */
-        mf_host_store<S>(hs, fhost, tid & 7, fz, fr, fh);
+        uint32_t fp = frow;
+        asm volatile("" : "+v"(fp)); /* unpacked here, not hoisted into three registers */
+        const int frz = (int)(fp & 0x1FF), frr = (int)((fp >> 9) & 0x1FF), frh = (int)((fp >> 18) & 0x1FF);
+        /* only lanes hosting a piece add (a shared dummy row would
+         * serialise every other lane's atomic on one LDS address) */
+        for (int s = 0; s < S; s++) {
+          if (frz != NA) atomicAdd(&part[(0 * S + s) * (NA + 1) + frz], fz[s]);
+          if (frr != NA) atomicAdd(&part[(1 * S + s) * (NA + 1) + frr], fr[s]);
+          if (frh != NA) atomicAdd(&part[(2 * S + s) * (NA + 1) + frh], fh[0][s] + fh[1][s]);
+        }
       } else if (TRACE) {
         mf_zr<1>(lds, wz, wr, oz, orr, nzr, vz, vr);
         mf_run<MF_HMAX, 2>(lds, wh, oh, nh, vh);
@@ -373,11 +382,32 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
             }
           }
           if constexpr (SPLIT) {
-            /* the hosted pieces' partial sums of this thread's row (stored
-             * between barriers Y and X); every slot is rewritten each sample */
+            /* the hosted pieces' partial sums of this thread's rows (written
+             * between barriers Y and X), then cleared for the next sample;
+             * only rows that have pieces (LDS bandwidth: all six waves do
+             * this at once, on the critical path) */
+            uint32_t fp = frow;
+            asm volatile("" : "+v"(fp));
+            if (fp >> 27 & 1)
+              for (int s = 0; s < S; s++) {
+                int *pz = &part[(0 * S + s) * (NA + 1) + i];
+                az[s] += *pz;
+                *pz = 0;
+              }
+            if (fp >> 28 & 1)
+              for (int s = 0; s < S; s++) {
+                int *pr = &part[(1 * S + s) * (NA + 1) + i];
+                ar[s] += *pr;
+                *pr = 0;
+              }
             int hadd[S];
             for (int s = 0; s < S; s++) hadd[s] = 0;
-            mf_owner_merge<S>(hs, fown, A.mf_kmax[wv], tid & 7, az, ar, hadd);
+            if (fp >> 29 & 1)
+              for (int s = 0; s < S; s++) {
+                int *ph = &part[(2 * S + s) * (NA + 1) + i];
+                hadd[s] = *ph;
+                *ph = 0;
+              }
             for (int s = 0; s < S; s++) {
               hpre[s] = (float)(ah[s] + hadd[s]) * kScale1;
               faz[s] = (float)az[s];

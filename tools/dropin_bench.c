@@ -87,6 +87,7 @@ int main(int argc, char **argv)
   long la0 = 0, rq0 = 0;
   int ns = 0;
   lpcnet_mi355x_pool_stats(nets[0], &la0, &rq0, &ns);
+  const double run0 = lpcnet_mi355x_pool_run_ms(nets[0]);
   pthread_barrier_init(&go, NULL, T + 1);
   for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, run, (void *)(size_t)t);
   pthread_barrier_wait(&go);
@@ -95,6 +96,7 @@ int main(int argc, char **argv)
   const double dt_pool = now() - t0;
   long la = 0, rq = 0;
   lpcnet_mi355x_pool_stats(nets[0], &la, &rq, &ns);
+  const double run_ms = lpcnet_mi355x_pool_run_ms(nets[0]) - run0;
   la -= la0;
   rq -= rq0;
   for (int t = 0; t < T; t++) lpcnet_destroy(nets[t]);
@@ -131,10 +133,11 @@ int main(int argc, char **argv)
 
   const double samples = (double)T * F * LPCNET_FRAME_SIZE;
   printf("{\"threads\": %d, \"frames\": %d, \"dropin_c_threads\": {\"samples_per_s\": %.1f, \"launches\": %ld, "
-         "\"requests\": %ld, \"mean_coalesced_streams\": %.2f, \"ms_per_launch\": %.4f}, "
+         "\"requests\": %ld, \"mean_coalesced_streams\": %.2f, \"ms_per_launch\": %.4f, \"launch_run_ms\": %.4f}, "
          "\"batch_host_io\": {\"samples_per_s\": %.1f, \"ms_per_frame\": %.4f}, "
          "\"batch_device\": {\"samples_per_s\": %.1f, \"ms_per_frame\": %.4f}}\n",
          T, F, samples / dt_pool, la, rq, (double)rq / (la > 0 ? la : 1), 1e3 * dt_pool / (la > 0 ? la : 1),
+         run_ms / (la > 0 ? la : 1),
          samples / dt_host, 1e3 * dt_host / F, samples / dt_dev, 1e3 * dt_dev / F);
   return 0;
 }
