@@ -647,6 +647,14 @@ struct MfPlan {
 
 /* hosted-piece merge cost of a wave, in MFMA slots: its partial sums'
  * LDS adds (per gate hosted) */
+#ifndef MF_HOSTED_WEIGHT
+#define MF_HOSTED_WEIGHT 14 /* tenths: cost of a hosted slot relative to an own one */
+#endif
+static thread_local int g_mf_hosted_f = MF_HOSTED_WEIGHT;
+#ifndef MF_PIECE_WEIGHT
+#define MF_PIECE_WEIGHT 10 /* tenths of a score unit per hosted piece (its LDS atomics) */
+#endif
+static thread_local int g_mf_piece_w = MF_PIECE_WEIGHT;
 #ifndef MF_HOST_ADD_SLOTS
 #define MF_HOST_ADD_SLOTS 4
 #endif
@@ -679,11 +687,14 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
       own[g * NUB + u].assign(v.begin(), v.begin() + std::min((int)v.size(), T[g]));
     }
   const int npz = (int)std::max(P.pieces[0].size(), P.pieces[1].size()), nph = (int)P.pieces[2].size();
+  const int npieces = (int)(P.pieces[0].size() + P.pieces[1].size() + P.pieces[2].size());
   int extra[SAMPLE_WAVES] = {};
   int mz = 0, mh = 0; /* hosting waves (bit masks) */
   long best = -1;
   if (const char *v = getenv("LPCNET_MF_ITERS")) iters = atoi(v); /* tuning hooks */
   g_mf_simd_weight = getenv("LPCNET_MF_SIMD_W") ? atoi(getenv("LPCNET_MF_SIMD_W")) : simd_w;
+  g_mf_hosted_f = getenv("LPCNET_MF_HOSTED_F") ? atoi(getenv("LPCNET_MF_HOSTED_F")) : MF_HOSTED_WEIGHT;
+  g_mf_piece_w = getenv("LPCNET_MF_PIECE_W") ? atoi(getenv("LPCNET_MF_PIECE_W")) : MF_PIECE_WEIGHT;
   P.perm = mf_assign_unit_blocks(own, extra, iters);
   for (int round = 0; round < 2; round++) {
     int c[SAMPLE_WAVES], gz[SAMPLE_WAVES], gh[SAMPLE_WAVES];
@@ -710,16 +721,16 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
           cc[w] = c[w];
           if (sz >> w & 1) {
             ok &= 4 * gz[w] + F[0] <= MF_ZMAX;
-            cc[w] += 2 * F[0] + 2 * MF_HOST_ADD_SLOTS;
+            cc[w] += (g_mf_hosted_f * 2 * F[0]) / 10 + 2 * MF_HOST_ADD_SLOTS;
           }
           if (sh >> w & 1) {
             ok &= 4 * gh[w] + F[2] <= MF_HMAX;
-            cc[w] += F[2] + MF_HOST_ADD_SLOTS;
+            cc[w] += (g_mf_hosted_f * F[2]) / 10 + MF_HOST_ADD_SLOTS;
           }
           sum += cc[w];
         }
         if (!ok) continue;
-        const long sc = (long)mf_simd_score(cc) * 4096 + sum;
+        const long sc = ((long)mf_simd_score(cc) + (long)g_mf_piece_w * npieces / 10) * 4096 + sum;
         if (best < 0 || sc < best) {
           best = sc;
           mz = sz;
@@ -731,7 +742,8 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
     if (round == 1) break;
     /* re-balance the own rows around the hosting waves' extra load */
     for (int w = 0; w < SAMPLE_WAVES; w++)
-      extra[w] = (mz >> w & 1 ? 2 * F[0] + 2 * MF_HOST_ADD_SLOTS : 0) + (mh >> w & 1 ? F[2] + MF_HOST_ADD_SLOTS : 0);
+      extra[w] = (mz >> w & 1 ? (g_mf_hosted_f * 2 * F[0]) / 10 + 2 * MF_HOST_ADD_SLOTS : 0) +
+                 (mh >> w & 1 ? (g_mf_hosted_f * F[2]) / 10 + MF_HOST_ADD_SLOTS : 0);
     P.perm = mf_assign_unit_blocks(own, extra, iters);
   }
   /* pieces -> lane groups of the hosting waves, spread over those waves
@@ -794,6 +806,14 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, int cls = 0)
   P.split = true;
   long best = -1;
   int bt[3] = {0, 0, 0}, bf[3] = {0, 0, 0};
+  if (const char *v = getenv("LPCNET_MF_CAPS")) {
+    /* tuning hook: "Tz,Fz,Th,Fh" (own caps and piece sizes in blocks) */
+    int c[4];
+    if (sscanf(v, "%d,%d,%d,%d", &c[0], &c[1], &c[2], &c[3]) == 4) {
+      const int T[3] = {c[0], c[0], c[2]}, F[3] = {c[1], c[1], c[3]};
+      if (mf_layout(ga, P, T, F, 40000, S4 ? 33 : MF_SAMPLER_SIMD_WEIGHT) >= 0) return true;
+    }
+  }
   for (int Tz = 4; Tz <= MF_ZMAX; Tz += 4)
     for (int Fz = 0; Tz + Fz <= MF_ZMAX; Fz += 4)
       for (int Th = 4; Th <= MF_HMAX; Th += 4)
@@ -2585,7 +2605,7 @@ static std::map<std::pair<uint64_t, int>, StatePool *> g_pools;
  * wake-ups of one launch's callers take about as long as the launch, so two
  * lanes keep the GPU busy while each group is woken and gathers again. */
 #ifndef POOL_LANES_DEFAULT
-#define POOL_LANES_DEFAULT 2
+#define POOL_LANES_DEFAULT 1
 #endif
 
 static uint64_t pool_key(const unsigned char *data, int len)
