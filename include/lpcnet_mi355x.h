@@ -55,6 +55,10 @@ typedef struct {
   /* 1: the blob carries the 1.6 kb/s decoder's codebooks (ceps_codebook1..3,
    * ceps_codebook_diff4), so lpcnet_decode / lpcnet_batch_decode* accept it */
   int has_codebooks;
+  /* 1: the fast kernels may use the hardware reciprocal for rcpps (the
+   * default Intel table); 0: a custom table is set and they run their
+   * table-only forms (the `HWR` template argument rocprofv3 shows) */
+  int rcp_hw;
 } LPCNetModelInfo;
 
 /* Create a batch of nb_streams streams on HIP device `device`.

@@ -134,7 +134,7 @@ class ModelInfo(C.Structure):
                 ("ops_per_sample", C.c_double), ("streams_per_workgroup", C.c_int), ("quad_path", C.c_int),
                 ("lds_bytes", C.c_int), ("mfma_ops_per_group_sample", C.c_double),
                 ("lpc_gamma", C.c_float), ("features_delay", C.c_int), ("end2end", C.c_int),
-                ("long_rows", C.c_int), ("has_codebooks", C.c_int)]
+                ("long_rows", C.c_int), ("has_codebooks", C.c_int), ("rcp_hw", C.c_int)]
 
     @property
     def kernel_name(self) -> str:
@@ -142,12 +142,13 @@ class ModelInfo(C.Structure):
         (as rocprofv3 names it)."""
         sat = "true" if self.may_saturate else "false"
         lr = "true" if self.long_rows else "false"
+        hw = "true" if self.rcp_hw else "false"
         if self.quad_path == 4:
-            return f"mf_kernel<{self.streams_per_workgroup}, 0, {lr}>"
+            return f"mf_kernel<{self.streams_per_workgroup}, 0, {lr}, {hw}>"
         if self.quad_path == 6:
-            return f"mf2_kernel<4, {lr}>"
+            return f"mf2_kernel<4, {lr}, {hw}>"
         if self.quad_path == 5:
-            return f"fp_kernel<0, {lr}>"
+            return f"fp_kernel<0, {lr}, {hw}>"
         quad = "true" if self.quad_path == 1 else "false"
         return f"sample_kernel<{self.streams_per_workgroup}, {self.variant}, {sat}, {quad}>"
 

@@ -447,6 +447,7 @@ void choose_kernel(LPCNetBatch *b)
    * kernels run their table-only forms (the hardware-reciprocal shortcut is
    * proven for the Intel table only) */
   b->sa.rcp_hw = b->fa.rcp_hw = b->rcp_custom ? 0 : 1;
+  b->info.rcp_hw = b->sa.rcp_hw;
   if (mode == 5 && b->fp_ok && fp_lds_bytes() <= 160 * 1024) {
     b->fp = true;
     b->info.streams_per_workgroup = 1;
@@ -2979,8 +2980,18 @@ struct HandleSnapshot {
 
 static_assert(sizeof(HandleSnapshot) <= LPCNET_MI355X_STATE_MAX, "LPCNET_MI355X_STATE_MAX too small");
 
-static std::mutex g_live_mu;
-static std::unordered_map<const LPCNetState *, Handle *> g_live;
+/* the registry, sharded by address: every lpcnet_synthesize looks its
+ * handle up, and one lock would serialise hundreds of calling threads */
+struct LiveShard {
+  std::mutex mu;
+  std::unordered_map<const LPCNetState *, Handle *> map;
+};
+static LiveShard g_live[64];
+static LiveShard &live_shard(const LPCNetState *st)
+{
+  const uint64_t a = (uint64_t)(uintptr_t)st;
+  return g_live[((a >> 4) ^ (a >> 10) ^ (a >> 16)) & 63];
+}
 
 static uint64_t new_token()
 {
@@ -2997,9 +3008,10 @@ static uint64_t new_token()
 static Handle *live_handle(const LPCNetState *st)
 {
   if (!st) return nullptr;
-  std::lock_guard<std::mutex> lk(g_live_mu);
-  auto it = g_live.find(st);
-  if (it == g_live.end() || st->magic != kMagic || st->token != it->second->token) return nullptr;
+  LiveShard &sh = live_shard(st);
+  std::lock_guard<std::mutex> lk(sh.mu);
+  auto it = sh.map.find(st);
+  if (it == sh.map.end() || st->magic != kMagic || st->token != it->second->token) return nullptr;
   return it->second;
 }
 
@@ -3014,11 +3026,12 @@ static void handle_deinit(LPCNetState *st)
 {
   Handle *h = nullptr;
   {
-    std::lock_guard<std::mutex> lk(g_live_mu);
-    auto it = g_live.find(st);
-    if (it != g_live.end() && st->magic == kMagic && st->token == it->second->token) {
+    LiveShard &sh = live_shard(st);
+    std::lock_guard<std::mutex> lk(sh.mu);
+    auto it = sh.map.find(st);
+    if (it != sh.map.end() && st->magic == kMagic && st->token == it->second->token) {
       h = it->second;
-      g_live.erase(it);
+      sh.map.erase(it);
     }
   }
   if (h) handle_free(h);
@@ -3034,14 +3047,15 @@ LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
   if (!st) return -1;
   Handle *stale = nullptr, *live = nullptr;
   {
-    std::lock_guard<std::mutex> lk(g_live_mu);
-    auto it = g_live.find(st);
-    if (it != g_live.end()) {
+    LiveShard &sh = live_shard(st);
+    std::lock_guard<std::mutex> lk(sh.mu);
+    auto it = sh.map.find(st);
+    if (it != sh.map.end()) {
       if (st->magic == kMagic && st->token == it->second->token) {
         live = it->second;
       } else {
         stale = it->second;
-        g_live.erase(it);
+        sh.map.erase(it);
       }
     }
     if (!live) {
@@ -3049,7 +3063,7 @@ LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
       h->token = new_token();
       const char *d = getenv("LPCNET_DEVICE");
       h->device = d ? atoi(d) : 0;
-      g_live[st] = h;
+      sh.map[st] = h;
       st->magic = kMagic;
       st->reserved = 0;
       st->token = h->token;

@@ -215,11 +215,15 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
         asm volatile("" : "+v"(fp));
         const int frz = (int)(fp & 0x1FF), frr = (int)((fp >> 9) & 0x1FF), frh = (int)((fp >> 18) & 0x1FF);
         int *pg = part + g * 3 * (NA + 1) * S;
+        int pz[S], pr[S], ph[S];
         for (int s = 0; s < S; s++) {
-          if (frz != NA) atomicAdd(&pg[(0 * S + s) * (NA + 1) + frz], fz[s]);
-          if (frr != NA) atomicAdd(&pg[(1 * S + s) * (NA + 1) + frr], fr[s]);
-          if (frh != NA) atomicAdd(&pg[(2 * S + s) * (NA + 1) + frh], fh[0][s] + fh[1][s]);
+          pz[s] = fz[s];
+          pr[s] = fr[s];
+          ph[s] = fh[0][s] + fh[1][s];
         }
+        if (frz != NA) part_add<S>(pg, 0, frz, pz);
+        if (frr != NA) part_add<S>(pg, 1, frr, pr);
+        if (frh != NA) part_add<S>(pg, 2, frh, ph);
         for (int s = 0; s < S; s++) {
           iaz[s] = vz[0][s];
           iar[s] = vr[0][s];
@@ -279,26 +283,11 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
         uint32_t fp = frow;
         asm volatile("" : "+v"(fp));
         int *pg = part + g * 3 * (NA + 1) * S;
-        if (fp >> 27 & 1)
-          for (int s = 0; s < S; s++) {
-            int *pz = &pg[(0 * S + s) * (NA + 1) + i];
-            iaz[s] += *pz;
-            *pz = 0;
-          }
-        if (fp >> 28 & 1)
-          for (int s = 0; s < S; s++) {
-            int *pr = &pg[(1 * S + s) * (NA + 1) + i];
-            iar[s] += *pr;
-            *pr = 0;
-          }
+        if (fp >> 27 & 1) part_take<S>(pg, 0, i, iaz);
+        if (fp >> 28 & 1) part_take<S>(pg, 1, i, iar);
         int hadd[S];
         for (int s = 0; s < S; s++) hadd[s] = 0;
-        if (fp >> 29 & 1)
-          for (int s = 0; s < S; s++) {
-            int *ph = &pg[(2 * S + s) * (NA + 1) + i];
-            hadd[s] = *ph;
-            *ph = 0;
-          }
+        if (fp >> 29 & 1) part_take<S>(pg, 2, i, hadd);
         for (int s = 0; s < S; s++) {
           hpre[s] = (float)(iah[s] + hadd[s]) * kScale1;
           az[s] = (float)iaz[s];

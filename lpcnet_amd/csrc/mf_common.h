@@ -179,6 +179,57 @@ __device__ __forceinline__ void mf_h_ct(const unsigned char *lds, const uint32_t
   }
 }
 
+/* Split models: a hosted piece's int32 partial sums go to its row's owner
+ * through LDS adds into pg = [3 gates][S][NA + 1] int32 words, two streams
+ * per 64-bit add when S is even ([3][S / 2][NA + 1] words of
+ * hi * 2^32 + lo, lo sign-extended).  Summed in 64-bit two's complement over
+ * the pieces that is (sum hi) * 2^32 + (sum lo) exactly, and a row's
+ * products stay below 384 * 255 * 128 < 2^24 in magnitude, so the low word
+ * read as int32 is sum lo and the rest is sum hi: half the LDS atomics of
+ * one add per stream. */
+#ifndef MF_PART_PACKED
+#define MF_PART_PACKED 1
+#endif
+template <int S>
+__device__ __forceinline__ void part_add(int *pg, int gate, int row, const int (&v)[S])
+{
+  if constexpr (S % 2 == 0 && MF_PART_PACKED) {
+    unsigned long long *p = (unsigned long long *)pg;
+#pragma unroll
+    for (int q = 0; q < S / 2; q++)
+      atomicAdd(&p[(gate * (S / 2) + q) * (NA + 1) + row],
+                ((unsigned long long)(uint32_t)v[2 * q + 1] << 32) + (unsigned long long)(long long)v[2 * q]);
+  } else {
+#pragma unroll
+    for (int s = 0; s < S; s++) atomicAdd(&pg[(gate * S + s) * (NA + 1) + row], v[s]);
+  }
+}
+
+/* the owner's side: acc[s] += the row's hosted sums, and the words cleared */
+template <int S>
+__device__ __forceinline__ void part_take(int *pg, int gate, int row, int (&acc)[S])
+{
+  if constexpr (S % 2 == 0 && MF_PART_PACKED) {
+    unsigned long long *p = (unsigned long long *)pg;
+#pragma unroll
+    for (int q = 0; q < S / 2; q++) {
+      unsigned long long *e = &p[(gate * (S / 2) + q) * (NA + 1) + row];
+      const unsigned long long t = *e;
+      *e = 0;
+      const int lo = (int)(uint32_t)t;
+      acc[2 * q] += lo;
+      acc[2 * q + 1] += (int)((long long)(t - (unsigned long long)(long long)lo) >> 32);
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      int *e = &pg[(gate * S + s) * (NA + 1) + row];
+      acc[s] += *e;
+      *e = 0;
+    }
+  }
+}
+
 /* runtime (no, nf) -> the compile-time forms (every count the plan allows) */
 __device__ __forceinline__ void mf_zr_split(const unsigned char *lds, const uint32_t (&wz)[MF_ZMAX],
                                             const uint32_t (&wr)[MF_ZMAX], const uint32_t (&oz)[MF_ZMAX / 2],

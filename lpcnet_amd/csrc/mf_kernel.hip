@@ -274,11 +274,15 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         const int frz = (int)(fp & 0x1FF), frr = (int)((fp >> 9) & 0x1FF), frh = (int)((fp >> 18) & 0x1FF);
         /* only lanes hosting a piece add (a shared dummy row would
          * serialise every other lane's atomic on one LDS address) */
+        int pz[S], pr[S], ph[S];
         for (int s = 0; s < S; s++) {
-          if (frz != NA) atomicAdd(&part[(0 * S + s) * (NA + 1) + frz], fz[s]);
-          if (frr != NA) atomicAdd(&part[(1 * S + s) * (NA + 1) + frr], fr[s]);
-          if (frh != NA) atomicAdd(&part[(2 * S + s) * (NA + 1) + frh], fh[0][s] + fh[1][s]);
+          pz[s] = fz[s];
+          pr[s] = fr[s];
+          ph[s] = fh[0][s] + fh[1][s];
         }
+        if (frz != NA) part_add<S>(part, 0, frz, pz);
+        if (frr != NA) part_add<S>(part, 1, frr, pr);
+        if (frh != NA) part_add<S>(part, 2, frh, ph);
       } else if (TRACE) {
         mf_zr<1>(lds, wz, wr, oz, orr, nzr, vz, vr);
         mf_run<MF_HMAX, 2>(lds, wh, oh, nh, vh);
@@ -388,26 +392,11 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
              * this at once, on the critical path) */
             uint32_t fp = frow;
             asm volatile("" : "+v"(fp));
-            if (fp >> 27 & 1)
-              for (int s = 0; s < S; s++) {
-                int *pz = &part[(0 * S + s) * (NA + 1) + i];
-                az[s] += *pz;
-                *pz = 0;
-              }
-            if (fp >> 28 & 1)
-              for (int s = 0; s < S; s++) {
-                int *pr = &part[(1 * S + s) * (NA + 1) + i];
-                ar[s] += *pr;
-                *pr = 0;
-              }
+            if (fp >> 27 & 1) part_take<S>(part, 0, i, az);
+            if (fp >> 28 & 1) part_take<S>(part, 1, i, ar);
             int hadd[S];
             for (int s = 0; s < S; s++) hadd[s] = 0;
-            if (fp >> 29 & 1)
-              for (int s = 0; s < S; s++) {
-                int *ph = &part[(2 * S + s) * (NA + 1) + i];
-                hadd[s] = *ph;
-                *ph = 0;
-              }
+            if (fp >> 29 & 1) part_take<S>(part, 2, i, hadd);
             for (int s = 0; s < S; s++) {
               hpre[s] = (float)(ah[s] + hadd[s]) * kScale1;
               faz[s] = (float)az[s];
