@@ -15,6 +15,9 @@
  * with the reference's exact expressions).
  */
 #include <hip/hip_runtime.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -2545,14 +2548,14 @@ struct StatePool {
     const unsigned char *packet; /* DECODE [8] */
     short *out;                  /* SYNTH / TAIL [N] (the first `preload` are input), DECODE [4 * FRAME] */
     int N, preload, nfr;
-    bool done = false;
     int rc = 0;
     std::string err;
     int lane = -1;                /* >= 0: this caller combines on that lane (taken, or handed over) */
     uint64_t group = 0;           /* the launch this caller's previous request completed in */
     std::thread::id tid = std::this_thread::get_id();
-    std::mutex m;                 /* guards done / lane once the caller waits: the notifier */
-    std::condition_variable cv;   /* holds it while notifying, so the caller outlives the notify */
+    /* REQ_WAITING -> REQ_DONE (rc / err set) or REQ_COMBINE (lane set): the
+     * caller sleeps on this word (futex); the notifier stores it last */
+    std::atomic<uint32_t> state{0};
     bool same_shape(const Req &o) const { return kind == o.kind && N == o.N && preload == o.preload && nfr == o.nfr; }
   };
   /* a lane: one work batch (its own HIP stream) driven by one combiner at a
@@ -2581,6 +2584,7 @@ struct StatePool {
   /* gather window: the callers of each recent launch that have not come back */
   std::unordered_map<std::thread::id, uint64_t> last_group; /* caller -> launch its last request completed in */
   std::unordered_map<uint64_t, int> group_away;             /* launch -> its callers not back yet */
+  int away_n = 0;                                           /* sum of group_away */
   std::unordered_set<uint64_t> gathering;                   /* launches a combiner is waiting for */
   uint64_t groups = 0;
   int window_us = 0; /* LPCNET_POOL_WINDOW_US */
@@ -2667,6 +2671,31 @@ static StatePool *pool_acquire(const unsigned char *data, int len, int device)
   return p;
 }
 
+/* Per-request wake-up: the caller sleeps on its request's state word, the
+ * notifier stores the word (release) and wakes that one thread -- one
+ * syscall, no lock the woken thread has to take (with a mutex the woken
+ * caller blocks on it until the notifier lets go, a second futex round trip
+ * per caller).  The caller may return as soon as it sees the store, so the
+ * wake can land on a word whose frame is gone: a futex wake on a stale
+ * address wakes at most a waiter that rechecks its own condition, or fails
+ * with EFAULT, both harmless. */
+enum : uint32_t { REQ_WAITING = 0, REQ_DONE = 1, REQ_COMBINE = 2 };
+
+static void req_post(StatePool::Req *q, uint32_t v)
+{
+  std::atomic<uint32_t> *w = &q->state;
+  w->store(v, std::memory_order_release);
+  syscall(SYS_futex, (uint32_t *)w, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
+
+static uint32_t req_wait(StatePool::Req &r)
+{
+  uint32_t v;
+  while ((v = r.state.load(std::memory_order_acquire)) == REQ_WAITING)
+    syscall(SYS_futex, (uint32_t *)&r.state, FUTEX_WAIT_PRIVATE, REQ_WAITING, nullptr, nullptr, 0);
+  return v;
+}
+
 /* (lock held) free lanes and pending requests: the oldest requests' callers
  * become combiners (each takes its lane through the hand-off) */
 static void pool_kick(StatePool *p)
@@ -2677,9 +2706,8 @@ static void pool_kick(StatePool *p)
     const int lane = p->free_lanes.back();
     p->free_lanes.pop_back();
     p->nbusy++;
-    std::lock_guard<std::mutex> g(q->m);
     q->lane = lane;
-    q->cv.notify_one();
+    req_post(q, REQ_COMBINE);
   }
 }
 
@@ -2851,6 +2879,7 @@ static uint64_t pool_back(StatePool *p, std::thread::id tid)
   p->last_group.erase(it);
   auto ga = p->group_away.find(g);
   if (ga == p->group_away.end()) return 0; /* that launch's window already gave up */
+  p->away_n--;
   if (--ga->second == 0) {
     p->group_away.erase(ga);
     p->cv_comb.notify_all();
@@ -2872,32 +2901,43 @@ static int pool_submit(StatePool *p, StatePool::Req &r)
   /* a caller whose launch-mates are being gathered by a combiner joins it */
   if (p->free_lanes.empty() || p->io_waiting || (r.group && p->gathering.count(r.group))) {
     p->pending.push_back(&r);
-    /* wait on this request's own lock (taken before the pool's is released,
-     * so a completion or hand-off cannot slip in between) */
-    std::unique_lock<std::mutex> rl(r.m);
     lk.unlock();
-    r.cv.wait(rl, [&] { return r.done || r.lane >= 0; });
-    if (r.done) {
-      rl.unlock();
+    if (req_wait(r) == REQ_DONE) {
       if (r.rc) set_err(r.err);
       return r.rc;
     }
-    rl.unlock();
-    lk.lock();
+    lk.lock(); /* REQ_COMBINE: r.lane is this caller's */
   } else {
     r.lane = p->free_lanes.back();
     p->free_lanes.pop_back();
     p->nbusy++;
   }
-  if (p->window_us > 0 && r.group && p->group_away.count(r.group)) {
-    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(p->window_us);
+  /* one lane: wait for every recent launch's callers (two groups that
+   * alternate would otherwise each keep launching half-size); several
+   * lanes: for the own launch's callers only (the others have their lanes) */
+  const bool all = p->lanes.size() == 1;
+  auto away = [&] { return all ? !p->group_away.empty() : p->group_away.count(r.group) > 0; };
+  if (p->window_us > 0 && (all || r.group) && away()) {
+    /* the window grows with the callers still away: the previous combiner
+     * wakes its callers one by one (about a microsecond each) */
+    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(p->window_us + 2 * p->away_n);
     p->gathering.insert(r.group);
-    while (p->group_away.count(r.group))
+    while (away())
       if (p->cv_comb.wait_until(lk, until) == std::cv_status::timeout) {
-        /* gave up on the stragglers: forget that launch */
-        p->group_away.erase(r.group);
-        for (auto it = p->last_group.begin(); it != p->last_group.end();)
-          it = it->second == r.group ? p->last_group.erase(it) : std::next(it);
+        /* gave up on the stragglers: forget those launches */
+        if (all) {
+          p->group_away.clear();
+          p->last_group.clear();
+          p->away_n = 0;
+        } else {
+          auto ga = p->group_away.find(r.group);
+          if (ga != p->group_away.end()) {
+            p->away_n -= ga->second;
+            p->group_away.erase(ga);
+          }
+          for (auto it = p->last_group.begin(); it != p->last_group.end();)
+            it = it->second == r.group ? p->last_group.erase(it) : std::next(it);
+        }
       }
     p->gathering.erase(r.group);
   }
@@ -2916,6 +2956,7 @@ static int pool_submit(StatePool *p, StatePool::Req &r)
   p->requests += (long)mine.size();
   const uint64_t g = ++p->groups;
   p->group_away[g] = (int)mine.size();
+  p->away_n += (int)mine.size();
   for (StatePool::Req *q : mine) {
     q->rc = rc;
     q->err = e;
@@ -2931,12 +2972,7 @@ static int pool_submit(StatePool *p, StatePool::Req &r)
   }
   lk.unlock();
   /* the wake-ups, after the hand-off: one futex call per completed caller */
-  for (size_t k = 1; k < mine.size(); k++) {
-    StatePool::Req *q = mine[k];
-    std::lock_guard<std::mutex> gq(q->m);
-    q->done = true;
-    q->cv.notify_one();
-  }
+  for (size_t k = 1; k < mine.size(); k++) req_post(mine[k], REQ_DONE);
   if (rc) set_err(e);
   return rc;
 }
@@ -3172,7 +3208,7 @@ static bool req_args_ok(const float *features, const short *output, int N, int p
 LPCNET_EXPORT void lpcnet_synthesize_impl(LPCNetState *st, const float *features, short *output, int N, int preload)
 {
   if (!req_args_ok(features, output, N, preload, true)) return;
-  StatePool::Req r{-1, StatePool::SYNTH, features, nullptr, output, N, std::min(preload, N), 0, false, 0, std::string()};
+  StatePool::Req r{-1, StatePool::SYNTH, features, nullptr, output, N, std::min(preload, N), 0, 0, std::string()};
   handle_run(st, r, "lpcnet_synthesize_impl");
 }
 
@@ -3182,14 +3218,14 @@ LPCNET_EXPORT void lpcnet_synthesize(LPCNetState *st, const float *features, sho
     if (output && N > 0 && N <= FRAME) memset(output, 0, sizeof(short) * N);
     return;
   }
-  StatePool::Req r{-1, StatePool::SYNTH, features, nullptr, output, N, 0, 0, false, 0, std::string()};
+  StatePool::Req r{-1, StatePool::SYNTH, features, nullptr, output, N, 0, 0, 0, std::string()};
   handle_run(st, r, "lpcnet_synthesize");
 }
 
 LPCNET_EXPORT void lpcnet_synthesize_tail_impl(LPCNetState *st, short *output, int N, int preload)
 {
   if (!req_args_ok(nullptr, output, N, preload, false) || N == 0) return;
-  StatePool::Req r{-1, StatePool::TAIL, nullptr, nullptr, output, N, std::min(preload, N), 0, false, 0, std::string()};
+  StatePool::Req r{-1, StatePool::TAIL, nullptr, nullptr, output, N, std::min(preload, N), 0, 0, std::string()};
   handle_run(st, r, "lpcnet_synthesize_tail_impl");
 }
 
@@ -3214,7 +3250,7 @@ LPCNET_EXPORT void run_frame_network_flush(LPCNetState *st)
   if (!h || h->fbuf_fill == 0) return;
   float f[MAX_FEATURE_BUFFER][NF];
   memcpy(f, h->fbuf, sizeof(f));
-  StatePool::Req r{-1, StatePool::FLUSH, &f[0][0], nullptr, nullptr, 0, 0, h->fbuf_fill, false, 0, std::string()};
+  StatePool::Req r{-1, StatePool::FLUSH, &f[0][0], nullptr, nullptr, 0, 0, h->fbuf_fill, 0, std::string()};
   h->fbuf_fill = 0;
   handle_run(st, r, "run_frame_network_flush");
 }
@@ -3335,7 +3371,7 @@ LPCNET_EXPORT int lpcnet_mi355x_decoder_load_model(LPCNetDecState *st, const uns
 LPCNET_EXPORT int lpcnet_decode(LPCNetDecState *st, const unsigned char *buf, short *pcm)
 {
   if (!st || !buf || !pcm) { set_err("bad arguments"); return -1; }
-  StatePool::Req r{-1, StatePool::DECODE, nullptr, buf, pcm, 4 * FRAME, 0, 0, false, 0, std::string()};
+  StatePool::Req r{-1, StatePool::DECODE, nullptr, buf, pcm, 4 * FRAME, 0, 0, 0, std::string()};
   return handle_run(&st->lpcnet_state, r, "lpcnet_decode") ? -1 : 0;
 }
 

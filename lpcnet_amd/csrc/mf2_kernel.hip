@@ -221,9 +221,9 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
           pr[s] = fr[s];
           ph[s] = fh[0][s] + fh[1][s];
         }
-        if (frz != NA) part_add<S>(pg, 0, frz, pz);
-        if (frr != NA) part_add<S>(pg, 1, frr, pr);
-        if (frh != NA) part_add<S>(pg, 2, frh, ph);
+        if (frz != NA) part_add<S, true>(pg, 0, frz, pz);
+        if (frr != NA) part_add<S, true>(pg, 1, frr, pr);
+        if (frh != NA) part_add<S, true>(pg, 2, frh, ph);
         for (int s = 0; s < S; s++) {
           iaz[s] = vz[0][s];
           iar[s] = vr[0][s];
@@ -283,11 +283,11 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
         uint32_t fp = frow;
         asm volatile("" : "+v"(fp));
         int *pg = part + g * 3 * (NA + 1) * S;
-        if (fp >> 27 & 1) part_take<S>(pg, 0, i, iaz);
-        if (fp >> 28 & 1) part_take<S>(pg, 1, i, iar);
+        if (fp >> 27 & 1) part_take<S, true>(pg, 0, i, iaz);
+        if (fp >> 28 & 1) part_take<S, true>(pg, 1, i, iar);
         int hadd[S];
         for (int s = 0; s < S; s++) hadd[s] = 0;
-        if (fp >> 29 & 1) part_take<S>(pg, 2, i, hadd);
+        if (fp >> 29 & 1) part_take<S, true>(pg, 2, i, hadd);
         for (int s = 0; s < S; s++) {
           hpre[s] = (float)(iah[s] + hadd[s]) * kScale1;
           az[s] = (float)iaz[s];

@@ -180,20 +180,19 @@ __device__ __forceinline__ void mf_h_ct(const unsigned char *lds, const uint32_t
 }
 
 /* Split models: a hosted piece's int32 partial sums go to its row's owner
- * through LDS adds into pg = [3 gates][S][NA + 1] int32 words, two streams
- * per 64-bit add when S is even ([3][S / 2][NA + 1] words of
- * hi * 2^32 + lo, lo sign-extended).  Summed in 64-bit two's complement over
+ * through LDS adds into pg = [3 gates][S][NA + 1] int32 words; PACK (S even):
+ * two streams per 64-bit add ([3][S / 2][NA + 1] words of hi * 2^32 + lo, lo
+ * sign-extended).  Summed in 64-bit two's complement over
  * the pieces that is (sum hi) * 2^32 + (sum lo) exactly, and a row's
  * products stay below 384 * 255 * 128 < 2^24 in magnitude, so the low word
  * read as int32 is sum lo and the rest is sum hi: half the LDS atomics of
- * one add per stream. */
-#ifndef MF_PART_PACKED
-#define MF_PART_PACKED 1
-#endif
-template <int S>
+ * one add per stream.  Measured (three alternating same-box rounds, skewed
+ * model): mf2_kernel at 2048 streams 0.6 % faster packed, mf_kernel<4> at
+ * 1024 streams 3.5 % slower, so only mf2_kernel packs. */
+template <int S, bool PACK>
 __device__ __forceinline__ void part_add(int *pg, int gate, int row, const int (&v)[S])
 {
-  if constexpr (S % 2 == 0 && MF_PART_PACKED) {
+  if constexpr (S % 2 == 0 && PACK) {
     unsigned long long *p = (unsigned long long *)pg;
 #pragma unroll
     for (int q = 0; q < S / 2; q++)
@@ -206,10 +205,10 @@ __device__ __forceinline__ void part_add(int *pg, int gate, int row, const int (
 }
 
 /* the owner's side: acc[s] += the row's hosted sums, and the words cleared */
-template <int S>
+template <int S, bool PACK>
 __device__ __forceinline__ void part_take(int *pg, int gate, int row, int (&acc)[S])
 {
-  if constexpr (S % 2 == 0 && MF_PART_PACKED) {
+  if constexpr (S % 2 == 0 && PACK) {
     unsigned long long *p = (unsigned long long *)pg;
 #pragma unroll
     for (int q = 0; q < S / 2; q++) {

@@ -280,9 +280,9 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
           pr[s] = fr[s];
           ph[s] = fh[0][s] + fh[1][s];
         }
-        if (frz != NA) part_add<S>(part, 0, frz, pz);
-        if (frr != NA) part_add<S>(part, 1, frr, pr);
-        if (frh != NA) part_add<S>(part, 2, frh, ph);
+        if (frz != NA) part_add<S, false>(part, 0, frz, pz);
+        if (frr != NA) part_add<S, false>(part, 1, frr, pr);
+        if (frh != NA) part_add<S, false>(part, 2, frh, ph);
       } else if (TRACE) {
         mf_zr<1>(lds, wz, wr, oz, orr, nzr, vz, vr);
         mf_run<MF_HMAX, 2>(lds, wh, oh, nh, vh);
@@ -392,11 +392,11 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
              * this at once, on the critical path) */
             uint32_t fp = frow;
             asm volatile("" : "+v"(fp));
-            if (fp >> 27 & 1) part_take<S>(part, 0, i, az);
-            if (fp >> 28 & 1) part_take<S>(part, 1, i, ar);
+            if (fp >> 27 & 1) part_take<S, false>(part, 0, i, az);
+            if (fp >> 28 & 1) part_take<S, false>(part, 1, i, ar);
             int hadd[S];
             for (int s = 0; s < S; s++) hadd[s] = 0;
-            if (fp >> 29 & 1) part_take<S>(part, 2, i, hadd);
+            if (fp >> 29 & 1) part_take<S, false>(part, 2, i, hadd);
             for (int s = 0; s < S; s++) {
               hpre[s] = (float)(ah[s] + hadd[s]) * kScale1;
               faz[s] = (float)az[s];
