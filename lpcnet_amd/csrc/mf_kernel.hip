@@ -268,7 +268,6 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
           xh[k] = mf_x(lds, oh, k);
         }
         mf_zr_split(lds, wz, wr, oz, orr, nzr, nfzr, xz, xr, vz[0], vr[0], fz, fr);
-        mf_h_split(lds, wh, oh, nh, nfh, xh, vh, fh);
         uint32_t fp = frow;
         asm volatile("" : "+v"(fp)); /* unpacked here, not hoisted into three registers */
         const int frz = (int)(fp & 0x1FF), frr = (int)((fp >> 9) & 0x1FF), frh = (int)((fp >> 18) & 0x1FF);
@@ -278,8 +277,10 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
         for (int s = 0; s < S; s++) {
           pz[s] = fz[s];
           pr[s] = fr[s];
-          ph[s] = fh[0][s] + fh[1][s];
         }
+        mf_h_split(lds, wh, oh, nh, nfh, xh, vh, fh);
+        for (int s = 0; s < S; s++) ph[s] = fh[0][s] + fh[1][s];
+        /* gate by gate: z of every stream, then r, then h */
         if (frz != NA) part_add<S, false>(part, 0, frz, pz);
         if (frr != NA) part_add<S, false>(part, 1, frr, pr);
         if (frh != NA) part_add<S, false>(part, 2, frh, ph);
