@@ -204,28 +204,38 @@ __device__ __forceinline__ void part_add(int *pg, int gate, int row, const int (
   }
 }
 
-/* the owner's side: acc[s] += the row's hosted sums, and the words cleared */
+/* the owner's side, in two parts so that no branch waits on the reads: the
+ * row's hosted sums (v[s]; a row without pieces reads its words, which no
+ * piece ever adds to, as 0), then -- only where the row has pieces -- the
+ * words cleared for the next sample */
 template <int S, bool PACK>
-__device__ __forceinline__ void part_take(int *pg, int gate, int row, int (&acc)[S])
+__device__ __forceinline__ void part_read(const int *pg, int gate, int row, int (&v)[S])
+{
+  if constexpr (S % 2 == 0 && PACK) {
+    const unsigned long long *p = (const unsigned long long *)pg;
+#pragma unroll
+    for (int q = 0; q < S / 2; q++) {
+      const unsigned long long t = p[(gate * (S / 2) + q) * (NA + 1) + row];
+      const int lo = (int)(uint32_t)t;
+      v[2 * q] = lo;
+      v[2 * q + 1] = (int)((long long)(t - (unsigned long long)(long long)lo) >> 32);
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < S; s++) v[s] = pg[(gate * S + s) * (NA + 1) + row];
+  }
+}
+
+template <int S, bool PACK>
+__device__ __forceinline__ void part_clear(int *pg, int gate, int row)
 {
   if constexpr (S % 2 == 0 && PACK) {
     unsigned long long *p = (unsigned long long *)pg;
 #pragma unroll
-    for (int q = 0; q < S / 2; q++) {
-      unsigned long long *e = &p[(gate * (S / 2) + q) * (NA + 1) + row];
-      const unsigned long long t = *e;
-      *e = 0;
-      const int lo = (int)(uint32_t)t;
-      acc[2 * q] += lo;
-      acc[2 * q + 1] += (int)((long long)(t - (unsigned long long)(long long)lo) >> 32);
-    }
+    for (int q = 0; q < S / 2; q++) p[(gate * (S / 2) + q) * (NA + 1) + row] = 0;
   } else {
 #pragma unroll
-    for (int s = 0; s < S; s++) {
-      int *e = &pg[(gate * S + s) * (NA + 1) + row];
-      acc[s] += *e;
-      *e = 0;
-    }
+    for (int s = 0; s < S; s++) pg[(gate * S + s) * (NA + 1) + row] = 0;
   }
 }
 

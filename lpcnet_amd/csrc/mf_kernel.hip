@@ -393,11 +393,26 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
              * this at once, on the critical path) */
             uint32_t fp = frow;
             asm volatile("" : "+v"(fp));
-            if (fp >> 27 & 1) part_take<S, false>(part, 0, i, az);
-            if (fp >> 28 & 1) part_take<S, false>(part, 1, i, ar);
-            int hadd[S];
-            for (int s = 0; s < S; s++) hadd[s] = 0;
-            if (fp >> 29 & 1) part_take<S, false>(part, 2, i, hadd);
+            /* only the rows with pieces read (mf2_kernel reads every row
+             * unconditionally instead: +3 % there, -0.8 % here) */
+            int zadd[S], radd[S], hadd[S];
+            for (int s = 0; s < S; s++) zadd[s] = radd[s] = hadd[s] = 0;
+            if (fp >> 27 & 1) {
+              part_read<S, false>(part, 0, i, zadd);
+              part_clear<S, false>(part, 0, i);
+            }
+            if (fp >> 28 & 1) {
+              part_read<S, false>(part, 1, i, radd);
+              part_clear<S, false>(part, 1, i);
+            }
+            if (fp >> 29 & 1) {
+              part_read<S, false>(part, 2, i, hadd);
+              part_clear<S, false>(part, 2, i);
+            }
+            for (int s = 0; s < S; s++) {
+              az[s] += zadd[s];
+              ar[s] += radd[s];
+            }
             for (int s = 0; s < S; s++) {
               hpre[s] = (float)(ah[s] + hadd[s]) * kScale1;
               faz[s] = (float)az[s];
