@@ -87,3 +87,49 @@ def test_handles_of_different_models_and_reset(require_gpu):
     assert np.array_equal(nb.synthesize(f[4]), xa.synthesize(f[4][None])[0])
     for n in (na, nb, nc):
         n.close()
+
+
+@pytest.mark.parametrize("lanes,window", [(2, 50), (3, 0), (1, 0)])
+def test_pool_lanes_and_window_match_oracle(require_gpu, monkeypatch, lanes, window):
+    """The pool's optional configurations (read when a pool is created):
+    several lanes (concurrent launches on their own work batches) with and
+    without a gather window, and one lane without the window.  32 threads x 6
+    frames, plus a save/restore on one handle half-way (slot I/O waits for
+    every lane to be idle): every stream equals the oracle's."""
+    monkeypatch.setenv("LPCNET_POOL_LANES", str(lanes))
+    monkeypatch.setenv("LPCNET_POOL_WINDOW_US", str(window))
+    T, F = 32, 6
+    blob = L.synthetic_model(10 + lanes * 10 + window, 0)  # a model of its own: a fresh pool with these settings
+    feats = [L.synthetic_features(t, F)[:, :20] for t in range(T)]
+    nets = [L.LPCNet(blob) for _ in range(T)]
+    monkeypatch.delenv("LPCNET_POOL_LANES")
+    monkeypatch.delenv("LPCNET_POOL_WINDOW_US")
+    outs = [None] * T
+    start = threading.Barrier(T)
+    errors = []
+
+    def run(t):
+        try:
+            start.wait()
+            res = []
+            for f in range(F):
+                if t == 0 and f == F // 2:
+                    snap = nets[0].save()
+                    nets[0].restore(snap)
+                res.append(nets[t].synthesize(feats[t][f]))
+            outs[t] = np.stack(res)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=300)
+    assert not errors, errors[:2]
+    for t in range(T):
+        assert np.array_equal(outs[t], O.synth_stream(blob, feats[t], 0)), t
+    la, rq, ns = pool_stats(nets[0])
+    assert ns == T and rq == T * F
+    for n in nets:
+        n.close()
