@@ -2071,19 +2071,28 @@ LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b)
   b->min_fc = v[0].frame_count;
 }
 
+/* Work a caller enqueues on b->stream after a step's kernels, before its one
+ * synchronisation (the drop-in pool's state scatter). */
+using PreSync = std::function<int()>;
+
 /* one frame for the first nB streams of a batch, host I/O ([nB][NF] in,
  * [nB][N] out) */
-static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm, int N, int preload)
+static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm, int N, int preload,
+                       const PreSync &pre = PreSync(), bool staged = false)
 {
   if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
   if (N < 0 || N > FRAME || !features || (N > 0 && !pcm) || preload < 0) { set_err("bad arguments"); return -1; }
   if (b->set_device()) return -1;
   if (ensure_trace(b, N)) return -1;
-  /* everything below is ordered after work already queued on b->stream */
-  HIPCHK(hipMemcpyAsync(b->d_feat, features, sizeof(float) * NF * nB, hipMemcpyHostToDevice, b->stream));
-  if (preload > 0 && N > 0)
-    HIPCHK(hipMemcpyAsync(b->d_pcm, pcm, sizeof(short) * N * nB, hipMemcpyHostToDevice, b->stream));
+  /* everything below is ordered after work already queued on b->stream
+   * (staged: the caller has queued the features / preload copies already) */
+  if (!staged) {
+    HIPCHK(hipMemcpyAsync(b->d_feat, features, sizeof(float) * NF * nB, hipMemcpyHostToDevice, b->stream));
+    if (preload > 0 && N > 0)
+      HIPCHK(hipMemcpyAsync(b->d_pcm, pcm, sizeof(short) * N * nB, hipMemcpyHostToDevice, b->stream));
+  }
   if (launch_frame_step(b, b->d_feat, b->d_lpc, true, b->d_pcm, N, preload, -1, nB)) return -1;
+  if (pre && pre()) return -1;
   if (N > 0) HIPCHK(hipMemcpyAsync(pcm, b->d_pcm, sizeof(short) * N * nB, hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
   return check_status(b);
@@ -2120,7 +2129,7 @@ static int decode_ready(LPCNetBatch *b)
 
 /* lpcnet_decode (lpcnet.c:310-319) on the first nB streams, host I/O:
  * packets [nB][8] -> pcm [nB][4 * FRAME] */
-static int decode_first(LPCNetBatch *b, int nB, const unsigned char *packets, short *pcm)
+static int decode_first(LPCNetBatch *b, int nB, const unsigned char *packets, short *pcm, const PreSync &pre = PreSync())
 {
   if (decode_ready(b)) return -1;
   if (!packets || !pcm) { set_err("bad arguments"); return -1; }
@@ -2138,6 +2147,7 @@ static int decode_first(LPCNetBatch *b, int nB, const unsigned char *packets, sh
     if (launch_frame_step(b, b->d_dfeat + (size_t)f * nB * NF, b->d_lpc, true, b->d_dpcm + (size_t)f * nB * FRAME, FRAME, 0,
                           -1, nB))
       return -1;
+  if (pre && pre()) return -1;
   std::vector<short> tmp((size_t)4 * nB * FRAME);
   HIPCHK(hipMemcpyAsync(tmp.data(), b->d_dpcm, sizeof(short) * tmp.size(), hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
@@ -2177,7 +2187,7 @@ LPCNET_EXPORT int lpcnet_batch_decode_frames(LPCNetBatch *b, const unsigned char
 
 /* lpcnet_synthesize_tail_impl on the first nB streams: the sample network on
  * the conditioning and LPC already in the stream states, no frame network */
-static int tail_first(LPCNetBatch *b, int nB, short *pcm, int N, int preload)
+static int tail_first(LPCNetBatch *b, int nB, short *pcm, int N, int preload, const PreSync &pre = PreSync())
 {
   if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
   if (N < 0 || N > FRAME || (N > 0 && !pcm) || preload < 0) { set_err("bad arguments"); return -1; }
@@ -2186,6 +2196,7 @@ static int tail_first(LPCNetBatch *b, int nB, short *pcm, int N, int preload)
   if (ensure_trace(b, N)) return -1;
   if (preload > 0) HIPCHK(hipMemcpyAsync(b->d_pcm, pcm, sizeof(short) * N * nB, hipMemcpyHostToDevice, b->stream));
   if (launch_frame_step(b, nullptr, nullptr, false, b->d_pcm, N, preload, -1, nB, false, false)) return -1;
+  if (pre && pre()) return -1;
   HIPCHK(hipMemcpyAsync(pcm, b->d_pcm, sizeof(short) * N * nB, hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
   return check_status(b);
@@ -2194,13 +2205,14 @@ static int tail_first(LPCNetBatch *b, int nB, short *pcm, int N, int preload)
 /* run_frame_network on the first nB streams (features [nB][NF]); keep_cond:
  * into the caller's locals as run_frame_network_flush does (lpcnet.c:134-144),
  * otherwise into the state's conditioning (lpcnet.c:275) */
-static int frame_first(LPCNetBatch *b, int nB, const float *features, bool keep_cond)
+static int frame_first(LPCNetBatch *b, int nB, const float *features, bool keep_cond, const PreSync &pre = PreSync())
 {
   if (!b || !b->have_model) { set_err("no model loaded"); return -1; }
   if (!features) { set_err("bad arguments"); return -1; }
   if (b->set_device()) return -1;
   HIPCHK(hipMemcpyAsync(b->d_feat, features, sizeof(float) * NF * nB, hipMemcpyHostToDevice, b->stream));
   if (launch_frame_step(b, b->d_feat, b->d_lpc, true, nullptr, 0, 0, -1, nB, true, keep_cond)) return -1;
+  if (pre && pre()) return -1;
   HIPCHK(hipStreamSynchronize(b->stream));
   return check_status(b);
 }
@@ -2564,6 +2576,11 @@ struct StatePool {
     LPCNetBatch *work = nullptr; /* work->B >= the largest coalesced call on this lane */
     int *d_map = nullptr;        /* [map_cap] work-batch stream -> slot */
     int map_cap = 0;
+    /* pinned host staging of a launch ([map_cap] entries each), so the
+     * copies are truly asynchronous: slot map, features, PCM */
+    int *h_map = nullptr;
+    float *h_feat = nullptr;
+    short *h_pcm = nullptr;
   };
   uint64_t key = 0;
   int device = 0;
@@ -2745,7 +2762,12 @@ static void pool_release(StatePool *p, int slot)
   /* unreachable now: no handle holds it and the map no longer lists it */
   if (hipSetDevice(p->device) == hipSuccess) {
     (void)hipFree(p->d_slots);
-    for (StatePool::Lane &l : p->lanes) (void)hipFree(l.d_map);
+    for (StatePool::Lane &l : p->lanes) {
+      (void)hipFree(l.d_map);
+      (void)hipHostFree(l.h_map);
+      (void)hipHostFree(l.h_feat);
+      (void)hipHostFree(l.h_pcm);
+    }
   }
   for (StatePool::Lane &l : p->lanes)
     if (l.work) lpcnet_batch_destroy(l.work);
@@ -2820,52 +2842,80 @@ static int pool_run(StatePool *p, StatePool::Lane &L, const std::vector<StatePoo
   if (w->set_device()) return -1;
   if (L.map_cap < n) {
     (void)hipFree(L.d_map);
+    (void)hipHostFree(L.h_map);
+    (void)hipHostFree(L.h_feat);
+    (void)hipHostFree(L.h_pcm);
     L.d_map = nullptr;
+    L.h_map = nullptr;
+    L.h_feat = nullptr;
+    L.h_pcm = nullptr;
+    L.map_cap = 0;
     HIPCHK(hipMalloc(&L.d_map, sizeof(int) * (size_t)w->B));
+    HIPCHK(hipHostMalloc(&L.h_map, sizeof(int) * (size_t)w->B, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&L.h_feat, sizeof(float) * NF * (size_t)w->B, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&L.h_pcm, sizeof(short) * 4 * FRAME * (size_t)w->B, hipHostMallocDefault));
     L.map_cap = w->B;
   }
-  std::vector<int> map(n);
-  for (int k = 0; k < n; k++) map[k] = rq[k]->slot;
-  HIPCHK(hipMemcpyAsync(L.d_map, map.data(), sizeof(int) * n, hipMemcpyHostToDevice, w->stream));
+  float *feat = L.h_feat;
+  short *pcm = L.h_pcm;
+  const int nout = r0.kind == StatePool::DECODE ? 4 * FRAME : N;
+  /* a synthesis step's inputs go first, so the copy engine's work precedes
+   * every kernel of the launch (one copy -> kernel hand-over instead of two) */
+  const bool staged = r0.kind == StatePool::SYNTH && w->set_device() == 0;
+  if (staged) {
+    for (int k = 0; k < n; k++) {
+      memcpy(&feat[(size_t)k * NF], rq[k]->feat, sizeof(float) * NF);
+      if (r0.preload > 0) memcpy(&pcm[(size_t)k * N], rq[k]->out, sizeof(short) * std::min(r0.preload, N));
+    }
+    HIPCHK(hipMemcpyAsync(w->d_feat, feat, sizeof(float) * NF * n, hipMemcpyHostToDevice, w->stream));
+    if (r0.preload > 0 && N > 0)
+      HIPCHK(hipMemcpyAsync(w->d_pcm, pcm, sizeof(short) * N * n, hipMemcpyHostToDevice, w->stream));
+  }
+  for (int k = 0; k < n; k++) L.h_map[k] = rq[k]->slot;
+  HIPCHK(hipMemcpyAsync(L.d_map, L.h_map, sizeof(int) * n, hipMemcpyHostToDevice, w->stream));
   if (launch_state_copy(w->d_state, p->d_slots, nullptr, L.d_map, n, w->stream)) { set_err("state gather failed"); return -1; }
   /* every stream of the work batch is this call's: the multi-frame bound is its min */
   w->min_fc = 0;
-  std::vector<float> feat((size_t)n * NF);
-  const int nout = r0.kind == StatePool::DECODE ? 4 * FRAME : N;
-  std::vector<short> pcm((size_t)n * std::max(nout, 1));
+  /* the states go back to their slots right behind the step's kernels, before
+   * its one synchronisation */
+  const PreSync scatter = [&]() -> int {
+    if (launch_state_copy(p->d_slots, w->d_state, L.d_map, nullptr, n, w->stream)) {
+      set_err("state scatter failed");
+      return -1;
+    }
+    return 0;
+  };
   int rc = 0;
   switch (r0.kind) {
   case StatePool::SYNTH:
   case StatePool::TAIL:
-    for (int k = 0; k < n; k++) {
-      if (r0.kind == StatePool::SYNTH) memcpy(&feat[(size_t)k * NF], rq[k]->feat, sizeof(float) * NF);
-      if (r0.preload > 0) memcpy(&pcm[(size_t)k * N], rq[k]->out, sizeof(short) * std::min(r0.preload, N));
-    }
-    rc = r0.kind == StatePool::SYNTH ? synth_first(w, n, feat.data(), pcm.data(), N, r0.preload)
-                                     : tail_first(w, n, pcm.data(), N, r0.preload);
+    if (!staged)
+      for (int k = 0; k < n; k++) {
+        if (r0.kind == StatePool::SYNTH) memcpy(&feat[(size_t)k * NF], rq[k]->feat, sizeof(float) * NF);
+        if (r0.preload > 0) memcpy(&pcm[(size_t)k * N], rq[k]->out, sizeof(short) * std::min(r0.preload, N));
+      }
+    rc = r0.kind == StatePool::SYNTH ? synth_first(w, n, feat, pcm, N, r0.preload, scatter, staged)
+                                     : tail_first(w, n, pcm, N, r0.preload, scatter);
     break;
   case StatePool::FLUSH:
     for (int j = 0; j < r0.nfr && rc == 0; j++) {
       for (int k = 0; k < n; k++) memcpy(&feat[(size_t)k * NF], rq[k]->feat + (size_t)j * NF, sizeof(float) * NF);
-      rc = frame_first(w, n, feat.data(), true);
+      rc = frame_first(w, n, feat, true, j + 1 == r0.nfr ? scatter : PreSync());
     }
     break;
   case StatePool::DECODE: {
     std::vector<unsigned char> pk((size_t)n * 8);
     for (int k = 0; k < n; k++) memcpy(&pk[(size_t)k * 8], rq[k]->packet, 8);
-    rc = decode_first(w, n, pk.data(), pcm.data());
+    rc = decode_first(w, n, pk.data(), pcm, scatter);
     break;
   }
   default:
     set_err("bad request");
     rc = -1;
   }
-  if (rc == 0) {
-    if (launch_state_copy(p->d_slots, w->d_state, L.d_map, nullptr, n, w->stream)) { set_err("state scatter failed"); return -1; }
-    HIPCHK(hipStreamSynchronize(w->stream));
+  if (rc == 0)
     for (int k = 0; k < n; k++)
       if (nout > 0 && r0.kind != StatePool::FLUSH) memcpy(rq[k]->out, &pcm[(size_t)k * nout], sizeof(short) * nout);
-  }
   return rc;
 }
 

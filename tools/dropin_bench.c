@@ -1,7 +1,7 @@
 /*
  * dropin_bench.c -- aggregate throughput of the drop-in API from C threads.
  *
- *   dropin_bench <threads> <frames>
+ *   dropin_bench <threads> <frames> [pool]
  *
  * T pthreads, one LPCNetState each (include/lpcnet.h: lpcnet_create,
  * lpcnet_load_model, lpcnet_synthesize -- the reference's own calling
@@ -11,6 +11,7 @@
  * I/O frame by frame (lpcnet_batch_synthesize) and device-resident
  * (lpcnet_batch_synthesize_frames).  One JSON object on stdout.  The C
  * driver separates the pool's own cost from a Python caller's turnaround.
+ * With "pool" only the drop-in part runs (for a kernel trace of it alone).
  */
 #define _POSIX_C_SOURCE 200809L
 #include <pthread.h>
@@ -48,7 +49,7 @@ static void *run(void *arg)
 int main(int argc, char **argv)
 {
   if (argc < 3) {
-    fprintf(stderr, "usage: %s <threads> <frames>\n", argv[0]);
+    fprintf(stderr, "usage: %s <threads> <frames> [pool]\n", argv[0]);
     return 2;
   }
   T = atoi(argv[1]);
@@ -100,6 +101,13 @@ int main(int argc, char **argv)
   la -= la0;
   rq -= rq0;
   for (int t = 0; t < T; t++) lpcnet_destroy(nets[t]);
+  const double samples = (double)T * F * LPCNET_FRAME_SIZE;
+  if (argc > 3 && !strcmp(argv[3], "pool")) {
+    printf("{\"threads\": %d, \"frames\": %d, \"dropin_c_threads\": {\"samples_per_s\": %.1f, \"launches\": %ld, "
+           "\"requests\": %ld, \"ms_per_launch\": %.4f, \"launch_run_ms\": %.4f}}\n",
+           T, F, samples / dt_pool, la, rq, 1e3 * dt_pool / (la > 0 ? la : 1), run_ms / (la > 0 ? la : 1));
+    return 0;
+  }
 
   /* the same streams through one batch: host I/O frame by frame */
   LPCNetBatch *b = lpcnet_batch_create(T, 0);
@@ -131,7 +139,6 @@ int main(int argc, char **argv)
   lpcnet_batch_device_free(b, d_p);
   lpcnet_batch_destroy(b);
 
-  const double samples = (double)T * F * LPCNET_FRAME_SIZE;
   printf("{\"threads\": %d, \"frames\": %d, \"dropin_c_threads\": {\"samples_per_s\": %.1f, \"launches\": %ld, "
          "\"requests\": %ld, \"mean_coalesced_streams\": %.2f, \"ms_per_launch\": %.4f, \"launch_run_ms\": %.4f}, "
          "\"batch_host_io\": {\"samples_per_s\": %.1f, \"ms_per_frame\": %.4f}, "
