@@ -2861,7 +2861,7 @@ static int pool_run(StatePool *p, StatePool::Lane &L, const std::vector<StatePoo
   const int nout = r0.kind == StatePool::DECODE ? 4 * FRAME : N;
   /* a synthesis step's inputs go first, so the copy engine's work precedes
    * every kernel of the launch (one copy -> kernel hand-over instead of two) */
-  const bool staged = r0.kind == StatePool::SYNTH && w->set_device() == 0;
+  const bool staged = r0.kind == StatePool::SYNTH;
   if (staged) {
     for (int k = 0; k < n; k++) {
       memcpy(&feat[(size_t)k * NF], rq[k]->feat, sizeof(float) * NF);
