@@ -2562,18 +2562,16 @@ struct StatePool {
     int N, preload, nfr;
     int rc = 0;
     std::string err;
-    int lane = -1;                /* >= 0: this caller combines on that lane (taken, or handed over) */
-    uint64_t group = 0;           /* the launch this caller's previous request completed in */
-    std::thread::id tid = std::this_thread::get_id();
-    /* REQ_WAITING -> REQ_DONE (rc / err set) or REQ_COMBINE (lane set): the
-     * caller sleeps on this word (futex); the notifier stores it last */
+    Req *next = nullptr;          /* the pool's inbox (a lock-free stack) */
+    /* REQ_WAITING -> REQ_DONE (rc / err set) or REQ_COMBINE (the caller now
+     * holds the pool): the caller sleeps on this word (futex), the notifier
+     * stores it last */
     std::atomic<uint32_t> state{0};
     bool same_shape(const Req &o) const { return kind == o.kind && N == o.N && preload == o.preload && nfr == o.nfr; }
   };
-  /* a lane: one work batch (its own HIP stream) driven by one combiner at a
-   * time; launches on different lanes run concurrently */
+  /* the work batch (its HIP stream) and its staging, driven by the combiner */
   struct Lane {
-    LPCNetBatch *work = nullptr; /* work->B >= the largest coalesced call on this lane */
+    LPCNetBatch *work = nullptr; /* work->B >= the largest coalesced call */
     int *d_map = nullptr;        /* [map_cap] work-batch stream -> slot */
     int map_cap = 0;
     /* pinned host staging of a launch ([map_cap] entries each), so the
@@ -2586,49 +2584,46 @@ struct StatePool {
   int device = 0;
   std::vector<unsigned char> blob;
   bool has_codebooks = false;
-  std::vector<Lane> lanes; /* fixed at creation */
-  std::vector<int> free_lanes;
+  Lane lane;
   StreamState *d_slots = nullptr;
   int cap = 0;
   std::vector<int> free_slots;
   int refs = 0; /* handles bound + transient acquisitions; changed under g_pools_mu only */
-  std::mutex mu;
-  std::condition_variable cv;      /* no launch runs (slot I/O waiters) */
-  std::condition_variable cv_comb; /* a launch's callers are all back (gather windows) */
-  int nbusy = 0;                   /* lanes with a combiner */
-  int io_waiting = 0; /* slot I/O callers waiting for an idle pool: no new combiner then */
-  std::vector<Req *> pending;
-  /* gather window: the callers of each recent launch that have not come back */
-  std::unordered_map<std::thread::id, uint64_t> last_group; /* caller -> launch its last request completed in */
-  std::unordered_map<uint64_t, int> group_away;             /* launch -> its callers not back yet */
-  int away_n = 0;                                           /* sum of group_away */
-  std::unordered_set<uint64_t> gathering;                   /* launches a combiner is waiting for */
-  uint64_t groups = 0;
-  int window_us = 0; /* LPCNET_POOL_WINDOW_US */
+  std::mutex mu; /* slot bookkeeping (taken with the pool idle: PoolIdle) */
+  /* Submission is lock-free: a request is pushed on `inbox` and its caller
+   * either takes `busy` (0 -> 1) and combines, or sleeps on its request until
+   * a combiner completes it or hands it the pool.  The combiner alone drains
+   * the inbox, runs the launch and updates expect_n. */
+  std::atomic<StatePool::Req *> inbox{nullptr};
+  std::atomic<uint32_t> busy{0};       /* 1: a combiner or a slot I/O holds the pool */
+  std::atomic<int> io_waiting{0};      /* slot I/O callers waiting: no new combiner takes the pool */
+  std::atomic<uint32_t> arrivals{0};   /* requests pushed and not drained yet */
+  std::atomic<uint32_t> win_target{0}; /* a combiner waits for this many arrivals (0: none waits) */
+  int expect_n = 0;                    /* requests of the previous launch (combiner-owned) */
+  /* broadcast wake-ups (LPCNET_POOL_BROADCAST): waiters sleep on wake_seq,
+   * the combiner marks its completed requests and wakes them all at once */
+  bool broadcast = false;
+  std::atomic<uint32_t> wake_seq{0};
+  int window_us = 0;                   /* LPCNET_POOL_WINDOW_US */
   /* statistics (tests / diagnostics) */
-  long launches = 0, requests = 0;
-  double run_us = 0; /* time inside pool_run (the launches themselves) */
+  std::atomic<long> launches{0}, requests{0};
+  std::atomic<long long> run_ns{0}; /* time inside pool_run (the launches themselves) */
 };
 
 static std::mutex g_pools_mu;
 static std::map<std::pair<uint64_t, int>, StatePool *> g_pools;
 
 /* Gather window of a combiner: before its launch it waits up to this long
- * for the other callers of the launch its own previous request ran in (a
- * thread calling lpcnet_synthesize in a loop is back within microseconds), so
- * K looping callers keep launching together instead of fragmenting into
- * ever smaller launches.  A launch whose callers do not all come back in time
- * is forgotten: a caller that stopped costs one window once. */
+ * (plus 2 us per caller expected) until as many requests have arrived as the
+ * previous launch carried (a thread calling lpcnet_synthesize in a loop is
+ * back within microseconds), so K looping callers keep launching together
+ * instead of settling into half-size launches that alternate.  Callers that
+ * stopped cost one window once: the next launch expects only those that
+ * came. */
 #ifndef POOL_WINDOW_US_DEFAULT
 #define POOL_WINDOW_US_DEFAULT 200
 #endif
-/* Lanes per pool (LPCNET_POOL_LANES): concurrent launches.  A frame step of
- * a few hundred streams is latency-bound (a few percent of the CUs), and the
- * wake-ups of one launch's callers take about as long as the launch, so two
- * lanes keep the GPU busy while each group is woken and gathers again. */
-#ifndef POOL_LANES_DEFAULT
-#define POOL_LANES_DEFAULT 1
-#endif
+
 
 static uint64_t pool_key(const unsigned char *data, int len)
 {
@@ -2676,12 +2671,9 @@ static StatePool *pool_acquire(const unsigned char *data, int len, int device)
   p->device = device;
   p->blob.assign(data, data + len);
   p->has_codebooks = w->has_codebooks;
-  int nl = POOL_LANES_DEFAULT;
-  if (const char *v = getenv("LPCNET_POOL_LANES")) nl = std::min(8, std::max(1, atoi(v)));
-  p->lanes.resize(nl);
-  p->lanes[0].work = w; /* the others load the model on first use */
-  for (int k = nl - 1; k >= 0; k--) p->free_lanes.push_back(k);
+  p->lane.work = w;
   p->refs = 1;
+  if (const char *v = getenv("LPCNET_POOL_BROADCAST")) p->broadcast = atoi(v) != 0;
   if (const char *v = getenv("LPCNET_POOL_WINDOW_US")) p->window_us = std::max(0, atoi(v));
   else p->window_us = POOL_WINDOW_US_DEFAULT;
   g_pools[{key, device}] = p;
@@ -2690,57 +2682,105 @@ static StatePool *pool_acquire(const unsigned char *data, int len, int device)
 
 /* Per-request wake-up: the caller sleeps on its request's state word, the
  * notifier stores the word (release) and wakes that one thread -- one
- * syscall, no lock the woken thread has to take (with a mutex the woken
- * caller blocks on it until the notifier lets go, a second futex round trip
- * per caller).  The caller may return as soon as it sees the store, so the
- * wake can land on a word whose frame is gone: a futex wake on a stale
- * address wakes at most a waiter that rechecks its own condition, or fails
- * with EFAULT, both harmless. */
+ * syscall, no lock the woken thread has to take.  The caller may return as
+ * soon as it sees the store, so the wake can land on a word whose frame is
+ * gone: a futex wake on a stale address wakes at most a waiter that rechecks
+ * its own condition, or fails with EFAULT, both harmless. */
 enum : uint32_t { REQ_WAITING = 0, REQ_DONE = 1, REQ_COMBINE = 2 };
 
-static void req_post(StatePool::Req *q, uint32_t v)
+static void futex_wake(std::atomic<uint32_t> *w, int n)
+{
+  syscall(SYS_futex, (uint32_t *)w, FUTEX_WAKE_PRIVATE, n, nullptr, nullptr, 0);
+}
+
+/* sleep while *w == v, at most `ns` nanoseconds (0: no limit) */
+static void futex_wait(std::atomic<uint32_t> *w, uint32_t v, long long ns = 0)
+{
+  struct timespec ts;
+  if (ns > 0) {
+    ts.tv_sec = (time_t)(ns / 1000000000);
+    ts.tv_nsec = (long)(ns % 1000000000);
+  }
+  syscall(SYS_futex, (uint32_t *)w, FUTEX_WAIT_PRIVATE, v, ns > 0 ? &ts : nullptr, nullptr, 0);
+}
+
+static void req_post(StatePool *p, StatePool::Req *q, uint32_t v)
 {
   std::atomic<uint32_t> *w = &q->state;
   w->store(v, std::memory_order_release);
-  syscall(SYS_futex, (uint32_t *)w, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+  if (p->broadcast) {
+    p->wake_seq.fetch_add(1, std::memory_order_release);
+    futex_wake(&p->wake_seq, INT32_MAX);
+  } else {
+    futex_wake(w, 1);
+  }
 }
 
-static uint32_t req_wait(StatePool::Req &r)
+/* r's state once it leaves `from` */
+static uint32_t req_wait(StatePool *p, StatePool::Req &r, uint32_t from = REQ_WAITING)
 {
   uint32_t v;
-  while ((v = r.state.load(std::memory_order_acquire)) == REQ_WAITING)
-    syscall(SYS_futex, (uint32_t *)&r.state, FUTEX_WAIT_PRIVATE, REQ_WAITING, nullptr, nullptr, 0);
+  if (p->broadcast) {
+    for (;;) {
+      const uint32_t seq = p->wake_seq.load(std::memory_order_acquire);
+      if ((v = r.state.load(std::memory_order_acquire)) != from) return v;
+      futex_wait(&p->wake_seq, seq);
+    }
+  }
+  while ((v = r.state.load(std::memory_order_acquire)) == from) futex_wait(&r.state, from);
   return v;
 }
 
-/* (lock held) free lanes and pending requests: the oldest requests' callers
- * become combiners (each takes its lane through the hand-off) */
-static void pool_kick(StatePool *p)
+static void inbox_push(StatePool *p, StatePool::Req *q)
 {
-  while (!p->io_waiting && !p->free_lanes.empty() && !p->pending.empty()) {
-    StatePool::Req *q = p->pending.front();
-    p->pending.erase(p->pending.begin());
-    const int lane = p->free_lanes.back();
-    p->free_lanes.pop_back();
-    p->nbusy++;
-    q->lane = lane;
-    req_post(q, REQ_COMBINE);
+  StatePool::Req *h = p->inbox.load(std::memory_order_relaxed);
+  do q->next = h;
+  while (!p->inbox.compare_exchange_weak(h, q, std::memory_order_release, std::memory_order_relaxed));
+}
+
+/* The holder of `busy` lets go: to the slot I/O callers waiting, else to the
+ * caller of the newest inbox request (REQ_COMBINE: `busy` stays held on its
+ * behalf; no one else drains the inbox meanwhile), else to no one -- with a
+ * recheck, since a request pushed just before the release found the pool
+ * busy and sleeps. */
+static void pool_let_go(StatePool *p)
+{
+  for (;;) {
+    if (p->io_waiting.load(std::memory_order_acquire) > 0) {
+      p->busy.store(0, std::memory_order_release);
+      futex_wake(&p->busy, INT32_MAX);
+      return;
+    }
+    StatePool::Req *h = p->inbox.load(std::memory_order_acquire);
+    if (h) {
+      req_post(p, h, REQ_COMBINE);
+      return;
+    }
+    p->busy.store(0, std::memory_order_seq_cst);
+    if (!p->inbox.load(std::memory_order_seq_cst)) return;
+    uint32_t b = 0;
+    if (!p->busy.compare_exchange_strong(b, 1, std::memory_order_seq_cst)) return; /* another caller took it */
   }
 }
 
-/* Slot I/O on an idle pool: waits (lock held) until no launch runs --
- * meanwhile the combiner does not hand its role on, so a stream of synthesis
- * calls cannot starve it -- and on scope exit hands the pool to any pending
- * requests */
+/* Slot I/O on an idle pool (lock held for the slot bookkeeping): takes
+ * `busy` -- meanwhile no new combiner takes the pool, so a stream of
+ * synthesis calls cannot starve it -- and on scope exit lets go (to any
+ * requests that arrived meanwhile).  No combiner takes p->mu, so holding it
+ * while waiting cannot deadlock. */
 struct PoolIdle {
   StatePool *p;
-  PoolIdle(StatePool *p_, std::unique_lock<std::mutex> &lk) : p(p_)
+  PoolIdle(StatePool *p_, std::unique_lock<std::mutex> &) : p(p_)
   {
-    p->io_waiting++;
-    p->cv.wait(lk, [&] { return p->nbusy == 0; });
-    p->io_waiting--;
+    p->io_waiting.fetch_add(1, std::memory_order_seq_cst);
+    for (;;) {
+      uint32_t b = 0;
+      if (p->busy.compare_exchange_strong(b, 1, std::memory_order_seq_cst)) break;
+      futex_wait(&p->busy, 1, 1000000); /* woken by the combiner's let-go; re-polled every ms */
+    }
+    p->io_waiting.fetch_sub(1, std::memory_order_seq_cst);
   }
-  ~PoolIdle() { pool_kick(p); }
+  ~PoolIdle() { pool_let_go(p); }
 };
 
 /* give back `slot` (if >= 0) and one reference; the last reference frees
@@ -2762,15 +2802,12 @@ static void pool_release(StatePool *p, int slot)
   /* unreachable now: no handle holds it and the map no longer lists it */
   if (hipSetDevice(p->device) == hipSuccess) {
     (void)hipFree(p->d_slots);
-    for (StatePool::Lane &l : p->lanes) {
-      (void)hipFree(l.d_map);
-      (void)hipHostFree(l.h_map);
-      (void)hipHostFree(l.h_feat);
-      (void)hipHostFree(l.h_pcm);
-    }
+    (void)hipFree(p->lane.d_map);
+    (void)hipHostFree(p->lane.h_map);
+    (void)hipHostFree(p->lane.h_feat);
+    (void)hipHostFree(p->lane.h_pcm);
   }
-  for (StatePool::Lane &l : p->lanes)
-    if (l.work) lpcnet_batch_destroy(l.work);
+  if (p->lane.work) lpcnet_batch_destroy(p->lane.work);
   delete p;
 }
 
@@ -2819,8 +2856,8 @@ static int pool_slot_io(StatePool *p, int slot, StreamState *get, const StreamSt
   return 0;
 }
 
-/* one coalesced step for requests rq (all of the same shape) on lane L
- * (only L's combiner touches L) */
+/* one coalesced step for requests rq (all of the same shape); the combiner
+ * alone touches L */
 static int pool_run(StatePool *p, StatePool::Lane &L, const std::vector<StatePool::Req *> &rq)
 {
   const int n = (int)rq.size();
@@ -2919,112 +2956,112 @@ static int pool_run(StatePool *p, StatePool::Lane &L, const std::vector<StatePoo
   return rc;
 }
 
-/* (lock held) `tid` is back: its previous launch has one caller less away;
- * that launch's id (0: none, or its window gave up) */
-static uint64_t pool_back(StatePool *p, std::thread::id tid)
+/* Flat combining with a hand-off, lock-free on the submission side: the
+ * caller pushes its request and either takes the idle pool or sleeps on its
+ * request.  The combiner waits (the gather window) until as many requests
+ * have arrived as the previous launch carried, drains the inbox, runs every
+ * request of the oldest one's shape, wakes exactly the callers it completed,
+ * and lets the pool go -- to the newest pending request's caller if any (the
+ * GPU idles until it launches).  No mutex on this path: with hundreds of C
+ * threads, waking callers that then queue on one lock costs more than the
+ * launch. */
+static int pool_combine(StatePool *p, StatePool::Req &r)
 {
-  auto it = p->last_group.find(tid);
-  if (it == p->last_group.end()) return 0;
-  const uint64_t g = it->second;
-  p->last_group.erase(it);
-  auto ga = p->group_away.find(g);
-  if (ga == p->group_away.end()) return 0; /* that launch's window already gave up */
-  p->away_n--;
-  if (--ga->second == 0) {
-    p->group_away.erase(ga);
-    p->cv_comb.notify_all();
-  }
-  return g;
-}
-
-/* Flat combining over lanes with a hand-off: a caller that finds a lane free
- * takes it, waits (the gather window) for the rest of its previous launch's
- * callers, and runs itself plus every pending request of its shape; when it
- * is done it hands free lanes to the oldest pending requests' callers first
- * (the GPU idles until they launch) and then wakes exactly the callers whose
- * requests completed -- no wake-up of every waiting thread per launch (with
- * 256 C threads that herd on one mutex cost more than the launch) */
-static int pool_submit(StatePool *p, StatePool::Req &r)
-{
-  std::unique_lock<std::mutex> lk(p->mu);
-  r.group = pool_back(p, r.tid);
-  /* a caller whose launch-mates are being gathered by a combiner joins it */
-  if (p->free_lanes.empty() || p->io_waiting || (r.group && p->gathering.count(r.group))) {
-    p->pending.push_back(&r);
-    lk.unlock();
-    if (req_wait(r) == REQ_DONE) {
+  while (r.state.load(std::memory_order_acquire) != REQ_DONE) {
+    const int expect = p->expect_n;
+    if (p->window_us > 0 && expect > 1 && (int)p->arrivals.load(std::memory_order_acquire) < expect) {
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(p->window_us + 2 * expect);
+      p->win_target.store((uint32_t)expect, std::memory_order_seq_cst);
+      for (;;) {
+        const uint32_t a = p->arrivals.load(std::memory_order_seq_cst);
+        if ((int)a >= expect) break;
+        const long long left = std::chrono::duration_cast<std::chrono::nanoseconds>(until - std::chrono::steady_clock::now()).count();
+        if (left <= 0) break;
+        futex_wait(&p->arrivals, a, left);
+      }
+      p->win_target.store(0, std::memory_order_relaxed);
+    }
+    /* drain: the stack reversed is arrival order */
+    StatePool::Req *h = p->inbox.exchange(nullptr, std::memory_order_acquire);
+    std::vector<StatePool::Req *> all;
+    for (; h; h = h->next) all.push_back(h);
+    if (all.empty()) {
+      /* r ran in the launch of the combiner that let the pool go to us: it
+       * still posts r's completion, so r's frame must outlive that store */
+      pool_let_go(p);
+      if (r.state.load(std::memory_order_acquire) != REQ_DONE) req_wait(p, r, r.state.load(std::memory_order_acquire));
       if (r.rc) set_err(r.err);
       return r.rc;
     }
-    lk.lock(); /* REQ_COMBINE: r.lane is this caller's */
-  } else {
-    r.lane = p->free_lanes.back();
-    p->free_lanes.pop_back();
-    p->nbusy++;
-  }
-  /* one lane: wait for every recent launch's callers (two groups that
-   * alternate would otherwise each keep launching half-size); several
-   * lanes: for the own launch's callers only (the others have their lanes) */
-  const bool all = p->lanes.size() == 1;
-  auto away = [&] { return all ? !p->group_away.empty() : p->group_away.count(r.group) > 0; };
-  if (p->window_us > 0 && (all || r.group) && away()) {
-    /* the window grows with the callers still away: the previous combiner
-     * wakes its callers one by one (about a microsecond each) */
-    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(p->window_us + 2 * p->away_n);
-    p->gathering.insert(r.group);
-    while (away())
-      if (p->cv_comb.wait_until(lk, until) == std::cv_status::timeout) {
-        /* gave up on the stragglers: forget those launches */
-        if (all) {
-          p->group_away.clear();
-          p->last_group.clear();
-          p->away_n = 0;
-        } else {
-          auto ga = p->group_away.find(r.group);
-          if (ga != p->group_away.end()) {
-            p->away_n -= ga->second;
-            p->group_away.erase(ga);
+    std::reverse(all.begin(), all.end());
+    p->arrivals.fetch_sub((uint32_t)all.size(), std::memory_order_acq_rel);
+    std::vector<StatePool::Req *> mine, rest;
+    for (StatePool::Req *q : all) (q->same_shape(*all[0]) ? mine : rest).push_back(q);
+    for (auto it = rest.rbegin(); it != rest.rend(); ++it) {
+      inbox_push(p, *it);
+      p->arrivals.fetch_add(1, std::memory_order_acq_rel);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = pool_run(p, p->lane, mine);
+    const std::string e = rc ? g_err : std::string();
+    p->run_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+    p->launches.fetch_add(1);
+    p->requests.fetch_add((long)mine.size());
+    p->expect_n = (int)mine.size();
+    bool self = false;
+    for (StatePool::Req *q : mine) {
+      q->rc = rc;
+      q->err = e;
+      if (q == &r) self = true;
+    }
+    if (self) r.state.store(REQ_DONE, std::memory_order_release);
+    /* the next launch first (the GPU idles until it starts), then the
+     * wake-ups: one futex call per completed caller */
+    auto post_all = [&]() {
+      if (p->broadcast) {
+        bool any = false;
+        for (StatePool::Req *q : mine)
+          if (q != &r) {
+            q->state.store(REQ_DONE, std::memory_order_release);
+            any = true;
           }
-          for (auto it = p->last_group.begin(); it != p->last_group.end();)
-            it = it->second == r.group ? p->last_group.erase(it) : std::next(it);
+        if (any) {
+          p->wake_seq.fetch_add(1, std::memory_order_release);
+          futex_wake(&p->wake_seq, INT32_MAX);
         }
+      } else {
+        for (StatePool::Req *q : mine)
+          if (q != &r) req_post(p, q, REQ_DONE);
       }
-    p->gathering.erase(r.group);
+    };
+    if (self) {
+      pool_let_go(p);
+      post_all();
+      if (r.rc) set_err(r.err);
+      return r.rc;
+    }
+    post_all();
   }
-  /* combine: this request and every pending one of its shape */
-  std::vector<StatePool::Req *> mine{&r}, rest;
-  for (StatePool::Req *q : p->pending) (q->same_shape(r) ? mine : rest).push_back(q);
-  p->pending.swap(rest);
-  StatePool::Lane &L = p->lanes[r.lane];
-  lk.unlock();
-  const auto t0 = std::chrono::steady_clock::now();
-  const int rc = pool_run(p, L, mine);
-  const std::string e = rc ? g_err : std::string();
-  lk.lock();
-  p->run_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-  p->launches++;
-  p->requests += (long)mine.size();
-  const uint64_t g = ++p->groups;
-  p->group_away[g] = (int)mine.size();
-  p->away_n += (int)mine.size();
-  for (StatePool::Req *q : mine) {
-    q->rc = rc;
-    q->err = e;
-    if (p->last_group.count(q->tid)) pool_back(p, q->tid);
-    p->last_group[q->tid] = g;
+  pool_let_go(p);
+  if (r.rc) set_err(r.err);
+  return r.rc;
+}
+
+static int pool_submit(StatePool *p, StatePool::Req &r)
+{
+  inbox_push(p, &r);
+  const uint32_t a = p->arrivals.fetch_add(1, std::memory_order_seq_cst) + 1;
+  const uint32_t t = p->win_target.load(std::memory_order_seq_cst);
+  if (t && a >= t) futex_wake(&p->arrivals, 1);
+  if (p->io_waiting.load(std::memory_order_seq_cst) == 0) {
+    uint32_t b = 0;
+    if (p->busy.compare_exchange_strong(b, 1, std::memory_order_seq_cst)) return pool_combine(p, r);
   }
-  p->free_lanes.push_back(r.lane);
-  p->nbusy--;
-  if (p->io_waiting) {
-    if (p->nbusy == 0) p->cv.notify_all(); /* slot I/O first; it hands the pool on when done */
-  } else {
-    pool_kick(p);
+  if (req_wait(p, r) == REQ_DONE) {
+    if (r.rc) set_err(r.err);
+    return r.rc;
   }
-  lk.unlock();
-  /* the wake-ups, after the hand-off: one futex call per completed caller */
-  for (size_t k = 1; k < mine.size(); k++) req_post(mine[k], REQ_DONE);
-  if (rc) set_err(e);
-  return rc;
+  return pool_combine(p, r); /* REQ_COMBINE: the pool was handed over */
 }
 
 /* ---- handles -------------------------------------------------------------
@@ -3353,7 +3390,7 @@ LPCNET_EXPORT double lpcnet_mi355x_pool_run_ms(const LPCNetState *st)
   Handle *h = live_handle(st);
   if (!h || !h->pool) return -1.0;
   std::lock_guard<std::mutex> lk(h->pool->mu);
-  return h->pool->run_us * 1e-3;
+  return h->pool->run_ns.load() * 1e-6;
 }
 
 LPCNET_EXPORT int lpcnet_mi355x_pool_stats(const LPCNetState *st, long *launches, long *requests, int *streams)
@@ -3363,8 +3400,8 @@ LPCNET_EXPORT int lpcnet_mi355x_pool_stats(const LPCNetState *st, long *launches
   StatePool *p = h->pool;
   {
     std::lock_guard<std::mutex> lk(p->mu);
-    if (launches) *launches = p->launches;
-    if (requests) *requests = p->requests;
+    if (launches) *launches = p->launches.load();
+    if (requests) *requests = p->requests.load();
   }
   if (streams) {
     std::lock_guard<std::mutex> lk(g_pools_mu);

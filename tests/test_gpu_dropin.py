@@ -89,21 +89,20 @@ def test_handles_of_different_models_and_reset(require_gpu):
         n.close()
 
 
-@pytest.mark.parametrize("lanes,window", [(2, 50), (3, 0), (1, 0)])
-def test_pool_lanes_and_window_match_oracle(require_gpu, monkeypatch, lanes, window):
-    """The pool's optional configurations (read when a pool is created):
-    several lanes (concurrent launches on their own work batches) with and
-    without a gather window, and one lane without the window.  32 threads x 6
-    frames, plus a save/restore on one handle half-way (slot I/O waits for
-    every lane to be idle): every stream equals the oracle's."""
-    monkeypatch.setenv("LPCNET_POOL_LANES", str(lanes))
+@pytest.mark.parametrize("window,broadcast", [(50, 0), (0, 0), (200, 1)])
+def test_pool_window_and_wakeups_match_oracle(require_gpu, monkeypatch, window, broadcast):
+    """The pool's optional settings (read when a pool is created): gather
+    window on or off, per-caller or broadcast wake-ups.  32 threads x 6
+    frames, plus a save/restore on one handle half-way (slot I/O takes the
+    pool while threads keep submitting): every stream equals the oracle's."""
     monkeypatch.setenv("LPCNET_POOL_WINDOW_US", str(window))
+    monkeypatch.setenv("LPCNET_POOL_BROADCAST", str(broadcast))
     T, F = 32, 6
-    blob = L.synthetic_model(10 + lanes * 10 + window, 0)  # a model of its own: a fresh pool with these settings
+    blob = L.synthetic_model(20 + window + broadcast, 0)  # a model of its own: a fresh pool with these settings
     feats = [L.synthetic_features(t, F)[:, :20] for t in range(T)]
     nets = [L.LPCNet(blob) for _ in range(T)]
-    monkeypatch.delenv("LPCNET_POOL_LANES")
     monkeypatch.delenv("LPCNET_POOL_WINDOW_US")
+    monkeypatch.delenv("LPCNET_POOL_BROADCAST")
     outs = [None] * T
     start = threading.Barrier(T)
     errors = []
