@@ -804,6 +804,10 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, int cls = 0)
     const int T[3] = {MF_ZMAX, MF_ZMAX, MF_HMAX}, F[3] = {0, 0, 0};
     return mf_layout(ga, P, T, F, S4 ? 400000 : 40000, w_unsplit) >= 0;
   }
+  /* split plans weight the sampler SIMDs 3.3x on mf_kernel (1-4 streams per
+   * workgroup: measured best plans at 256 and 1024 streams) and 2.7x on
+   * mf2_kernel (best at 8192) */
+  const int w_split = cls == 2 ? MF_SAMPLER_SIMD_WEIGHT : 33;
   /* split: every own cap / piece size pair, screened with a short
    * assignment search, the best re-laid-out in full (LPCNET_MF_FORCE_SPLIT:
    * split even a model that fits -- pieces required -- for tests) */
@@ -815,7 +819,7 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, int cls = 0)
     int c[4];
     if (sscanf(v, "%d,%d,%d,%d", &c[0], &c[1], &c[2], &c[3]) == 4) {
       const int T[3] = {c[0], c[0], c[2]}, F[3] = {c[1], c[1], c[3]};
-      if (mf_layout(ga, P, T, F, 40000, S4 ? 33 : MF_SAMPLER_SIMD_WEIGHT) >= 0) return true;
+      if (mf_layout(ga, P, T, F, 40000, w_split) >= 0) return true;
     }
   }
   for (int Tz = 4; Tz <= MF_ZMAX; Tz += 4)
@@ -843,7 +847,7 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, int cls = 0)
           if (!fits || (force && !need)) continue;
           MfPlan C;
           const int T[3] = {Tz, Tz, Th}, F[3] = {Fz, Fz, Fh};
-          const long sc = mf_layout(ga, C, T, F, 1500, S4 ? 33 : MF_SAMPLER_SIMD_WEIGHT);
+          const long sc = mf_layout(ga, C, T, F, 1500, w_split);
           if (sc < 0) continue;
           if (best < 0 || sc < best) {
             best = sc;
@@ -852,7 +856,7 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, int cls = 0)
           }
         }
   if (best < 0) return false; /* does not fit even split: the lockstep kernel runs it */
-  return mf_layout(ga, P, bt, bf, 40000, S4 ? 33 : MF_SAMPLER_SIMD_WEIGHT) >= 0;
+  return mf_layout(ga, P, bt, bf, 40000, w_split) >= 0;
 }
 
 /* The model constants of a blob (see load_model); -1 on a malformed record
