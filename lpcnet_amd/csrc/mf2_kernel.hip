@@ -49,7 +49,7 @@ struct Mf2Lds {
   static constexpr int okw = 2 * 2 * 8 * 4;         /* range words [frame parity][group][GRU_A wave] */
   static constexpr int gbw = 3 * 64 * 16;           /* GRU_B recurrent A tiles [3][64] */
   static constexpr int total = x + xb + sb + ix + lpc + cnd + gbs + gbr + okw + gbw;
-  static constexpr int part = 2 * 3 * (NA + 1) * S * 4; /* split models: hosted partial sums [group][3][S][NA + 1] */
+  static constexpr int part = 2 * 3 * (NA + 1) * S * 4; /* split models: hosted partial sums [group][3][NA + 1][S] */
 };
 
 int mf2_lds_bytes(int S, int split)
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
   int *gbr = gbs + 2 * 2 * S * GB_ROWS;
   int *okw = gbr + GB_ROWS;
   v4i *gbw = (v4i *)(okw + 32);
-  int *part = (int *)(gbw + 3 * 64); /* SPLIT: [2 groups][3][S][NA + 1] */
+  int *part = (int *)(gbw + 3 * 64); /* SPLIT: [2 groups][3][NA + 1][S / 2] 64-bit words */
   __shared__ uint4 img_s[IMG_VAR / 16];
   unsigned char *img = (unsigned char *)img_s;
 

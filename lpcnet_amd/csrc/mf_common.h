@@ -180,8 +180,9 @@ __device__ __forceinline__ void mf_h_ct(const unsigned char *lds, const uint32_t
 }
 
 /* Split models: a hosted piece's int32 partial sums go to its row's owner
- * through LDS adds into pg = [3 gates][S][NA + 1] int32 words; PACK (S even):
- * two streams per 64-bit add ([3][S / 2][NA + 1] words of hi * 2^32 + lo, lo
+ * through LDS adds into pg: PACK false, [3 gates][NA + 1][S] int32 words (a row's S streams
+ * contiguous: one 16-byte read and clear per gate at S = 4); PACK (S even):
+ * two streams per 64-bit add ([3][NA + 1][S / 2] words of hi * 2^32 + lo, lo
  * sign-extended).  Summed in 64-bit two's complement over
  * the pieces that is (sum hi) * 2^32 + (sum lo) exactly, and a row's
  * products stay below 384 * 255 * 128 < 2^24 in magnitude, so the low word
@@ -189,6 +190,10 @@ __device__ __forceinline__ void mf_h_ct(const unsigned char *lds, const uint32_t
  * one add per stream.  Measured (three alternating same-box rounds, skewed
  * model): mf2_kernel at 2048 streams 0.6 % faster packed, mf_kernel<4> at
  * 1024 streams 3.5 % slower, so only mf2_kernel packs. */
+/* PACK word q of a row: [3 gates][NA + 1][S / 2], a row's words contiguous
+ * (one 16-byte read and clear per gate at S = 4: mf2_kernel at 2048 streams
+ * -1.1 % against [3][S / 2][NA + 1]) */
+#define PIDX(gate, q, row) (((gate) * (NA + 1) + (row)) * (S / 2) + (q))
 template <int S, bool PACK>
 __device__ __forceinline__ void part_add(int *pg, int gate, int row, const int (&v)[S])
 {
@@ -196,11 +201,11 @@ __device__ __forceinline__ void part_add(int *pg, int gate, int row, const int (
     unsigned long long *p = (unsigned long long *)pg;
 #pragma unroll
     for (int q = 0; q < S / 2; q++)
-      atomicAdd(&p[(gate * (S / 2) + q) * (NA + 1) + row],
+      atomicAdd(&p[PIDX(gate, q, row)],
                 ((unsigned long long)(uint32_t)v[2 * q + 1] << 32) + (unsigned long long)(long long)v[2 * q]);
   } else {
 #pragma unroll
-    for (int s = 0; s < S; s++) atomicAdd(&pg[(gate * S + s) * (NA + 1) + row], v[s]);
+    for (int s = 0; s < S; s++) atomicAdd(&pg[(gate * (NA + 1) + row) * S + s], v[s]);
   }
 }
 
@@ -215,14 +220,20 @@ __device__ __forceinline__ void part_read(const int *pg, int gate, int row, int 
     const unsigned long long *p = (const unsigned long long *)pg;
 #pragma unroll
     for (int q = 0; q < S / 2; q++) {
-      const unsigned long long t = p[(gate * (S / 2) + q) * (NA + 1) + row];
+      const unsigned long long t = p[PIDX(gate, q, row)];
       const int lo = (int)(uint32_t)t;
       v[2 * q] = lo;
       v[2 * q + 1] = (int)((long long)(t - (unsigned long long)(long long)lo) >> 32);
     }
+  } else if constexpr (S == 4) {
+    const int4 t = *(const int4 *)&pg[(gate * (NA + 1) + row) * 4];
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else if constexpr (S == 2) {
+    const int2 t = *(const int2 *)&pg[(gate * (NA + 1) + row) * 2];
+    v[0] = t.x; v[1] = t.y;
   } else {
 #pragma unroll
-    for (int s = 0; s < S; s++) v[s] = pg[(gate * S + s) * (NA + 1) + row];
+    for (int s = 0; s < S; s++) v[s] = pg[(gate * (NA + 1) + row) * S + s];
   }
 }
 
@@ -232,10 +243,14 @@ __device__ __forceinline__ void part_clear(int *pg, int gate, int row)
   if constexpr (S % 2 == 0 && PACK) {
     unsigned long long *p = (unsigned long long *)pg;
 #pragma unroll
-    for (int q = 0; q < S / 2; q++) p[(gate * (S / 2) + q) * (NA + 1) + row] = 0;
+    for (int q = 0; q < S / 2; q++) p[PIDX(gate, q, row)] = 0;
+  } else if constexpr (S == 4) {
+    *(int4 *)&pg[(gate * (NA + 1) + row) * 4] = make_int4(0, 0, 0, 0);
+  } else if constexpr (S == 2) {
+    *(int2 *)&pg[(gate * (NA + 1) + row) * 2] = make_int2(0, 0);
   } else {
 #pragma unroll
-    for (int s = 0; s < S; s++) pg[(gate * S + s) * (NA + 1) + row] = 0;
+    for (int s = 0; s < S; s++) pg[(gate * (NA + 1) + row) * S + s] = 0;
   }
 }
 

@@ -49,7 +49,7 @@ struct MfLds {
   static constexpr int okw = 8 * 4;           /* per-GRU_A-wave "inputs in range" words */
   static constexpr int gbw = 3 * 64 * 16;     /* GRU_B recurrent A tiles [3][64 lanes] (LDS, not registers) */
   static constexpr int total = x + xb + sb + ix + pcm + cnd + gbs + gbr + okw + gbw;
-  static constexpr int part = 3 * (NA + 1) * S * 4; /* split models: hosted partial sums [3][S][NA + 1] (row NA: none) */
+  static constexpr int part = 3 * (NA + 1) * S * 4; /* split models: hosted partial sums [3][NA + 1][S] (row NA: none) */
 };
 
 int mf_lds_bytes(int S, int split)
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   int *gbr = gbs + S * GB_ROWS;
   int *okw = gbr + GB_ROWS;
   v4i *gbw = (v4i *)(okw + 8);
-  int *part = (int *)(gbw + 3 * 64); /* SPLIT: [3][S][NA + 1] (rows contiguous: a lane group's 8 rows on 8 banks) */
+  int *part = (int *)(gbw + 3 * 64); /* SPLIT: [3][NA + 1][S] (a row's streams contiguous: one 16-byte read per gate at S = 4) */
   /* fixed image sections (rcpps / u-law / logit tables, dual_fc) in static
    * LDS: addresses into dynamic LDS carry an extra add of its base per
    * access, on the activation and walk chains */
@@ -278,12 +278,27 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
           pz[s] = fz[s];
           pr[s] = fr[s];
         }
+        /* S < 4: branch-free, a lane without a piece adds 0 to its own row's
+         * words (same box, skewed model: 1 and 256 streams -1 to -2 %); S = 4
+         * keeps the branches (+1 % branch-free) */
+        auto padd = [&](int g, int fr_, int (&v)[S]) {
+          if constexpr (S < 4) {
+            const bool h = fr_ != NA;
+            int vv[S];
+            for (int s = 0; s < S; s++) vv[s] = h ? v[s] : 0;
+            part_add<S, false>(part, g, h ? fr_ : i, vv);
+          } else if (fr_ != NA) {
+            part_add<S, false>(part, g, fr_, v);
+          }
+        };
         mf_h_split(lds, wh, oh, nh, nfh, xh, vh, fh);
         for (int s = 0; s < S; s++) ph[s] = fh[0][s] + fh[1][s];
-        /* gate by gate: z of every stream, then r, then h */
-        if (frz != NA) part_add<S, false>(part, 0, frz, pz);
-        if (frr != NA) part_add<S, false>(part, 1, frr, pr);
-        if (frh != NA) part_add<S, false>(part, 2, frh, ph);
+        /* gate by gate: z of every stream, then r, then h (wave-uniform skips) */
+        if (nfzr > 0) {
+          padd(0, frz, pz);
+          padd(1, frr, pr);
+        }
+        if (nfh > 0) padd(2, frh, ph);
       } else if (TRACE) {
         mf_zr<1>(lds, wz, wr, oz, orr, nzr, vz, vr);
         mf_run<MF_HMAX, 2>(lds, wh, oh, nh, vh);
@@ -397,6 +412,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
              * unconditionally instead: +3 % there, -0.8 % here) */
             int zadd[S], radd[S], hadd[S];
             for (int s = 0; s < S; s++) zadd[s] = radd[s] = hadd[s] = 0;
+            if (S < 4) fp |= 7u << 27; /* S < 4: every row, branch-free (-4 to -5 % at 1 and 256 streams) */
             if (fp >> 27 & 1) {
               part_read<S, false>(part, 0, i, zadd);
               part_clear<S, false>(part, 0, i);
