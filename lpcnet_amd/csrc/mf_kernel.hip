@@ -364,11 +364,18 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
           /* GRU_A input (nnet.c:484-491): all 9*S gathers in flight at once */
           float e[S][9];
           if constexpr (S > 1) {
+            /* split form: every stream's indices read before the first
+             * gather (one LDS wait instead of one per stream: skewed model at
+             * 1024 streams -2.6 %; the unsplit form and mf2_kernel lose
+             * 0.2-1 % with it, so they read stream by stream) */
+            int4 ixv[S];
+            if constexpr (SPLIT)
+              for (int s = 0; s < S; s++) ixv[s] = *(const int4 *)(ix + s * 4);
             for (int s = 0; s < S; s++) {
               /* table base in SGPRs, row + lane offset in one 32-bit VGPR: the
                * global_load saddr form with no scalar address chain per row
                * (gathers 1,520 -> 1,435 cycles at 4 streams; neutral at 1) */
-              const int4 v = *(const int4 *)(ix + s * 4);
+              const int4 v = SPLIT ? ixv[s] : *(const int4 *)(ix + s * 4);
               uint32_t o1 = (uint32_t)tid * 4u + (uint32_t)v.x;
               uint32_t o2 = (uint32_t)tid * 4u + (uint32_t)v.y;
               uint32_t o3 = (uint32_t)tid * 4u + (uint32_t)v.z;
