@@ -221,11 +221,22 @@ __global__ __launch_bounds__(MF_THREADS) void mf2_kernel(SampleArgs A)
         }
         /* the z/r adds go out before the h product and drain beside its
          * MFMAs (2048 streams: -0.9 % frame step; neutral on mf_kernel<4>) */
-        if (frz != NA) part_add<S, true>(pg, 0, frz, pz);
-        if (frr != NA) part_add<S, true>(pg, 1, frr, pr);
+        /* branch-free: a lane of a hosting wave without a piece adds 0 to
+         * its own row's words (skewed model: 2048 / 8192 streams -0.7 /
+         * -0.9 %, three same-box rounds) */
+        auto padd = [&](int gt, int fr_, int (&v)[S]) {
+          const bool h = fr_ != NA;
+          int vv[S];
+          for (int s = 0; s < S; s++) vv[s] = h ? v[s] : 0;
+          part_add<S, true>(pg, gt, h ? fr_ : i, vv);
+        };
+        if (nfzr > 0) {
+          padd(0, frz, pz);
+          padd(1, frr, pr);
+        }
         mf_h_split(xg, wh, oh, nh, nfh, xh, vh, fh);
         for (int s = 0; s < S; s++) ph[s] = fh[0][s] + fh[1][s];
-        if (frh != NA) part_add<S, true>(pg, 2, frh, ph);
+        if (nfh > 0) padd(2, frh, ph);
         for (int s = 0; s < S; s++) {
           iaz[s] = vz[0][s];
           iar[s] = vr[0][s];
