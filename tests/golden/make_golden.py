@@ -136,6 +136,10 @@ def stream_fixture(name, variant, saturating, constants=None, STREAMS=STREAMS, N
     """constants: (LPC_GAMMA, FEATURES_DELAY, END2END) of a trained model's
     nnet_data.h (dump_lpcnet.py:423-446); None = the dump defaults."""
     blob = L.synthetic_model(1, variant, saturating)
+    # the fixture's blob is one the reference's own parser and binders accept
+    # (parse_lpcnet_weights.c compiled unmodified, oracle/ref_parse.c)
+    assert O.have_ref_parser(), "oracle/_ref/ref_parse_* missing: run `make -C oracle`"
+    assert O.ref_parse(blob, variant)[0] == "accept", f"{name}: reference parser rejects the blob"
     d = {"blob_sha256": np.frombuffer(hashlib.sha256(blob).digest(), np.uint8), "variant": np.int32(variant),
          "streams": np.array(STREAMS, np.int32)}
     if constants is not None:

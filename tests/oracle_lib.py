@@ -90,6 +90,38 @@ def have_ref() -> bool:
     return _ref is not None
 
 
+REF_PARSE = {0: os.path.join(ROOT, "oracle", "_ref", "ref_parse_int8"),
+             1: os.path.join(ROOT, "oracle", "_ref", "ref_parse_fp32")}
+
+
+def have_ref_parser() -> bool:
+    return all(os.path.exists(p) for p in REF_PARSE.values())
+
+
+def ref_parse(blob: bytes, variant: int = 0, timeout: float = 5.0):
+    """Run the reference's own parse_weights + layer binders
+    (parse_lpcnet_weights.c, compiled unmodified by oracle/Makefile, driven by
+    oracle/ref_parse.c) on ``blob`` in a fresh process.  Returns (outcome,
+    bound): outcome "accept", "reject" (a binder refused), "parse_reject"
+    (parse_weights refused), "hang" (killed at the timeout: find_idx_check's
+    nb = -1 loop) or "crash" (killed by a signal); bound = {array name:
+    (offset into the blob, bytes)} of the arrays the binders took."""
+    try:
+        r = subprocess.run([REF_PARSE[variant]], input=blob, capture_output=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return "hang", {}
+    if r.returncode < 0:
+        return "crash", {}
+    outcome = {0: "accept", 1: "reject", 2: "parse_reject"}.get(r.returncode)
+    if outcome is None:
+        return "crash", {}
+    bound = {}
+    for line in r.stdout.decode().splitlines():
+        name, off, n = line.split()
+        bound[name] = (int(off), int(n))
+    return outcome, bound
+
+
 def port_kernels():
     return _ora.oracle_port_kernels()
 

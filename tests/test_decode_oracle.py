@@ -143,3 +143,26 @@ def test_oracle_snapshot_round_trip():
     o.restore(snap)
     b = [o.synthesize(feats[f]) for f in range(3, 6)]
     assert np.array_equal(np.stack(a), np.stack(b))
+
+
+def test_append_codebooks_tool_round_trip(tmp_path):
+    """tools/append_codebooks.py rebuilds the codebook-carrying blob from a
+    plain blob and the concatenated codebook arrays; appending again replaces
+    the records instead of duplicating them."""
+    import subprocess
+    import sys
+    import os
+    cb = codebooks(BLOB)
+    flat = np.concatenate([cb["ceps_codebook1"], cb["ceps_codebook2"], cb["ceps_codebook3"],
+                           cb["ceps_codebook_diff4"]]).astype("<f4")
+    base = L.synthetic_model(1, L.VARIANT_INT8)
+    (tmp_path / "w.bin").write_bytes(base)
+    flat.tofile(tmp_path / "cb.f32")
+    tool = os.path.join(O.ROOT, "tools", "append_codebooks.py")
+    for src in ("w.bin", "out.bin"):
+        subprocess.run([sys.executable, tool, str(tmp_path / src), str(tmp_path / "cb.f32"), str(tmp_path / "out.bin")],
+                       check=True)
+        assert (tmp_path / "out.bin").read_bytes() == BLOB
+    bad = subprocess.run([sys.executable, tool, str(tmp_path / "w.bin"), str(tmp_path / "w.bin"),
+                          str(tmp_path / "x.bin")], capture_output=True)
+    assert bad.returncode != 0

@@ -5,14 +5,23 @@ a mutated synthetic blob must make the engine's loader and the CPU oracle
 both refuse it; blobs the reference accepts (records reordered, unknown or
 duplicate records) must still load.
 
+Round 5: the verdict is the REFERENCE's own parser.  oracle/Makefile compiles
+parse_lpcnet_weights.c unmodified (DOT_PROD and DISABLE_DOT_PROD builds)
+behind oracle/ref_parse.c, which runs the binder list dump_lpcnet.py
+generates (dump_lpcnet.py:405-493); every mutation, every fuzz case and every
+synthetic blob the tests use is run through it in a fresh process
+(oracle_lib.ref_parse) and the engine must accept exactly what it accepts.
+
 CPU tests go through lpcnet_mi355x_validate_model (the same parse and checks
 lpcnet_load_model runs, without a device); the -m gpu tests go through
 lpcnet_load_model / lpcnet_batch_load_model themselves.
 
 Two inputs the reference mishandles are rejected here on purpose
 (documented deviations): a negative block count in an idx
-array (find_idx_check loops forever or walks backwards) and a negative
-block position (accepted by find_idx_check, then read out of bounds)."""
+array (find_idx_check then consumes nothing from its count and reads the
+next words as counts -- data-dependent, possibly past the array) and a
+negative block position (accepted by find_idx_check, then read out of
+bounds)."""
 import os
 import struct
 
@@ -136,6 +145,58 @@ def mutated(blob, fn):
     return join(recs)
 
 
+needs_ref_parser = pytest.mark.skipif(not O.have_ref_parser(),
+                                      reason="oracle/_ref parser not built (no /root/reference here)")
+
+
+def _deviation(blob: bytes) -> bool:
+    """True when the reference's find_idx_check (:90-113), walking an idx
+    array it binds (the first record of the name, find_array_entry :79-82),
+    reaches a negative block count (it then consumes nothing from ``remain``
+    and reads the following words -- past the array's end, eventually -- as
+    counts: data-dependent) or lets a negative block position through (pos =
+    -4, -8, ...: 4-aligned and < nb_in - 3, then read out of bounds by
+    sparse_sgemv_accum8x4).  The engine rejects both."""
+    try:
+        recs = records(blob)
+    except (struct.error, UnicodeDecodeError):
+        return False  # not even parse_weights gets that far
+    for name in ("sparse_gru_a_recurrent_weights_idx", "gru_b_weights_idx"):
+        r = next((q for q in recs if q[0] == name), None)
+        if r is None:
+            continue
+        size = struct.unpack_from("<i", r[1], 12)[0]
+        w = np.frombuffer(bytes(r[2][:max(size, 0) // 4 * 4]), np.int32)
+        remain, p = len(w), 0
+        while remain > 0:
+            nb = int(w[p])
+            p += 1
+            if nb < 0:
+                return True
+            if remain < nb + 1:
+                break
+            pos = w[p:p + nb]
+            p += nb
+            if any(x < 0 and x % 4 == 0 for x in pos) and not any(x % 4 or x + 3 >= 384 for x in pos):
+                return True
+            if any(x % 4 or x + 3 >= 384 for x in pos):
+                break
+            remain -= nb + 1
+    return False
+
+
+def engine_expected(blob: bytes, variant: int = 0):
+    """What the engine must do with ``blob``: the reference parser's own
+    verdict, except the two documented deviations where the
+    reference walks a negative block count (data-dependent, may read past
+    the array) or accepts a block it then reads out of bounds (negative
+    position): rejected."""
+    outcome, _ = O.ref_parse(blob, variant)
+    if outcome in ("hang", "crash") or _deviation(blob):
+        return False, outcome
+    return outcome == "accept", outcome
+
+
 def test_records_roundtrip(blob):
     assert join(records(blob)) == blob
     assert L.validate_model(blob) is None
@@ -153,11 +214,63 @@ def test_rejected_by_engine_and_oracle(blob, name):
         O.Oracle(bad)
 
 
+@needs_ref_parser
+@pytest.mark.parametrize("name", sorted(MUTATIONS))
+def test_rejection_table_against_reference_parser(blob, name):
+    """The reference's own parser on every row of the rejection table: it
+    refuses the blob (or, for the two deviation rows, walks a negative count
+    / accepts an out-of-bounds block, which the engine refuses on purpose)."""
+    bad = mutated(blob, MUTATIONS[name])
+    outcome, _ = O.ref_parse(bad)
+    if name == "idx_negative_block_count":
+        assert _deviation(bad)
+    elif name == "idx_negative_position":
+        assert outcome == "accept" and _deviation(bad)
+    else:
+        assert not _deviation(bad)
+        assert outcome in ("reject", "parse_reject"), outcome
+    assert engine_expected(bad)[0] is False
+
+
 @pytest.mark.parametrize("name", sorted(ACCEPTED))
 def test_accepted_by_engine_and_oracle(blob, name):
     good = mutated(blob, ACCEPTED[name])
     L.validate_model(good)
     O.Oracle(good)
+    if O.have_ref_parser():
+        assert O.ref_parse(good)[0] == "accept"
+
+
+@needs_ref_parser
+@pytest.mark.parametrize("variant", [L.VARIANT_INT8, L.VARIANT_FP32])
+@pytest.mark.parametrize("extra", ["plain", "saturating", "skewed", "codebooks", "constants", "constants+codebooks"])
+def test_reference_parser_binds_the_same_arrays(variant, extra):
+    """Every synthetic blob the tests and the bench use is accepted by the
+    reference's parser, and the side records this engine reads (LPC_GAMMA /
+    FEATURES_DELAY / END2END, the ceps_codebook* arrays)
+    are ignored by it: it binds byte-identical arrays with and without them."""
+    v = 0 if variant == L.VARIANT_INT8 else 1
+    sat, skew = extra == "saturating", extra == "skewed"
+    if sat and variant != L.VARIANT_INT8:
+        pytest.skip("saturating is an int8 property")
+    base = L.synthetic_model(1, variant, saturating=sat, skewed=skew)
+    out0, b0 = O.ref_parse(base, v)
+    assert out0 == "accept"
+    L.validate_model(base)
+    blob2 = base
+    if "codebooks" in extra:
+        blob2 = L.synthetic_model(1, variant, codebooks=True)
+    if "constants" in extra:
+        blob2 = L.with_model_constants(blob2, 0.92, 3, True)
+    out1, b1 = O.ref_parse(blob2, v)
+    assert out1 == "accept"
+    L.validate_model(blob2)
+    assert set(b0) == set(b1) and len(b0) == 30
+    for name, (off, n) in b0.items():
+        off1, n1 = b1[name]
+        assert n1 == n
+        if n:
+            assert base[off:off + n] == blob2[off1:off1 + n], name
 
 
 def test_fp32_blob_validates():
@@ -250,10 +363,12 @@ def _fuzz_cases(blob, n, seed):
 @pytest.mark.parametrize("variant", ["int8", "fp32"])
 def test_fuzzed_blobs_engine_and_oracle_agree(variant):
     """200 seeded random corruptions per variant: the engine's loader never
-    crashes, and it accepts exactly the blobs the CPU oracle (the reference's
-    parse rules restated) accepts."""
+    crashes, and it accepts exactly the blobs the reference's own parser
+    (compiled from parse_lpcnet_weights.c, oracle/_ref) accepts -- and the
+    CPU oracle (the same rules restated, which travels to the GPU box) too."""
+    v = 0 if variant == "int8" else 1
     base = L.synthetic_model(1, L.VARIANT_INT8 if variant == "int8" else L.VARIANT_FP32)
-    seen = {"accepted": 0, "rejected": 0}
+    seen = {"accepted": 0, "rejected": 0, "ref_checked": 0, "deviation": 0}
     for k, (kind, b) in enumerate(_fuzz_cases(base, 200, 7 if variant == "int8" else 8)):
         try:
             L.validate_model(b)
@@ -261,13 +376,19 @@ def test_fuzzed_blobs_engine_and_oracle_agree(variant):
         except L.LPCNetError:
             eng = False
         try:
-            O.Oracle(b, 0 if variant == "int8" else 1)
+            O.Oracle(b, v)
             orc = True
         except ValueError:
             orc = False
         assert eng == orc, (k, kind, eng, orc)
+        if O.have_ref_parser():
+            exp, outcome = engine_expected(b, v)
+            assert eng == exp, (k, kind, eng, outcome)
+            seen["ref_checked"] += 1
+            seen["deviation"] += (outcome == "accept") != exp or outcome in ("hang", "crash")
         seen["accepted" if eng else "rejected"] += 1
     assert seen["rejected"] > 50 and seen["accepted"] > 0, seen
+    assert seen["ref_checked"] in (0, 200), seen
 
 
 @pytest.mark.gpu
