@@ -4,8 +4,11 @@
  * Each entry point replaces the symbol of the same name in the reference's
  * include/lpcnet.h (auliaadila/LPCNet, cited as <file>:<line> relative to the
  * reference root) with identical signature, argument meaning and error
- * behaviour.  Only the synthesis subset is provided;
- * encoder / decoder / PLC prototypes of the reference header are out of scope.
+ * behaviour.  Provided: the synthesis entry points
+ * and the 1.6 kb/s decoder (lpcnet_decoder_* / lpcnet_decode, row f4, which
+ * feeds the same synthesis).  The encoder and PLC prototypes of the
+ * reference header are out of scope (the PLC's internal entry points are in
+ * lpcnet_mi355x.h).
  *
  * Behavioural notes versus the reference:
  *  - The reference binds a compiled-in model in lpcnet_init unless built with

@@ -61,6 +61,8 @@ def _load():
         "lpcnet_batch_set_rcp_table": (i, [vp, vp]),
         "lpcnet_mi355x_host_rcp_table": (i, [vp, i]),
         "lpcnet_mi355x_pool_stats": (i, [vp, vp, vp, vp]),
+        "lpcnet_mi355x_set_placement": (i, [vp, i]),
+        "lpcnet_mi355x_handle_placement": (i, [vp, vp, vp]),
         "lpcnet_batch_reset": (None, [vp]),
         "lpcnet_batch_reset_stream": (i, [vp, i]),
         "lpcnet_batch_nb_streams": (i, [vp]),
@@ -176,6 +178,14 @@ def validate_model(blob: bytes) -> None:
 
 def device_count() -> int:
     return lib.lpcnet_mi355x_device_count()
+
+
+def set_placement(devices) -> None:
+    """Placement list of drop-in handles initialised from now on (a device
+    may appear twice); [] restores the default (every visible device)."""
+    arr = (C.c_int * max(len(devices), 1))(*devices)
+    if lib.lpcnet_mi355x_set_placement(arr, len(devices)) != 0:
+        raise LPCNetError(last_error())
 
 
 def synthetic_model(seed: int = 1, variant: int = VARIANT_INT8, saturating: bool = False, skewed: bool = False,
@@ -302,6 +312,13 @@ class LPCNet:
     def restore(self, state: bytes) -> None:
         if lib.lpcnet_mi355x_state_restore(self._st, state) != 0:
             raise LPCNetError(last_error())
+
+    def placement(self) -> tuple[int, int]:
+        """(device, placement index; -1 when pinned by LPCNET_DEVICE)."""
+        d, p = C.c_int(), C.c_int()
+        if lib.lpcnet_mi355x_handle_placement(self._st, C.byref(d), C.byref(p)) != 0:
+            raise LPCNetError(last_error())
+        return d.value, p.value
 
     def close(self) -> None:
         if self._st:

@@ -2586,6 +2586,7 @@ struct StatePool {
   };
   uint64_t key = 0;
   int device = 0;
+  int place = 0; /* placement index (g_pools key) */
   std::vector<unsigned char> blob;
   bool has_codebooks = false;
   Lane lane;
@@ -2615,6 +2616,9 @@ struct StatePool {
 };
 
 static std::mutex g_pools_mu;
+/* (model key, placement) -> pool: one pool per model per placement, so
+ * handles spread over devices (and, for tests, over several placements of
+ * one device) never share a launch across placements */
 static std::map<std::pair<uint64_t, int>, StatePool *> g_pools;
 
 /* Gather window of a combiner: before its launch it waits up to this long
@@ -2646,13 +2650,13 @@ static uint64_t pool_key(const unsigned char *data, int len)
   return h;
 }
 
-/* the pool of (blob, device), created with its model on first use; refs+1 */
-static StatePool *pool_acquire(const unsigned char *data, int len, int device)
+/* the pool of (blob, placement), created with its model on first use; refs+1 */
+static StatePool *pool_acquire(const unsigned char *data, int len, int device, int place)
 {
   if (!data || len <= 0) { set_err("lpcnet_load_model: empty blob"); return nullptr; }
   const uint64_t key = pool_key(data, len);
   std::lock_guard<std::mutex> lk(g_pools_mu);
-  auto it = g_pools.find({key, device});
+  auto it = g_pools.find({key, place});
   if (it != g_pools.end() && it->second->blob.size() == (size_t)len && !memcmp(it->second->blob.data(), data, len)) {
     it->second->refs++;
     return it->second;
@@ -2673,6 +2677,7 @@ static StatePool *pool_acquire(const unsigned char *data, int len, int device)
   StatePool *p = new StatePool();
   p->key = key;
   p->device = device;
+  p->place = place;
   p->blob.assign(data, data + len);
   p->has_codebooks = w->has_codebooks;
   p->lane.work = w;
@@ -2680,7 +2685,7 @@ static StatePool *pool_acquire(const unsigned char *data, int len, int device)
   if (const char *v = getenv("LPCNET_POOL_BROADCAST")) p->broadcast = atoi(v) != 0;
   if (const char *v = getenv("LPCNET_POOL_WINDOW_US")) p->window_us = std::max(0, atoi(v));
   else p->window_us = POOL_WINDOW_US_DEFAULT;
-  g_pools[{key, device}] = p;
+  g_pools[{key, place}] = p;
   return p;
 }
 
@@ -2739,7 +2744,10 @@ static void inbox_push(StatePool *p, StatePool::Req *q)
 {
   StatePool::Req *h = p->inbox.load(std::memory_order_relaxed);
   do q->next = h;
-  while (!p->inbox.compare_exchange_weak(h, q, std::memory_order_release, std::memory_order_relaxed));
+  /* seq_cst: pairs with pool_let_go's busy = 0 / inbox re-load (a
+   * store-then-load hand-off on both sides; release alone would let the
+   * let-go miss this push while our busy CAS still sees it held) */
+  while (!p->inbox.compare_exchange_weak(h, q, std::memory_order_seq_cst, std::memory_order_relaxed));
 }
 
 /* The holder of `busy` lets go: to the slot I/O callers waiting, else to the
@@ -2801,7 +2809,7 @@ static void pool_release(StatePool *p, int slot)
   {
     std::lock_guard<std::mutex> lk(g_pools_mu);
     if (--p->refs > 0) return;
-    g_pools.erase({p->key, p->device});
+    g_pools.erase({p->key, p->place});
   }
   /* unreachable now: no handle holds it and the map no longer lists it */
   if (hipSetDevice(p->device) == hipSuccess) {
@@ -2992,8 +3000,11 @@ static int pool_combine(StatePool *p, StatePool::Req &r)
     if (all.empty()) {
       /* r ran in the launch of the combiner that let the pool go to us: it
        * still posts r's completion, so r's frame must outlive that store */
+      /* r's state is read once: the other combiner may post REQ_DONE at any
+       * moment, and waiting "while state == DONE" would never end */
+      const uint32_t s = r.state.load(std::memory_order_acquire);
       pool_let_go(p);
-      if (r.state.load(std::memory_order_acquire) != REQ_DONE) req_wait(p, r, r.state.load(std::memory_order_acquire));
+      if (s != REQ_DONE) req_wait(p, r, s);
       if (r.rc) set_err(r.err);
       return r.rc;
     }
@@ -3001,7 +3012,9 @@ static int pool_combine(StatePool *p, StatePool::Req &r)
     p->arrivals.fetch_sub((uint32_t)all.size(), std::memory_order_acq_rel);
     std::vector<StatePool::Req *> mine, rest;
     for (StatePool::Req *q : all) (q->same_shape(*all[0]) ? mine : rest).push_back(q);
-    for (auto it = rest.rbegin(); it != rest.rend(); ++it) {
+    /* oldest first onto the stack: the next drain's reversal gives arrival
+     * order again */
+    for (auto it = rest.begin(); it != rest.end(); ++it) {
       inbox_push(p, *it);
       p->arrivals.fetch_add(1, std::memory_order_acq_rel);
     }
@@ -3090,6 +3103,7 @@ constexpr int MAX_FEATURE_BUFFER = 4; /* lpcnet_private.h:26 MAX_FEATURE_BUFFER_
 struct Handle {
   uint64_t token = 0;
   int device = 0;
+  int place = 0; /* placement index: auto placements 0.., LPCNET_DEVICE pins kPinned + device */
   StatePool *pool = nullptr; /* bound model (nullptr: none) */
   int slot = -1;
   /* run_frame_network_deferred's buffer (lpcnet_private.h:37-38, lpcnet.c:122-132) */
@@ -3142,10 +3156,88 @@ static Handle *live_handle(const LPCNetState *st)
   return it->second;
 }
 
+/* ---- placement of drop-in handles over the visible GPUs ------------------
+ * The reference's lpcnet_init/lpcnet_create take no device (lpcnet.c:184-219),
+ * so placement is library policy: each new handle goes to the placement with
+ * the fewest live handles (one slot each once a model is bound), over every
+ * visible device by default, over the list LPCNET_DEVICES="0,1,..." names, or
+ * over lpcnet_mi355x_set_placement()'s list (handles initialised afterwards).
+ * A list may name a device twice: two placements, two pools, one GPU (the
+ * tests use this to exercise placement on a one-GPU box).  LPCNET_DEVICE=d
+ * pins every new handle to device d, as before. */
+constexpr int kMaxPlace = 64;
+constexpr int kPinned = 1 << 20;
+static std::mutex g_place_mu;
+static std::vector<int> g_place_dev; /* placement -> device (empty: not set up yet) */
+static int g_place_load[kMaxPlace];  /* live handles per placement */
+
+static bool parse_device_list(const char *v, std::vector<int> &out)
+{
+  out.clear();
+  while (v && *v) {
+    char *end = nullptr;
+    const long d = strtol(v, &end, 10);
+    if (end == v || d < 0 || d > 1023) return false;
+    out.push_back((int)d);
+    v = end;
+    while (*v == ',' || *v == ' ') v++;
+  }
+  return !out.empty() && out.size() <= (size_t)kMaxPlace;
+}
+
+/* the placement of a new handle (g_place_mu held) */
+static void place_new_handle(Handle *h)
+{
+  if (const char *d = getenv("LPCNET_DEVICE")) {
+    h->device = atoi(d);
+    h->place = kPinned + h->device;
+    return;
+  }
+  if (g_place_dev.empty()) {
+    if (!parse_device_list(getenv("LPCNET_DEVICES"), g_place_dev)) {
+      const int n = std::min(std::max(lpcnet_mi355x_device_count(), 1), kMaxPlace);
+      g_place_dev.clear();
+      for (int k = 0; k < n; k++) g_place_dev.push_back(k);
+    }
+  }
+  int best = 0;
+  for (int k = 1; k < (int)g_place_dev.size(); k++)
+    if (g_place_load[k] < g_place_load[best]) best = k;
+  g_place_load[best]++;
+  h->place = best;
+  h->device = g_place_dev[best];
+}
+
+static void unplace_handle(const Handle *h)
+{
+  std::lock_guard<std::mutex> lk(g_place_mu);
+  if (h->place >= 0 && h->place < kMaxPlace && g_place_load[h->place] > 0) g_place_load[h->place]--;
+}
+
 static void handle_free(Handle *h)
 {
   if (h->pool) pool_release(h->pool, h->slot);
+  unplace_handle(h);
   delete h;
+}
+
+LPCNET_EXPORT int lpcnet_mi355x_set_placement(const int *devices, int n)
+{
+  if (n < 0 || n > kMaxPlace || (n > 0 && !devices)) { set_err("lpcnet_mi355x_set_placement: 0..64 devices"); return -1; }
+  const int ndev = lpcnet_mi355x_device_count();
+  for (int k = 0; k < n; k++)
+    if (devices[k] < 0 || (ndev > 0 && devices[k] >= ndev)) {
+      set_err("lpcnet_mi355x_set_placement: device index outside the visible devices");
+      return -1;
+    }
+  std::lock_guard<std::mutex> lk(g_place_mu);
+  for (int k = 0; k < kMaxPlace; k++)
+    if (g_place_load[k] != 0) {
+      set_err("lpcnet_mi355x_set_placement: live handles still hold placements");
+      return -1;
+    }
+  g_place_dev.assign(devices, devices + n); /* n = 0: back to the default */
+  return 0;
 }
 
 /* unregister st (if live) and release its device resources */
@@ -3188,8 +3280,10 @@ LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
     if (!live) {
       Handle *h = new Handle();
       h->token = new_token();
-      const char *d = getenv("LPCNET_DEVICE");
-      h->device = d ? atoi(d) : 0;
+      {
+        std::lock_guard<std::mutex> plk(g_place_mu);
+        place_new_handle(h);
+      }
       sh.map[st] = h;
       st->magic = kMagic;
       st->reserved = 0;
@@ -3244,7 +3338,7 @@ LPCNET_EXPORT int lpcnet_load_model(LPCNetState *st, const unsigned char *data, 
 {
   Handle *h = live_handle(st);
   if (!h) { set_err("lpcnet_load_model: not an initialised LPCNetState"); return -1; }
-  StatePool *p = pool_acquire(data, len, h->device);
+  StatePool *p = pool_acquire(data, len, h->device, h->place);
   if (!p) return -1;
   if (p == h->pool) {
     pool_release(p, -1); /* same model: keep the binding */
@@ -3357,6 +3451,15 @@ LPCNET_EXPORT void lpcnet_reset_signal(LPCNetState *st)
   pool_slot_io(h->pool, h->slot, nullptr, &s);
 }
 
+LPCNET_EXPORT int lpcnet_mi355x_handle_placement(const LPCNetState *st, int *device, int *placement)
+{
+  Handle *h = live_handle(st);
+  if (!h) { set_err("not an initialised LPCNetState"); return -1; }
+  if (device) *device = h->device;
+  if (placement) *placement = h->place >= kPinned ? -1 : h->place;
+  return 0;
+}
+
 LPCNET_EXPORT int lpcnet_mi355x_state_size(void) { return (int)sizeof(HandleSnapshot); }
 
 LPCNET_EXPORT int lpcnet_mi355x_state_save(LPCNetState *st, void *buf)
@@ -3428,6 +3531,10 @@ LPCNET_EXPORT int lpcnet_decoder_get_size(void) { return (int)sizeof(LPCNetDecSt
 LPCNET_EXPORT int lpcnet_decoder_init(LPCNetDecState *st)
 {
   if (!st) return -1;
+  /* re-initialising a live decoder resets its stream (vq_mem included:
+   * host_reset_state) and keeps its model, as lpcnet_init does for a live
+   * LPCNetState; only a never-initialised (or stale) one starts from zero */
+  if (live_handle(&st->lpcnet_state)) return lpcnet_init(&st->lpcnet_state);
   memset(st, 0, sizeof(*st));
   return lpcnet_init(&st->lpcnet_state);
 }

@@ -112,3 +112,18 @@ def test_decoder_refuses_blob_without_codebooks(require_gpu):
     assert b.info().has_codebooks == 0
     with pytest.raises(L.LPCNetError):
         b.decode(np.zeros((1, 8), np.uint8))
+
+
+def test_decoder_reinit_keeps_model_and_resets_stream(require_gpu):
+    """lpcnet_decoder_init on a live, bound decoder (the reference's way to
+    reset one, lpcnet.c:290-295) resets its stream -- vq_mem included -- and
+    keeps its model: decoding continues without a new load."""
+    pk = packets(1, 4, seed=21)
+    d = L.LPCNetDecoder(BLOB)
+    first = np.stack([d.decode(bytes(pk[p, 0])) for p in range(2)])
+    assert L.lib.lpcnet_decoder_init(d._st) == 0
+    again = np.stack([d.decode(bytes(pk[p, 0])) for p in range(4)])
+    want = oracle_decode(0, pk)
+    assert np.array_equal(first, want[:2])
+    assert np.array_equal(again, want)
+    d.close()

@@ -6,6 +6,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 
 import lpcnet_amd as L
 
@@ -160,3 +161,33 @@ def test_handle_entry_points_fail_cleanly_without_model():
     assert L.lib.lpcnet_decode(d, bytes(8), pcm.ctypes.data) == -1 and np.all(pcm == 0)
     L.lib.lpcnet_decoder_destroy(d)
     L.lib.lpcnet_destroy(st)
+
+
+def test_placement_policy_without_gpu():
+    """Drop-in placement (no device touched before a model is bound): handles
+    go to the least-loaded placement of the list; the list cannot change
+    under live handles; LPCNET_DEVICE pins (placement -1)."""
+    import gc
+    import os
+    gc.collect()
+    L.set_placement([0, 0, 0])
+    try:
+        nets = [L.LPCNet() for _ in range(7)]
+        assert [n.placement() for n in nets] == [(0, k % 3) for k in range(7)]
+        with pytest.raises(L.LPCNetError):
+            L.set_placement([0])
+        nets[1].close()
+        nets[4].close()
+        late = L.LPCNet()  # placement 1 had 2 live handles, now none
+        assert late.placement() == (0, 1)
+        os.environ["LPCNET_DEVICE"] = "0"
+        try:
+            pinned = L.LPCNet()
+            assert pinned.placement() == (0, -1)
+        finally:
+            del os.environ["LPCNET_DEVICE"]
+        for n in nets + [late, pinned]:
+            n.close()
+    finally:
+        gc.collect()
+        L.set_placement([])
