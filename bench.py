@@ -43,6 +43,16 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: int8 MFMA dense = 2x the ~2.5 PF bf16 rate
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2 aggregate, measured
+# MI355X_MICROARCH.md "Indexed rows: gather into LDS": 1,152-B rows shared by
+# every workgroup (served by the XCD's L2) gather at 16.8-18.8 TB/s chip-wide;
+# the upper figure is the peak the sample kernel's embedding gathers are priced at
+L2_GATHER_PEAK_GBS = 18800.0
+# VALU issue: 4 SIMD-32 per CU, one wave64 instruction per 2 cycles each
+# (MI355X_MICROARCH.md "Wave scheduling") = 2 wave64 VALU instructions per
+# CU-cycle, 256 CUs
+VALU_ISSUE_PER_CU_CYCLE = 2.0
+N_CU = 256
+GATHER_BYTES_PER_STREAM_SAMPLE = 3 * 1152 * 4  # three embedding rows, nnet.c:484-491
 
 
 def measured_pmc(config, kernel_name):
@@ -205,7 +215,31 @@ def roofline(info, B, frame_ms, config, frames_per_launch=1.0):
          # L2 hit rate of the gathers (the algorithmic bytes are served by L2)
          "hbm_actual_GBs": traffic / (launch_ms * 1e-3) / 1e9 if traffic else None,
          "l2_hit": pmc.get("l2_hit"),
-         "l2_frac": achieved / L2_PEAK_GBS}
+         "l2_frac": achieved / L2_PEAK_GBS,
+         "pmc_frames_per_launch": pmc.get("frames_per_launch")}
+    # the resource that serves the algorithmic bytes: the gathered embedding
+    # rows come from the XCD's L2 (l2_hit ~0.99), priced at the guide's
+    # shared-row gather rate
+    gath = GATHER_BYTES_PER_STREAM_SAMPLE * 160 * B * frames_per_launch
+    r["roofline_l2"] = {"bound": "l2_gather", "achieved": gath / (launch_ms * 1e-3) / 1e9,
+                        "peak": L2_GATHER_PEAK_GBS, "unit": "GB/s",
+                        "frac": gath / (launch_ms * 1e-3) / 1e9 / L2_GATHER_PEAK_GBS,
+                        "bytes_per_stream_sample": GATHER_BYTES_PER_STREAM_SAMPLE,
+                        "what": "3 embedding rows per stream-sample (nnet.c:484-491) against the 16.8-18.8 TB/s "
+                                "shared-row gather rate of MI355X_MICROARCH.md"}
+    # VALU issue from the PMC pass of this tree (SQ_INSTS_VALU per frame)
+    if "valu_insts_per_frame" in pmc or "valu_insts_per_launch" in pmc:
+        per_frame = pmc.get("valu_insts_per_frame")
+        if per_frame is None:
+            per_frame = pmc["valu_insts_per_launch"] / max(pmc.get("frames_per_launch") or frames_per_launch, 1)
+        insts = per_frame * frames_per_launch
+        peak = VALU_ISSUE_PER_CU_CYCLE * N_CU * (clock_ghz() * 1e9)
+        r["valu"] = {"bound": "valu_issue", "insts_per_stream_sample": per_frame / (160 * B),
+                     "achieved_insts_per_s": insts / (launch_ms * 1e-3), "peak_insts_per_s": peak,
+                     "frac": insts / (launch_ms * 1e-3) / peak, "frac_pmc_busy_cycles": pmc.get("valu_issue_frac"),
+                     "what": "wave64 VALU instructions (SQ_INSTS_VALU) against 2 per CU-cycle x 256 CUs at the "
+                             "2.4 GHz spec clock"}
+    r["binding"] = binding_text(r, pmc)
     mf = None
     if info.mfma_ops_per_group_sample > 0:
         groups = (B + info.streams_per_workgroup - 1) // info.streams_per_workgroup
@@ -213,6 +247,28 @@ def roofline(info, B, frame_ms, config, frames_per_launch=1.0):
         mf = {"achieved_tops": ops / (launch_ms * 1e-3) / 1e12, "peak_tops": I8_PEAK_TOPS,
               "ops_per_launch": ops, "busy_frac_pmc": pmc.get("mfma_util")}
     return r, mf
+
+
+def clock_ghz():
+    """shader clock of the VALU peak: the 2.4 GHz spec maximum (the measured
+    clock under load is lower, so the fraction is a lower bound)"""
+    return 2.4
+
+
+def binding_text(r, pmc):
+    """What actually binds the sample kernel, beside the contract's HBM figure."""
+    parts = []
+    if r.get("hbm_actual_GBs"):
+        parts.append(f"HBM traffic {r['hbm_actual_GBs']:.0f} GB/s = {r['hbm_actual_GBs'] / HBM_PEAK_GBS:.3f} of peak "
+                     f"(weights in registers/LDS, tables in L2, l2_hit {pmc.get('l2_hit', 0):.3f})")
+    parts.append(f"L2 gathers {r['roofline_l2']['frac']:.2f} of the shared-row rate")
+    if "valu" in r:
+        parts.append(f"VALU issue {r['valu']['frac']:.2f} of peak")
+    if pmc.get("mfma_util") is not None:
+        parts.append(f"MFMA busy {pmc['mfma_util']:.2f}")
+    parts.append("none saturated: the per-sample recurrence (walk -> gathers -> GRU_A elementwise -> GRU_B) "
+                 "is a latency chain; see `latency`")
+    return "; ".join(parts)
 
 
 def latency(L, blob, B, measured_ms):
@@ -437,6 +493,86 @@ def capacity(L, blob, args, ladder=(1024, 1025, 1536, 2048, 4096, 8192, 16384, 2
             "steps_per_point": steps, "ladder": {str(k): v for k, v in sorted(rows.items())}}
 
 
+def run_live(L, blob, B, warmup, steps, preheat_ms=0.0):
+    """A live server's tick, frame by frame: every 10 ms of audio the host
+    hands over B feature frames (host memory) and takes back B x 160 PCM
+    samples (host memory) -- lpcnet_batch_synthesize once per frame
+    (lpcnet_demo.c:208-219's loop for B streams at once; PCIe copies, the
+    LPC, frame and sample kernels and the synchronisation all inside the
+    timed region).  Returns (seconds per frame for each timed frame, pcm of
+    the last frame)."""
+    F = warmup + steps
+    feats = np.ascontiguousarray(np.stack([L.synthetic_features(s, F)[:, :20] for s in range(B)], 1), np.float32)
+    b = L.LPCNetBatch(B, int(os.environ.get("LOCAL_RANK", "0")) % max(1, L.device_count()), blob)
+    if preheat_ms > 0:
+        t_end = time.perf_counter() + preheat_ms * 1e-3
+        k = 0
+        while time.perf_counter() < t_end:
+            b.synthesize(feats[k % F])
+            k += 1
+        b.reset()
+    for f in range(warmup):
+        b.synthesize(feats[f])
+    per = []
+    pcm = None
+    for f in range(warmup, F):
+        t0 = time.perf_counter()
+        pcm = b.synthesize(feats[f])
+        per.append(time.perf_counter() - t0)
+    b.close()
+    return np.array(per), pcm
+
+
+def live_line(L, blob, B, args, device_resident_value):
+    nf = max(args.steps, 20)
+    per, _ = run_live(L, blob, B, args.warmup, nf, args.preheat_ms)
+    v = B * 160 * len(per) / per.sum()
+    return {"samples_per_s": v, "ms_per_frame": per.mean() * 1e3, "ms_per_frame_p50": float(np.median(per)) * 1e3,
+            "ms_per_frame_max": float(per.max()) * 1e3, "frames": len(per),
+            "vs_device_resident": v / device_resident_value if device_resident_value else None,
+            "what": "host features in, host PCM out, one lpcnet_batch_synthesize per 10 ms frame "
+                    "(PCIe-inclusive; the headline `value` keeps the inputs resident in HBM)"}
+
+
+def capacity_live(L, blob, ladder=(1024, 2048, 4096, 8192, 16384, 24576, 28672, 32768)):
+    """capacity() for the live tick: the largest batch whose per-frame
+    host-I/O step (lpcnet_batch_synthesize: features from host memory, PCM
+    to host memory) stays within 10 ms, bracketed by bisection in steps of
+    256."""
+    steps = 6
+    rows = {}
+
+    def run(B):
+        per, _ = run_live(L, blob, B, 2, steps)
+        ms = per.mean() * 1e3
+        rows[B] = {"frame_step_ms": ms, "frame_step_ms_max": float(per.max()) * 1e3,
+                   "samples_per_s": B * 160 / per.mean(), "realtime": ms <= 10.0}
+        return ms
+
+    ok, bad = 0, None
+    for B in ladder:
+        if run(B) <= 10.0:
+            ok = max(ok, B)
+        else:
+            bad = B
+            break
+    if bad is not None:
+        lo, hi = ok, bad
+        while hi - lo > 256:
+            mid = (lo + hi) // 2 // 256 * 256
+            if mid <= lo:
+                break
+            if run(mid) <= 10.0:
+                lo = mid
+            else:
+                hi = mid
+        ok = lo
+    return {"max_realtime_streams": ok,
+            "criterion": "per-frame host-I/O step (features in / PCM out over PCIe, one call per frame) <= 10 ms, "
+                         "measured mean of the timed frames",
+            "steps_per_point": steps, "ladder": {str(k): v for k, v in sorted(rows.items())}}
+
+
 def skewed_lines(L, args):
     """A trained-model-like sparsity pattern (Sparsify's global per-gate
     threshold over skewed block energies, training_tf2/lpcnet.py:140-160:
@@ -548,8 +684,12 @@ def main():
         out["skewed_int8"] = skewed_lines(L, args)
         out["lockstep"] = lockstep_lines(L, args)
         out["host_rcpps"] = host_rcpps_lines(L, args)
+    if rank == 0 and world == 1 and not args.no_batch1:
+        # the same workload as a live server runs it: host I/O every frame
+        out["live"] = live_line(L, blob, B, args, value)
     if rank == 0 and world == 1 and not args.no_capacity:
         out["capacity"] = capacity(L, blob, args)
+        out["capacity_live"] = capacity_live(L, blob)
         # the same ladder on the trained-like (Sparsify) sparsity pattern
         out["capacity_skewed"] = capacity(L, L.synthetic_model(1, L.VARIANT_INT8, skewed=True), args)
     if rank == 0 and world == 1 and not args.no_cpu:

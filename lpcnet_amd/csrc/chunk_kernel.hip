@@ -63,27 +63,44 @@ struct CkGeom {
   static constexpr int FLOATS = R0 + R1 + R2;
 };
 
-/* Row tile rt (16 rows) of a layer for the 4 column tiles:
+/* Row tile of a layer for the column tiles:
  *   acc[j][i] = bias[row] + sum_k W[k][row] * X(col, k),  row = 16 rt + 4 g + i,
  * col = 16 j + (lane & 15), the chain in k order.  X(col, k) =
  * xs[xb[j] + (k / SEG) * SST + k % SEG]: a column's inputs as segments of SEG
- * values SST apart (conv windows over padded frame rows). */
-template <int K, int NOUT, int SEG, int SST, int NCT>
-__device__ __forceinline__ void ck_tile(const float *__restrict__ W, const float *__restrict__ bias, int rt,
-                                        const float *xs, const int (&xb)[NCT], f32x4 (&acc)[NCT])
+ * values SST apart (conv windows over padded frame rows).
+ * Weights: the row tile's re-tiled copy (FrameArgs::ck_*, one float4 per
+ * lane = 4 k steps) through a ring of CK_WPAD quads in registers that streams
+ * the wave's whole sequence of row tiles -- conv1, conv2, dense1, dense2 and
+ * its projection tiles -- so the next tile's quads (and bias) are in flight
+ * while this tile's chain runs (each tile's first loads no longer wait a
+ * full Infinity-Cache round trip: a one-frame launch spent ~40 of its ~50 us
+ * there).  Every layer's quad count is a multiple of CK_WPAD, so the ring's
+ * phase is 0 at every tile start. */
+struct CkRing {
+  float4 w[CK_WPAD];
+  float4 b; /* the current tile's bias quad (rows 16 rt + 4 g ..) */
+};
+
+__device__ __forceinline__ void ck_prime(CkRing &R, const float4 *tile, const float *bias)
+{
+#pragma unroll
+  for (int d = 0; d < CK_WPAD; d++) R.w[d] = tile[(size_t)d * 64];
+  R.b = *(const float4 *)bias;
+}
+
+template <int K, int SEG, int SST, int NCT>
+__device__ __forceinline__ void ck_tile(CkRing &R, const float4 *__restrict__ cur, const float4 *__restrict__ nxt,
+                                        const float *nbias, const float *xs, const int (&xb)[NCT], f32x4 (&acc)[NCT])
 {
   static_assert(K % 4 == 0 && SEG % 4 == 0, "k quads stay inside a segment");
   constexpr int KS = K / 4;
-  constexpr int PD = 16; /* weight fragments in flight */
-  static_assert(4 * PD <= FRAME_PREFETCH, "prefetch beyond the padding");
-  const int l = threadIdx.x & 63, g = l >> 4, r = l & 15;
-  const float *wp = W + (size_t)g * NOUT + 16 * rt + r;
-  float w[PD];
+  constexpr int NQ = (KS + 3) / 4;
+  constexpr int PQ = CK_WPAD;
+  static_assert(NQ % PQ == 0, "ring phase 0 at every tile start");
+  const int g = (threadIdx.x & 63) >> 4;
 #pragma unroll
-  for (int d = 0; d < PD; d++) w[d] = wp[(size_t)(4 * d) * NOUT];
-  const float4 b4 = *(const float4 *)(bias + 16 * rt + 4 * g);
-#pragma unroll
-  for (int j = 0; j < NCT; j++) acc[j] = f32x4{b4.x, b4.y, b4.z, b4.w};
+  for (int j = 0; j < NCT; j++) acc[j] = f32x4{R.b.x, R.b.y, R.b.z, R.b.w};
+  if (nbias) R.b = *(const float4 *)nbias; /* the next tile's bias, in flight beside this chain */
   float xv[NCT], xn[NCT];
 #pragma unroll
   for (int j = 0; j < NCT; j++) xv[j] = xs[xb[j] + g];
@@ -94,22 +111,46 @@ __device__ __forceinline__ void ck_tile(const float *__restrict__ W, const float
 #pragma unroll
       for (int j = 0; j < NCT; j++) xn[j] = xs[xb[j] + g + o];
     }
-    const float a = w[kk % PD];
+    const int q = kk / 4;
+    const float4 &wq = R.w[q % PQ];
+    const float a = (kk & 3) == 0 ? wq.x : (kk & 3) == 1 ? wq.y : (kk & 3) == 2 ? wq.z : wq.w;
 #pragma unroll
     for (int j = 0; j < NCT; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xv[j], acc[j], 0, 0, 0);
-    w[kk % PD] = wp[(size_t)(4 * (kk + PD)) * NOUT];
+    if ((kk & 3) == 3 || kk + 1 == KS) {
+      /* quad q consumed: its slot takes quad q + PQ of this tile, past the
+       * tile's end the next tile's first quads */
+      if (q + PQ < NQ)
+        R.w[q % PQ] = cur[(size_t)(q + PQ) * 64];
+      else if (nxt)
+        R.w[q % PQ] = nxt[(size_t)(q + PQ - NQ) * 64];
+    }
 #pragma unroll
     for (int j = 0; j < NCT; j++) xv[j] = xn[j];
   }
 }
 
+/* quads per row tile of a re-tiled K-input matrix, padding included */
+constexpr int ck_tq(int K) { return (K / 4 + 3) / 4 + CK_WPAD; }
+
 /* frame_count before frame f's update, given its value fc0 at the chunk start
  * (lpcnet.c:119: incremented while below 1000) */
 __device__ __forceinline__ int ck_fc(int fc0, int f) { return fc0 >= 1000 ? fc0 : min(fc0 + f, 1000); }
 
+/* diagnostics (CK_STAMPS builds only, tools/ab_build.sh): s_memtime at the
+ * phase boundaries of workgroup 0, wave 0, printed once per launch */
+#ifdef CK_STAMPS
+#define CK_T(k) do { if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) ck_t[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define CK_T(k) do { } while (0)
+#endif
+
 template <int NFR, int SC, bool HWR>
 __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
 {
+#ifdef CK_STAMPS
+  unsigned long long ck_t[10] = {};
+#endif
+  CK_T(0);
   using G = CkGeom<NFR, SC>;
   constexpr int NCT = G::NCT;
   extern __shared__ float4 lds4_[];
@@ -161,6 +202,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   }
   if (tid < G::SC) fcs[tid] = s0 + tid < B ? A.st[s0 + tid].frame_count : 1000;
   __syncthreads();
+  CK_T(1);
 
   /* this lane's column of each column tile */
   int cs[NCT], cf[NCT];
@@ -171,11 +213,22 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   }
   int xb[NCT];
   f32x4 acc[NCT];
+  /* this wave's weight stream: conv1, conv2, dense1, dense2 row tile `wave`,
+   * then projection tiles wave, wave + 8, ... (ck_tile) */
+  const int l64 = tid & 63;
+  const float4 *t_c1 = A.ck_conv1 + (size_t)wave * ck_tq(3 * FIN) * 64 + l64;
+  const float4 *t_c2 = A.ck_conv2 + (size_t)wave * ck_tq(3 * COND) * 64 + l64;
+  const float4 *t_d1 = A.ck_dense1 + (size_t)wave * ck_tq(COND) * 64 + l64;
+  const float4 *t_d2 = A.ck_dense2 + (size_t)wave * ck_tq(COND) * 64 + l64;
+  auto t_pj = [&](int rt) { return A.ck_proj + (size_t)rt * ck_tq(COND) * 64 + l64; };
+  const int bo = 16 * wave + 4 * g; /* this lane's bias quad in a 128-row layer */
+  CkRing R;
+  ck_prime(R, t_c1, A.conv1_b + bo);
 
   /* conv1 (nnet.c:452-470): 252 inputs -> 128, tanh; cleared while frame_count < 1 (lpcnet.c:99) */
 #pragma unroll
   for (int j = 0; j < NCT; j++) xb[j] = cs[j] * G::IN_SS + cf[j] * FIN; /* window = frames f-2..f */
-  ck_tile<3 * FIN, COND, 3 * FIN, 3 * FIN>(A.conv1_w, A.conv1_b, wave, inl, xb, acc);
+  ck_tile<3 * FIN, 3 * FIN, 3 * FIN>(R, t_c1, t_c2, A.conv2_b + bo, inl, xb, acc);
 #pragma unroll
   for (int j = 0; j < NCT; j++) {
     const bool clr = ck_fc(fcs[cs[j]], cf[j]) < 1;
@@ -188,6 +241,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   }
   __syncthreads();
 
+  CK_T(2);
   /* the conv1 memory after the chunk: inputs of frames n-2, n-1 (nnet.c:469) */
   for (int e = tid; e < G::SC * 2 * FIN; e += CK_THREADS) {
     const int s = e / (2 * FIN), j = e % (2 * FIN), sid = s0 + s;
@@ -196,7 +250,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   /* conv2: 384 inputs -> 128, tanh; cleared while frame_count < FEATURES_DELAY (lpcnet.c:101) */
 #pragma unroll
   for (int j = 0; j < NCT; j++) xb[j] = cs[j] * G::C1_SS + cf[j] * CK_RS;
-  ck_tile<3 * COND, COND, COND, CK_RS>(A.conv2_w, A.conv2_b, wave, c1, xb, acc);
+  ck_tile<3 * COND, COND, CK_RS>(R, t_c2, t_d1, A.dense1_b + bo, c1, xb, acc);
 #pragma unroll
   for (int j = 0; j < NCT; j++) {
     const bool clr = ck_fc(fcs[cs[j]], cf[j]) < D;
@@ -209,17 +263,18 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   }
   __syncthreads();
 
+  CK_T(3);
   /* dense1, dense2 (lpcnet.c:104-105) */
 #pragma unroll
   for (int j = 0; j < NCT; j++) xb[j] = (16 * j + r) * CK_RS;
-  ck_tile<COND, COND, COND, CK_RS>(A.dense1_w, A.dense1_b, wave, ya, xb, acc);
+  ck_tile<COND, COND, CK_RS>(R, t_d1, t_d2, A.dense2_b + bo, ya, xb, acc);
 #pragma unroll
   for (int j = 0; j < NCT; j++)
     *(float4 *)&yb[(16 * j + r) * CK_RS + 16 * wave + 4 * g] =
         make_float4(tanh_x86<HWR>(acc[j][0], rcp), tanh_x86<HWR>(acc[j][1], rcp), tanh_x86<HWR>(acc[j][2], rcp),
                     tanh_x86<HWR>(acc[j][3], rcp));
   __syncthreads();
-  ck_tile<COND, COND, COND, CK_RS>(A.dense2_w, A.dense2_b, wave, yb, xb, acc);
+  ck_tile<COND, COND, CK_RS>(R, t_d2, t_pj(wave), A.proj_b + bo, yb, xb, acc);
 #pragma unroll
   for (int j = 0; j < NCT; j++)
     *(float4 *)&ya[(16 * j + r) * CK_RS + 16 * wave + 4 * g] =
@@ -227,6 +282,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
                     tanh_x86<HWR>(acc[j][3], rcp));
   __syncthreads();
 
+  CK_T(4);
   /* END2END models (lpcnet.c:104,107-108): each frame's LPC = rc2lpc of the
    * first LPC_ORDER conditioning values, weighted by LPC_GAMMA; one lane per
    * (stream, frame) column */
@@ -257,7 +313,9 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
    * to cond[f], the last frame's also to the stream state */
 #pragma unroll 1
   for (int rt = wave; rt < CK_PROJ_TILES; rt += CK_THREADS / 64) {
-    ck_tile<COND, CK_PROJ, COND, CK_RS>(A.proj_w, A.proj_b, rt, ya, xb, acc);
+    const int rn = rt + CK_THREADS / 64;
+    ck_tile<COND, COND, CK_RS>(R, t_pj(rt), rn < CK_PROJ_TILES ? t_pj(rn) : nullptr,
+                               rn < CK_PROJ_TILES ? A.proj_b + 16 * rn + 4 * g : nullptr, ya, xb, acc);
 #pragma unroll
     for (int j = 0; j < NCT; j++) {
       const int sid = s0 + cs[j], f = cf[j];
@@ -275,6 +333,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
     }
   }
 
+  CK_T(5);
   /* per frame: the LPC it synthesises with (lpcnet.c:110-118: the ring's
    * oldest slot, i.e. lpc_from_cepstrum of frame f - FEATURES_DELAY, then
    * lpc_weighting; END2END: written above) and frame_count after its update */
@@ -307,6 +366,13 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
     }
   }
   if (tid < G::SC && s0 + tid < B) A.st[s0 + tid].frame_count = ck_fc(fcs[tid], n);
+#ifdef CK_STAMPS
+  CK_T(6);
+  if (blockIdx.x == 0 && tid == 0)
+    printf("ck<%d,%d> grid %d: inputs %llu conv1 %llu conv2 %llu dense %llu proj %llu epi %llu total %llu\n", NFR, SC,
+           (int)gridDim.x, ck_t[1] - ck_t[0], ck_t[2] - ck_t[1], ck_t[3] - ck_t[2], ck_t[4] - ck_t[3], ck_t[5] - ck_t[4],
+           ck_t[6] - ck_t[5], ck_t[6] - ck_t[0]);
+#endif
 }
 
 template <int NFR, int SC, bool HWR>
@@ -330,6 +396,12 @@ static int launch_chunk_h(const FrameArgs &a, void *stream)
   const int cus = current_device_cus();
   /* estimated time: rounds of workgroups x column tiles per workgroup */
   auto cost = [&](int sc, int nct) { return ((a.nstreams + sc - 1) / sc + cus - 1) / cus * nct; };
+  /* one frame (the per-frame host-I/O path of large batches: a live server's
+   * 10 ms tick): stream-only columns, 16 or 32 streams per workgroup -- a
+   * workgroup's time is mostly its pass over the 1.08 MB of weights, so the
+   * smaller tile while the grid fits two rounds */
+  if (a.nframes == 1)
+    return (a.nstreams + 15) / 16 <= 2 * cus ? launch_chunk_t<1, 16, HWR>(a, stream) : launch_chunk_t<1, 32, HWR>(a, stream);
   if (a.nframes <= 8) return launch_chunk_t<8, 8, HWR>(a, stream);
   if (a.nframes <= 16) return launch_chunk_t<16, 4, HWR>(a, stream);
   if (a.nframes <= 20 && cost(4, 5) < cost(2, 4)) return launch_chunk_t<20, 4, HWR>(a, stream);

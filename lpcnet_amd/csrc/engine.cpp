@@ -352,6 +352,12 @@ struct LPCNetBatch {
    * frame f in d_chunk[f][B] */
   FrameCond *d_chunk = nullptr;
   bool chunking = true;
+  /* per-frame host-I/O path of large batches (synth_first): one frame's
+   * chunk_kernel outputs [B], and pinned staging of the caller's features and
+   * PCM (so both copies are asynchronous, behind one synchronisation) */
+  FrameCond *d_cond1 = nullptr;
+  float *h_io_feat = nullptr;
+  short *h_io_pcm = nullptr;
   /* trace */
   bool trace = false;
   float *d_trace_logits = nullptr;
@@ -1475,6 +1481,37 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     UP(fa.proj_w, pw.data(), pw.size() * 4);
     UP(fa.proj_b, pb.data(), pb.size() * 4);
   }
+  {
+    /* chunk_kernel's copies: each row tile's k steps as per-lane float4 quads
+     * (one 1 KiB wave-instruction per 4 k steps instead of 256 B per step:
+     * the kernel streams the weights from the Infinity Cache with 4x the
+     * bytes in flight per CU) */
+    auto tiled = [](const float *w, int nin, int nout) {
+      const int ks = nin / 4, nq = (ks + 3) / 4, nrt = nout / 16;
+      std::vector<float> t((size_t)nrt * (nq + CK_WPAD) * 64 * 4, 0.f);
+      for (int rt = 0; rt < nrt; rt++)
+        for (int q = 0; q < nq; q++)
+          for (int l = 0; l < 64; l++)
+            for (int j = 0; j < 4; j++) {
+              const int k = 4 * (4 * q + j) + (l >> 4), row = 16 * rt + (l & 15);
+              if (k < nin) t[(((size_t)rt * (nq + CK_WPAD) + q) * 64 + l) * 4 + j] = w[(size_t)k * nout + row];
+            }
+      return t;
+    };
+    std::vector<float> pwf((size_t)COND * (GA_ROWS + GB_ROWS));
+    for (int j = 0; j < COND; j++) {
+      memcpy(&pwf[(size_t)j * (GA_ROWS + GB_ROWS)], gadf_w + (size_t)j * GA_ROWS, GA_ROWS * 4);
+      memcpy(&pwf[(size_t)j * (GA_ROWS + GB_ROWS) + GA_ROWS], gbdf_w + (size_t)j * GB_ROWS, GB_ROWS * 4);
+    }
+    std::vector<float> t1 = tiled(conv1_w, 3 * FIN, COND), t2 = tiled(conv2_w, 3 * COND, COND);
+    std::vector<float> t3 = tiled(dense1_w, COND, COND), t4 = tiled(dense2_w, COND, COND);
+    std::vector<float> t5 = tiled(pwf.data(), COND, GA_ROWS + GB_ROWS);
+    UP(fa.ck_conv1, t1.data(), t1.size() * 4);
+    UP(fa.ck_conv2, t2.data(), t2.size() * 4);
+    UP(fa.ck_dense1, t3.data(), t3.size() * 4);
+    UP(fa.ck_dense2, t4.data(), t4.size() * 4);
+    UP(fa.ck_proj, t5.data(), t5.size() * 4);
+  }
   UP(fa.embed_pitch, embed_pitch, 256 * EP * 4);
   UP(fa.rcp, rcp_dev.data(), RCP_ENTRIES * 4);
   UP(sa.emb_sig, emb_sig, 256 * GA_ROWS * 4);
@@ -1974,6 +2011,9 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
   (void)hipFree(b->d_lpc);
   (void)hipFree(b->d_lpc_tab);
   (void)hipFree(b->d_chunk);
+  (void)hipFree(b->d_cond1);
+  (void)hipHostFree(b->h_io_feat);
+  (void)hipHostFree(b->h_io_pcm);
   (void)hipFree(b->d_packets);
   (void)hipFree(b->d_dfeat);
   (void)hipFree(b->d_dpcm);
@@ -2079,6 +2119,83 @@ LPCNET_EXPORT void lpcnet_batch_reset(LPCNetBatch *b)
  * synchronisation (the drop-in pool's state scatter). */
 using PreSync = std::function<int()>;
 
+/* One frame of a large batch in the chunked form (a live server's tick:
+ * lpcnet_batch_synthesize once per 10 ms): lpc_kernel, chunk_kernel with
+ * stream-only columns (weights fetched once per 16-32 streams instead of the
+ * per-frame frame_kernel's once per 4: at 1024 streams ~44 -> ~20 us, at
+ * 28 K streams 28 rounds of workgroups -> 2-4), then the sample kernel
+ * reading the outputs from d_cond1.  Same arithmetic as every other frame
+ * path (the chunk kernel is bit-identical to the frame kernel). */
+static bool single_frame_chunked(const LPCNetBatch *b, int nB, int N, int preload)
+{
+  return b->chunking && (b->mf || b->fp) && nB > OVERLAP_MAX_STREAMS && N > 0 && preload == 0 && !b->d_stamps &&
+         !b->sa.trace_logits && !getenv("LPCNET_NO_CHUNK");
+}
+
+static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_features, short *d_pcm, int N)
+{
+  if (!b->d_cond1) HIPCHK(hipMalloc(&b->d_cond1, sizeof(FrameCond) * (size_t)b->B));
+  if (!b->mc.end2end && launch_lpc(d_features, b->d_lpc, nB, b->d_lpc_tab, b->stream)) {
+    set_err("lpc kernel launch failed");
+    return -1;
+  }
+  FrameArgs fa = b->fa;
+  fa.st = b->d_state;
+  fa.mc = b->mc;
+  fa.nstreams = nB;
+  fa.features = d_features;
+  fa.lpc_new = b->d_lpc;
+  fa.nframes = 1;
+  fa.cond = b->d_cond1;
+  fa.stamps = nullptr;
+  hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+  if (b->timing >= 2) e[0] = get_event(b);
+  if (b->timing >= 1) {
+    e[1] = get_event(b);
+    e[2] = get_event(b);
+  }
+  if (e[0]) HIPCHK(hipEventRecord(e[0], b->stream));
+  if (launch_chunk(fa, b->stream)) {
+    set_err("chunk kernel launch failed");
+    return -1;
+  }
+  b->frames_done(1);
+  SampleArgs sa = b->sa;
+  sa.st = b->d_state;
+  sa.delay = b->mc.delay;
+  sa.cond = b->d_cond1;
+  sa.nstreams = nB;
+  sa.N = N;
+  sa.nframes = 1;
+  sa.pcm = d_pcm;
+  sa.preload = 0;
+  sa.stamps = nullptr;
+  sa.status = b->d_status;
+  sa.spin_limit = b->spin_limit;
+  if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
+  const int lrc = b->fp ? launch_fp(sa, b->stream)
+                  : b->mf2 ? launch_mf2(sa, 4, b->stream)
+                           : launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream);
+  if (lrc) {
+    set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return -1;
+  }
+  if (e[2]) HIPCHK(hipEventRecord(e[2], b->stream));
+  if (e[0]) {
+    b->ev_pairs[1].push_back(e[0]);
+    b->ev_pairs[1].push_back(e[1]);
+    b->ev_frames[1].push_back(1);
+  }
+  if (e[1]) {
+    b->ev_pairs[0].push_back(e[1]);
+    b->ev_pairs[0].push_back(e[2]);
+    b->ev_frames[0].push_back(1);
+  }
+  for (hipEvent_t x : e)
+    if (x) b->ev_taken.push_back(x);
+  return 0;
+}
+
 /* one frame for the first nB streams of a batch, host I/O ([nB][NF] in,
  * [nB][N] out) */
 static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm, int N, int preload,
@@ -2088,6 +2205,20 @@ static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm
   if (N < 0 || N > FRAME || !features || (N > 0 && !pcm) || preload < 0) { set_err("bad arguments"); return -1; }
   if (b->set_device()) return -1;
   if (ensure_trace(b, N)) return -1;
+  if (!staged && !pre && single_frame_chunked(b, nB, N, preload)) {
+    /* the caller's buffers through pinned staging: both copies truly
+     * asynchronous, one synchronisation per frame */
+    if (!b->h_io_feat) HIPCHK(hipHostMalloc(&b->h_io_feat, sizeof(float) * NF * (size_t)b->B, hipHostMallocDefault));
+    if (!b->h_io_pcm) HIPCHK(hipHostMalloc(&b->h_io_pcm, sizeof(short) * FRAME * (size_t)b->B, hipHostMallocDefault));
+    memcpy(b->h_io_feat, features, sizeof(float) * NF * nB);
+    HIPCHK(hipMemcpyAsync(b->d_feat, b->h_io_feat, sizeof(float) * NF * nB, hipMemcpyHostToDevice, b->stream));
+    if (launch_single_frame_chunked(b, nB, b->d_feat, b->d_pcm, N)) return -1;
+    HIPCHK(hipMemcpyAsync(b->h_io_pcm, b->d_pcm, sizeof(short) * N * nB, hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    if (check_status(b)) return -1;
+    memcpy(pcm, b->h_io_pcm, sizeof(short) * N * nB);
+    return 0;
+  }
   /* everything below is ordered after work already queued on b->stream
    * (staged: the caller has queued the features / preload copies already) */
   if (!staged) {

@@ -161,7 +161,13 @@ struct FrameArgs {
    * and frame_count advance, the state's conditioning and lpc stay */
   int keep_cond;
   int rcp_hw; /* chunk_kernel: hardware-reciprocal tanh allowed (see SampleArgs::rcp_hw) */
+  /* chunk_kernel: the same five weight matrices re-tiled for 16-byte
+   * per-lane loads (ck_tile_weights): [row tile][k quad][64 lanes] float4,
+   * lane l = (g, r) = (l / 16, l % 16), element j of quad q = W[4 (4q + j) +
+   * g][16 rt + r] (0 past K), CK_WPAD zero quads after each row tile's last */
+  const float4 *ck_conv1, *ck_conv2, *ck_dense1, *ck_dense2, *ck_proj;
 };
+constexpr int CK_WPAD = 8; /* chunk_kernel: k quads in flight per wave (zero padding of each row tile) */
 
 struct SampleArgs {
   StreamState *st;

@@ -1,5 +1,6 @@
 """Sharded multi-rank path (streams shard, no data-path
-collective), world size 2 over gloo.
+collective), world sizes 2, 4 and 8 over gloo (stream s
+gives identical PCM for G in {1, 2, 4, 8}).
 
 * CPU (no GPU needed): the rank/shard plumbing with the CPU ORACLE standing
   in for the per-rank engine -- each rank synthesises its own shard of
@@ -64,11 +65,12 @@ def test_shard_ranges_partition():
     assert list(weak_shard(3, 1024)) == list(range(3072, 4096))
 
 
-def test_two_rank_gloo_shard_invariance():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_two_rank_gloo_shard_invariance(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     sums, maxlen = q.get(timeout=240)
@@ -79,7 +81,7 @@ def test_two_rank_gloo_shard_invariance():
     blob = L.synthetic_model(1, 0)
     single = [int(np.abs(_stream_pcm(blob, sid).astype(np.int64)).sum()) for sid in range(TOTAL)]
     assert sums == single
-    assert maxlen == 3.0
+    assert maxlen == float(max(len(shard_range(r, world, TOTAL)) for r in range(world)))
 
 
 def _engine_worker(rank, world, port, out, per_rank, frames):
@@ -102,15 +104,17 @@ def _engine_worker(rank, world, port, out, per_rank, frames):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("per_rank,frames", [(96, 6), (1024, 10)])
-def test_two_rank_engine_shard_invariance(require_gpu, per_rank, frames):
+@pytest.mark.parametrize("world,per_rank,frames", [(2, 96, 6), (2, 1024, 10), (4, 128, 6), (8, 64, 6)])
+def test_two_rank_engine_shard_invariance(require_gpu, world, per_rank, frames):
     """per_rank 96: mf_kernel<1> with the overlapped per-frame frame kernel
     (<= 128 streams); per_rank 1024 is BASELINE configs[4]'s own per-GPU
     size: each rank runs mf_kernel<4>, the chunked frame network and the
-    multi-frame sample launches, exactly as `bench.py --gpus N` does."""
+    multi-frame sample launches, exactly as `bench.py --gpus N` does.
+    World sizes 4 and 8 (all ranks sharing the one GPU): 128 / 64 streams per
+    rank on the overlapped path against one 512-stream process on the chunked
+    mf_kernel<2> path, and the oracle on a stream of every shard."""
     import bench
     import lpcnet_amd as L
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -126,6 +130,12 @@ def test_two_rank_engine_shard_invariance(require_gpu, per_rank, frames):
     assert sharded.shape == single.shape == (frames, world * per_rank, 160)
     assert np.array_equal(sharded, single.astype(np.int32))
     assert np.abs(single[2:].astype(np.float64)).mean() > 100
+    if world > 2:
+        import oracle_lib as O
+        for r in range(world):
+            sid = r * per_rank + (r * 37) % per_rank
+            ref = O.synth_stream(blob, L.synthetic_features(sid, frames)[:, :20], 0)
+            assert np.array_equal(single[:, sid], ref), sid
     if per_rank >= 1024:
         # the single-process 2048-stream run takes mf2_kernel (two staggered
         # 4-stream groups per workgroup), each rank's 1024 streams mf_kernel<4>:

@@ -739,3 +739,30 @@ def test_bench_preheat_computes_the_same_frames(require_gpu, blobs):
     _, _, _, warm = bench.run_batch(L, blob, 64, 0, 3, 6, None, 1, 20.0)
     assert np.array_equal(cold, warm)
     assert np.abs(cold[3:].astype(np.int64)).sum() > 0
+
+
+@pytest.mark.parametrize("variant,skewed,B", [(0, False, 300), (0, False, 1030), (0, True, 1030), (0, False, 2100),
+                                              (1, False, 200)])
+def test_live_single_frame_chunked_matches_oracle(require_gpu, monkeypatch, variant, skewed, B):
+    """The per-frame host-I/O path of large batches (lpcnet_batch_synthesize
+    once per frame: a live server's 10 ms tick) runs lpc_kernel +
+    chunk_kernel<1, SC> (stream-only columns) + the sample kernel reading
+    the frame's outputs from FrameCond: PCM identical to the per-frame
+    frame_kernel path (LPCNET_NO_CHUNK=1) on every stream and to the oracle
+    on sampled streams -- through the silent FEATURES_DELAY frames, mf_kernel
+    (incl. its split form for the skewed model), mf2_kernel (2100 streams,
+    one ragged workgroup) and fp_kernel."""
+    blob = L.synthetic_model(1, variant, skewed=skewed)
+    F = 6
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    b = L.LPCNetBatch(B, 0, blob)
+    got = np.stack([b.synthesize(allf[f]) for f in range(F)], 1)
+    b.close()
+    monkeypatch.setenv("LPCNET_NO_CHUNK", "1")
+    b2 = L.LPCNetBatch(B, 0, blob)
+    per = np.stack([b2.synthesize(allf[f]) for f in range(F)], 1)
+    b2.close()
+    assert np.array_equal(got, per)
+    for s in sorted({0, 1, B // 2, B - 1}):
+        o = O.Oracle(blob, variant)
+        assert np.array_equal(got[s], np.stack([o.synthesize(allf[f, s]) for f in range(F)])), s

@@ -23,7 +23,7 @@ echo "trace ok"
 # PMC passes: one counter group per run (slot limits, MI355X_MICROARCH.md)
 for cfg in "b1024:--streams 1024" "b256:--streams 256" "b1:--streams 1" "b1_fp32:--streams 1 --variant fp32"; do
   name=${cfg%%:*}; args=${cfg#*:}
-  for pass in "fetch:FETCH_SIZE" "write:WRITE_SIZE" "l2:TCC_HIT_sum TCC_MISS_sum" "mfma:SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+  for pass in "fetch:FETCH_SIZE" "write:WRITE_SIZE" "l2:TCC_HIT_sum TCC_MISS_sum" "mfma:SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" "valu:SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE"; do
     pn=${pass%%:*}; ctr=${pass#*:}
     timeout -s KILL 120 rocprofv3 --pmc $ctr -d "$R/gpurun_out/pmc_${pn}_${name}" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 2 $args --no-cpu --no-batch1 --no-latency --no-capacity > "$R/gpurun_out/pmc_${pn}_${name}.log" 2>&1 || { echo "pmc $pn $name rc=$?"; exit 1; }
   done
