@@ -276,9 +276,10 @@ LPCNET_EXPORT int lpcnet_mi355x_pool_stats(const LPCNetState *st, long *launches
  * lpcnet_decoder_init take no device, lpcnet.c:184-219): each new handle
  * goes to the placement with the fewest live handles, over every visible
  * device by default or over `devices[0..n)` (env LPCNET_DEVICES="0,1,...";
- * a device may appear twice: two placements, two pools on one GPU).  Only
- * while no handle is live; n = 0 restores the default.  LPCNET_DEVICE=d pins
- * every new handle to device d instead.  0 / -1. */
+ * a device may appear twice: two placements, two pools on one GPU).  Live
+ * handles keep their device; handles initialised afterwards are placed over
+ * the new list; n = 0 restores the default.  LPCNET_DEVICE=d pins every new
+ * handle to device d instead.  0 / -1. */
 LPCNET_EXPORT int lpcnet_mi355x_set_placement(const int *devices, int n);
 /* The device and placement index (-1: pinned by LPCNET_DEVICE) of handle st. */
 LPCNET_EXPORT int lpcnet_mi355x_handle_placement(const LPCNetState *st, int *device, int *placement);

@@ -3234,7 +3234,8 @@ constexpr int MAX_FEATURE_BUFFER = 4; /* lpcnet_private.h:26 MAX_FEATURE_BUFFER_
 struct Handle {
   uint64_t token = 0;
   int device = 0;
-  int place = 0; /* placement index: auto placements 0.., LPCNET_DEVICE pins kPinned + device */
+  int place = 0;     /* placement index: auto placements 0.., LPCNET_DEVICE pins kPinned + device */
+  unsigned place_gen = 0; /* generation of the placement list it was counted in */
   StatePool *pool = nullptr; /* bound model (nullptr: none) */
   int slot = -1;
   /* run_frame_network_deferred's buffer (lpcnet_private.h:37-38, lpcnet.c:122-132) */
@@ -3300,7 +3301,8 @@ constexpr int kMaxPlace = 64;
 constexpr int kPinned = 1 << 20;
 static std::mutex g_place_mu;
 static std::vector<int> g_place_dev; /* placement -> device (empty: not set up yet) */
-static int g_place_load[kMaxPlace];  /* live handles per placement */
+static int g_place_load[kMaxPlace];  /* live handles per placement (of generation g_place_gen) */
+static unsigned g_place_gen = 1;     /* bumped by lpcnet_mi355x_set_placement */
 
 static bool parse_device_list(const char *v, std::vector<int> &out)
 {
@@ -3319,6 +3321,7 @@ static bool parse_device_list(const char *v, std::vector<int> &out)
 /* the placement of a new handle (g_place_mu held) */
 static void place_new_handle(Handle *h)
 {
+  h->place_gen = g_place_gen;
   if (const char *d = getenv("LPCNET_DEVICE")) {
     h->device = atoi(d);
     h->place = kPinned + h->device;
@@ -3342,7 +3345,8 @@ static void place_new_handle(Handle *h)
 static void unplace_handle(const Handle *h)
 {
   std::lock_guard<std::mutex> lk(g_place_mu);
-  if (h->place >= 0 && h->place < kMaxPlace && g_place_load[h->place] > 0) g_place_load[h->place]--;
+  if (h->place_gen == g_place_gen && h->place >= 0 && h->place < kMaxPlace && g_place_load[h->place] > 0)
+    g_place_load[h->place]--;
 }
 
 static void handle_free(Handle *h)
@@ -3361,12 +3365,11 @@ LPCNET_EXPORT int lpcnet_mi355x_set_placement(const int *devices, int n)
       set_err("lpcnet_mi355x_set_placement: device index outside the visible devices");
       return -1;
     }
+  /* live handles keep their device and pool; only handles initialised from
+   * now on are counted against (and placed over) the new list */
   std::lock_guard<std::mutex> lk(g_place_mu);
-  for (int k = 0; k < kMaxPlace; k++)
-    if (g_place_load[k] != 0) {
-      set_err("lpcnet_mi355x_set_placement: live handles still hold placements");
-      return -1;
-    }
+  for (int k = 0; k < kMaxPlace; k++) g_place_load[k] = 0;
+  g_place_gen++;
   g_place_dev.assign(devices, devices + n); /* n = 0: back to the default */
   return 0;
 }
@@ -3469,7 +3472,9 @@ LPCNET_EXPORT int lpcnet_load_model(LPCNetState *st, const unsigned char *data, 
 {
   Handle *h = live_handle(st);
   if (!h) { set_err("lpcnet_load_model: not an initialised LPCNetState"); return -1; }
-  StatePool *p = pool_acquire(data, len, h->device, h->place);
+  /* pools per (model, placement, device): a placement index of a later
+   * list may name another device */
+  StatePool *p = pool_acquire(data, len, h->device, h->place >= kPinned ? h->place : h->place * 1024 + h->device);
   if (!p) return -1;
   if (p == h->pool) {
     pool_release(p, -1); /* same model: keep the binding */

@@ -165,8 +165,10 @@ def test_handle_entry_points_fail_cleanly_without_model():
 
 def test_placement_policy_without_gpu():
     """Drop-in placement (no device touched before a model is bound): handles
-    go to the least-loaded placement of the list; the list cannot change
-    under live handles; LPCNET_DEVICE pins (placement -1)."""
+    go to the least-loaded placement of the list (counted from the last
+    lpcnet_mi355x_set_placement on; earlier handles keep theirs); a device
+    index outside the visible ones is refused; LPCNET_DEVICE pins
+    (placement -1)."""
     import gc
     import os
     gc.collect()
@@ -175,7 +177,7 @@ def test_placement_policy_without_gpu():
         nets = [L.LPCNet() for _ in range(7)]
         assert [n.placement() for n in nets] == [(0, k % 3) for k in range(7)]
         with pytest.raises(L.LPCNetError):
-            L.set_placement([0])
+            L.set_placement([-1])
         nets[1].close()
         nets[4].close()
         late = L.LPCNet()  # placement 1 had 2 live handles, now none
