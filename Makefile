@@ -15,7 +15,7 @@ CSRC := lpcnet_amd/csrc
 HDRS := include/lpcnet.h include/lpcnet_mi355x.h $(CSRC)/lpcnet_engine.h $(CSRC)/device_math.h $(CSRC)/sampler.h $(CSRC)/lds_flags.h $(CSRC)/mf_common.h $(CSRC)/l2_warm.h $(CSRC)/pow10_dd.h $(CSRC)/rcp_table_x86.inc
 EXTRA ?=
 COMMON := $(EXTRA) -O3 -fPIC -ffp-contract=off -fno-fast-math -std=c++17 -Iinclude -I$(CSRC) -fvisibility=hidden -Wall -Wno-unused-function
-OBJS := $(BUILD)/kernels.o $(BUILD)/mf_kernel.o $(BUILD)/mf2_kernel.o $(BUILD)/fp_kernel.o $(BUILD)/selftest.o $(BUILD)/frame_kernel.o $(BUILD)/engine.o $(BUILD)/lpc_kernel.o $(BUILD)/chunk_kernel.o $(BUILD)/model_gen.o $(BUILD)/host_rcpps.o $(BUILD)/decode_kernel.o
+OBJS := $(BUILD)/kernels.o $(BUILD)/mf_kernel.o $(BUILD)/mf2_kernel.o $(BUILD)/fp_kernel.o $(BUILD)/selftest.o $(BUILD)/frame_kernel.o $(BUILD)/engine.o $(BUILD)/lpc_kernel.o $(BUILD)/chunk_kernel.o $(BUILD)/model_gen.o $(BUILD)/host_rcpps.o $(BUILD)/decode_kernel.o $(BUILD)/mfw_kernel.o
 
 SYNTH := tools/lpcnet_synth
 DROPIN := tools/dropin_bench
@@ -51,6 +51,9 @@ $(BUILD)/mf_kernel.o: $(CSRC)/mf_kernel.hip $(HDRS) | $(BUILD)
 	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -fno-slp-vectorize -c $< -o $@
 
 $(BUILD)/mf2_kernel.o: $(CSRC)/mf2_kernel.hip $(HDRS) | $(BUILD)
+	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -fno-slp-vectorize -c $< -o $@
+
+$(BUILD)/mfw_kernel.o: $(CSRC)/mfw_kernel.hip $(HDRS) | $(BUILD)
 	$(HIPCC) -x hip --offload-arch=$(ARCH) $(COMMON) -fno-slp-vectorize -c $< -o $@
 
 # the fp32 chains schedule better under the max-ILP machine scheduler (batch-1 fp32 +0.6 %)

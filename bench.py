@@ -454,7 +454,8 @@ def side_line(L, blob, B, args, config, variant_name):
     return out
 
 
-def capacity(L, blob, args, ladder=(1024, 1025, 1536, 2048, 4096, 8192, 16384, 24576, 28672, 32768)):
+def capacity(L, blob, args, ladder=(1024, 1025, 1536, 2048, 4096, 8192, 16384, 24576, 28672, 32768, 36864, 40960,
+                                     49152, 57344)):
     """Measured real-time capacity of one GPU: the whole frame step (LPC,
     frame network, 160 samples of every stream; device-resident I/O) timed
     at each batch size of the ladder, including the non-multiples 1025 and
@@ -534,7 +535,7 @@ def live_line(L, blob, B, args, device_resident_value):
                     "(PCIe-inclusive; the headline `value` keeps the inputs resident in HBM)"}
 
 
-def capacity_live(L, blob, ladder=(1024, 2048, 4096, 8192, 16384, 24576, 28672, 32768)):
+def capacity_live(L, blob, ladder=(1024, 2048, 4096, 8192, 16384, 24576, 28672, 32768, 36864, 40960, 49152, 57344)):
     """capacity() for the live tick: the largest batch whose per-frame
     host-I/O step (lpcnet_batch_synthesize: features from host memory, PCM
     to host memory) stays within 10 ms, bracketed by bisection in steps of

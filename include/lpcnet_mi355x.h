@@ -40,7 +40,9 @@ typedef struct {
                                      LDS layout), 4 mf_kernel (matrix cores), 5 fp_kernel (fp32),
                                      6 mf2_kernel (matrix cores, two staggered 4-stream groups per
                                      workgroup; batches >= 2048; launches with preload or trace
-                                     take mf_kernel) */
+                                     take mf_kernel), 7 mfw_kernel (three 4-stream groups with dedicated
+                                     gather/elementwise, recurrent and sampler waves; batches >= 3072,
+                                     non-split models, default rcpps; the same launches as 6) */
   int lds_bytes;                  /* dynamic LDS of the sample kernel */
   double mfma_ops_per_group_sample; /* int8 matrix-core ops issued per workgroup per sample
                                        (mf_kernel; padding included), 0 otherwise */

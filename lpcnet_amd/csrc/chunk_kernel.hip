@@ -63,74 +63,110 @@ struct CkGeom {
   static constexpr int FLOATS = R0 + R1 + R2;
 };
 
-/* Row tile of a layer for the column tiles:
- *   acc[j][i] = bias[row] + sum_k W[k][row] * X(col, k),  row = 16 rt + 4 g + i,
- * col = 16 j + (lane & 15), the chain in k order.  X(col, k) =
- * xs[xb[j] + (k / SEG) * SST + k % SEG]: a column's inputs as segments of SEG
- * values SST apart (conv windows over padded frame rows).
- * Weights: the row tile's re-tiled copy (FrameArgs::ck_*, one float4 per
- * lane = 4 k steps) through a ring of CK_WPAD quads in registers that streams
- * the wave's whole sequence of row tiles -- conv1, conv2, dense1, dense2 and
- * its projection tiles -- so the next tile's quads (and bias) are in flight
- * while this tile's chain runs (each tile's first loads no longer wait a
- * full Infinity-Cache round trip: a one-frame launch spent ~40 of its ~50 us
- * there).  Every layer's quad count is a multiple of CK_WPAD, so the ring's
- * phase is 0 at every tile start. */
+/* T row tiles of a layer for the column tiles (T > 1: the projection's
+ * tiles of one wave side by side, independent chains that share every x
+ * read):
+ *   acc[t][j][i] = bias[row] + sum_k W[k][row] * X(col, k),  row = 16 rt_t + 4 g + i,
+ * col = 16 j + (lane & 15), each chain in k order (sgemv_accum16's
+ * sequential fmaf, bit for bit).  X(col, k) = xs[xb[j] + (k / SEG) * SST +
+ * k % SEG]: a column's inputs as segments of SEG values SST apart (conv
+ * windows over padded frame rows), read XL k steps ahead.
+ * Weights: each row tile's re-tiled copy (FrameArgs::ck_*, one float4 per
+ * lane = 4 k steps) through a ring of PQ quads in registers; for T = 1 the
+ * ring streams the wave's whole sequence of row tiles (conv1, conv2, dense1,
+ * dense2, its projection tiles), so the next tile's first quads and bias are
+ * in flight while this tile's chain runs.  Quad counts are multiples of PQ,
+ * so the ring's phase is 0 at every tile start.
+ * Stamped (CK_STAMPS, one-frame launch, 16 streams per workgroup): with one
+ * quad of x lookahead and one projection tile at a time the LDS reads and
+ * the dependent MFMA chains left ~300 cycles per k step. */
+template <int T, int PQ>
 struct CkRing {
-  float4 w[CK_WPAD];
-  float4 b; /* the current tile's bias quad (rows 16 rt + 4 g ..) */
+  float4 w[PQ][T];
+  float4 b[T]; /* the current tiles' bias quads (rows 16 rt + 4 g ..) */
 };
 
-__device__ __forceinline__ void ck_prime(CkRing &R, const float4 *tile, const float *bias)
+template <int T, int PQ>
+__device__ __forceinline__ void ck_prime(CkRing<T, PQ> &R, const float4 *const (&tile)[T], const float *const (&bias)[T])
 {
 #pragma unroll
-  for (int d = 0; d < CK_WPAD; d++) R.w[d] = tile[(size_t)d * 64];
-  R.b = *(const float4 *)bias;
+  for (int d = 0; d < PQ; d++)
+#pragma unroll
+    for (int t = 0; t < T; t++) R.w[d][t] = tile[t][(size_t)d * 64];
+#pragma unroll
+  for (int t = 0; t < T; t++) R.b[t] = *(const float4 *)bias[t];
 }
 
-template <int K, int SEG, int SST, int NCT>
-__device__ __forceinline__ void ck_tile(CkRing &R, const float4 *__restrict__ cur, const float4 *__restrict__ nxt,
-                                        const float *nbias, const float *xs, const int (&xb)[NCT], f32x4 (&acc)[NCT])
+template <int K, int SEG, int SST, int NCT, int T, int PQ, int XL>
+__device__ __forceinline__ void ck_tiles(CkRing<T, PQ> &R, const float4 *const (&cur)[T], const float4 *nxt,
+                                         const float *nbias, const float *xs, const int (&xb)[NCT],
+                                         f32x4 (&acc)[T][NCT])
 {
   static_assert(K % 4 == 0 && SEG % 4 == 0, "k quads stay inside a segment");
   constexpr int KS = K / 4;
   constexpr int NQ = (KS + 3) / 4;
-  constexpr int PQ = CK_WPAD;
   static_assert(NQ % PQ == 0, "ring phase 0 at every tile start");
+  static_assert(T == 1 || PQ <= NQ, "multi-tile: no streaming into a next tile");
   const int g = (threadIdx.x & 63) >> 4;
 #pragma unroll
-  for (int j = 0; j < NCT; j++) acc[j] = f32x4{R.b.x, R.b.y, R.b.z, R.b.w};
-  if (nbias) R.b = *(const float4 *)nbias; /* the next tile's bias, in flight beside this chain */
-  float xv[NCT], xn[NCT];
+  for (int t = 0; t < T; t++)
 #pragma unroll
-  for (int j = 0; j < NCT; j++) xv[j] = xs[xb[j] + g];
+    for (int j = 0; j < NCT; j++) acc[t][j] = f32x4{R.b[t].x, R.b[t].y, R.b[t].z, R.b[t].w};
+  if (T == 1 && nbias) R.b[0] = *(const float4 *)nbias; /* the next tile's bias, in flight beside this chain */
+  auto xoff = [](int kk) { return ((4 * kk) / SEG) * SST + (4 * kk) % SEG; };
+  float xv[XL][NCT];
+#pragma unroll
+  for (int d = 0; d < XL; d++)
+    if (d < KS)
+#pragma unroll
+      for (int j = 0; j < NCT; j++) xv[d][j] = xs[xb[j] + g + xoff(d)];
 #pragma unroll
   for (int kk = 0; kk < KS; kk++) {
-    if (kk + 1 < KS) {
-      const int o = ((4 * (kk + 1)) / SEG) * SST + (4 * (kk + 1)) % SEG;
-#pragma unroll
-      for (int j = 0; j < NCT; j++) xn[j] = xs[xb[j] + g + o];
-    }
     const int q = kk / 4;
-    const float4 &wq = R.w[q % PQ];
-    const float a = (kk & 3) == 0 ? wq.x : (kk & 3) == 1 ? wq.y : (kk & 3) == 2 ? wq.z : wq.w;
+    float a[T];
 #pragma unroll
-    for (int j = 0; j < NCT; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xv[j], acc[j], 0, 0, 0);
-    if ((kk & 3) == 3 || kk + 1 == KS) {
-      /* quad q consumed: its slot takes quad q + PQ of this tile, past the
-       * tile's end the next tile's first quads */
-      if (q + PQ < NQ)
-        R.w[q % PQ] = cur[(size_t)(q + PQ) * 64];
-      else if (nxt)
-        R.w[q % PQ] = nxt[(size_t)(q + PQ - NQ) * 64];
+    for (int t = 0; t < T; t++) {
+      const float4 &wq = R.w[q % PQ][t];
+      a[t] = (kk & 3) == 0 ? wq.x : (kk & 3) == 1 ? wq.y : (kk & 3) == 2 ? wq.z : wq.w;
     }
+    float xc[NCT];
 #pragma unroll
-    for (int j = 0; j < NCT; j++) xv[j] = xn[j];
+    for (int j = 0; j < NCT; j++) xc[j] = xv[kk % XL][j];
+    if (kk + XL < KS)
+#pragma unroll
+      for (int j = 0; j < NCT; j++) xv[kk % XL][j] = xs[xb[j] + g + xoff(kk + XL)];
+#pragma unroll
+    for (int t = 0; t < T; t++)
+#pragma unroll
+      for (int j = 0; j < NCT; j++) acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], xc[j], acc[t][j], 0, 0, 0);
+    if ((kk & 3) == 3 || kk + 1 == KS) {
+      /* quad q consumed: its slot takes quad q + PQ of the tile(s), past the
+       * tile's end (T = 1) the next tile's first quads */
+#pragma unroll
+      for (int t = 0; t < T; t++) {
+        if (q + PQ < NQ)
+          R.w[q % PQ][t] = cur[t][(size_t)(q + PQ) * 64];
+        else if (T == 1 && nxt)
+          R.w[q % PQ][t] = nxt[(size_t)(q + PQ - NQ) * 64];
+      }
+    }
+    /* k step boundary: without it the scheduler sinks every x read and ring
+     * refill to its use (ds_read; s_waitcnt lgkmcnt(0); mfma -- the ~235
+     * cycles per k step CK_STAMPS measured); not at 5-6 column tiles, whose
+     * lookahead is one step and whose registers are full */
+    if constexpr (NCT <= 4) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 /* quads per row tile of a re-tiled K-input matrix, padding included */
 constexpr int ck_tq(int K) { return (K / 4 + 3) / 4 + CK_WPAD; }
+
+/* per column-tile count: x lookahead, weight ring depth, projection tiles
+ * per pass (registers: 4 T NCT accumulators + 4 PQ T ring + XL NCT x) */
+constexpr int ck_xl(int nct) { return nct <= 2 ? 8 : (nct <= 4 ? 2 : 1); }
+constexpr int ck_pq(int nct) { return nct <= 4 ? 8 : 2; }
+constexpr int ck_tp(int nct) { return nct == 1 ? 10 : (nct == 2 ? 5 : (nct <= 4 ? 2 : 1)); }
+constexpr int ck_pqp(int tp, int nct) { return tp >= 5 ? 2 : (tp >= 2 ? 4 : ck_pq(nct)); }
 
 /* frame_count before frame f's update, given its value fc0 at the chunk start
  * (lpcnet.c:119: incremented while below 1000) */
@@ -169,35 +205,51 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   const float gamma = A.mc.lpc_gamma;
 
   /* inputs (lpcnet.c:91-99): frames -2, -1 from the conv1 memory, then
-   * features | pitch embedding of each frame of the chunk */
-  for (int e = tid; e < G::SC * G::INF * FIN; e += CK_THREADS) {
-    const int s = e / (G::INF * FIN), rem = e % (G::INF * FIN);
-    const int fr = rem / FIN - 2, j = rem % FIN, sid = s0 + s;
-    float v = 0.f;
-    if (sid < B) {
-      if (fr < 0) {
-        v = A.st[sid].conv1_mem[(fr + 2) * FIN + j];
-      } else if (fr < n) {
-        const float *ft = A.features + ((size_t)fr * B + sid) * NF;
-        if (j < NF) {
-          v = ft[j];
-        } else {
-          /* lpcnet.c:93-94: the 0.1 avoids rounding issues */
-          int pitch = (int)floor(.1 + (double)(50.f * ft[18]) + 100);
-          pitch = min(255, max(33, pitch));
-          v = A.embed_pitch[pitch * EP + (j - NF)];
-        }
-      }
+   * features | pitch embedding of each frame of the chunk.  The pitch rows
+   * first (one feature read per (stream, frame)), so the element loop below
+   * issues only independent loads (unrolled: one round trip instead of one
+   * per iteration -- stamped, the prologue of a one-frame launch was ~15 K
+   * cycles) */
+  __shared__ int pit[G::SC * NFR];
+  for (int e = tid; e < G::SC * NFR; e += CK_THREADS) {
+    const int s = e / NFR, fr = e % NFR, sid = s0 + s;
+    int pitch = 0;
+    if (sid < B && fr < n) {
+      /* lpcnet.c:93-94: the 0.1 avoids rounding issues */
+      pitch = (int)floor(.1 + (double)(50.f * A.features[((size_t)fr * B + sid) * NF + 18]) + 100);
+      pitch = min(255, max(33, pitch));
     }
-    inl[s * G::IN_SS + rem] = v;
+    pit[e] = pitch;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e0 = 0; e0 < G::SC * G::INF * FIN; e0 += CK_THREADS) {
+    const int e = e0 + tid;
+    if (e < G::SC * G::INF * FIN) {
+      const int s = e / (G::INF * FIN), rem = e % (G::INF * FIN);
+      const int fr = rem / FIN - 2, j = rem % FIN, sid = s0 + s;
+      float v = 0.f;
+      if (sid < B) {
+        if (fr < 0)
+          v = A.st[sid].conv1_mem[(fr + 2) * FIN + j];
+        else if (fr < n)
+          v = j < NF ? A.features[((size_t)fr * B + sid) * NF + j] : A.embed_pitch[pit[s * NFR + fr] * EP + (j - NF)];
+      }
+      inl[s * G::IN_SS + rem] = v;
+    }
   }
   /* conv1 outputs of frames -2, -1: the conv2 memory */
-  for (int e = tid; e < G::SC * 2 * COND; e += CK_THREADS) {
-    const int s = e / (2 * COND), j = e % (2 * COND), sid = s0 + s;
-    c1[s * G::C1_SS + (j / COND) * CK_RS + j % COND] = sid < B ? A.st[sid].conv2_mem[j] : 0.f;
+#pragma unroll
+  for (int e0 = 0; e0 < G::SC * 2 * COND; e0 += CK_THREADS) {
+    const int e = e0 + tid;
+    if (e < G::SC * 2 * COND) {
+      const int s = e / (2 * COND), j = e % (2 * COND), sid = s0 + s;
+      c1[s * G::C1_SS + (j / COND) * CK_RS + j % COND] = sid < B ? A.st[sid].conv2_mem[j] : 0.f;
+    }
   }
-  if (tid < G::SC * D * NLPC) {
-    const int s = tid / (D * NLPC), q = tid % (D * NLPC), sid = s0 + s;
+  /* (a loop: 16-32 streams x FEATURES_DELAY 4 x 16 exceed the 512 threads) */
+  for (int e = tid; e < G::SC * D * NLPC; e += CK_THREADS) {
+    const int s = e / (D * NLPC), q = e % (D * NLPC), sid = s0 + s;
     olpc[s][q / NLPC][q % NLPC] = sid < B ? A.st[sid].old_lpc[q / NLPC][q % NLPC] : 0.f;
   }
   if (tid < G::SC) fcs[tid] = s0 + tid < B ? A.st[s0 + tid].frame_count : 1000;
@@ -212,23 +264,32 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
     cf[j] = (16 * j + r) % NFR;
   }
   int xb[NCT];
-  f32x4 acc[NCT];
-  /* this wave's weight stream: conv1, conv2, dense1, dense2 row tile `wave`,
-   * then projection tiles wave, wave + 8, ... (ck_tile) */
+  /* this wave's weight stream: conv1, conv2, dense1, dense2 row tile `wave`
+   * (one ring), then its projection tiles wave, wave + 8, ... TP at a time */
   const int l64 = tid & 63;
+  constexpr int XL = ck_xl(NCT), PQ = ck_pq(NCT), TP = ck_tp(NCT), PQP = ck_pqp(TP, NCT);
   const float4 *t_c1 = A.ck_conv1 + (size_t)wave * ck_tq(3 * FIN) * 64 + l64;
   const float4 *t_c2 = A.ck_conv2 + (size_t)wave * ck_tq(3 * COND) * 64 + l64;
   const float4 *t_d1 = A.ck_dense1 + (size_t)wave * ck_tq(COND) * 64 + l64;
   const float4 *t_d2 = A.ck_dense2 + (size_t)wave * ck_tq(COND) * 64 + l64;
   auto t_pj = [&](int rt) { return A.ck_proj + (size_t)rt * ck_tq(COND) * 64 + l64; };
   const int bo = 16 * wave + 4 * g; /* this lane's bias quad in a 128-row layer */
-  CkRing R;
-  ck_prime(R, t_c1, A.conv1_b + bo);
+  CkRing<1, PQ> R;
+  {
+    const float4 *const t0[1] = {t_c1};
+    const float *const b0[1] = {A.conv1_b + bo};
+    ck_prime(R, t0, b0);
+  }
+  f32x4 acc1[1][NCT];
+  f32x4 (&acc)[NCT] = acc1[0];
 
   /* conv1 (nnet.c:452-470): 252 inputs -> 128, tanh; cleared while frame_count < 1 (lpcnet.c:99) */
 #pragma unroll
   for (int j = 0; j < NCT; j++) xb[j] = cs[j] * G::IN_SS + cf[j] * FIN; /* window = frames f-2..f */
-  ck_tile<3 * FIN, 3 * FIN, 3 * FIN>(R, t_c1, t_c2, A.conv2_b + bo, inl, xb, acc);
+  {
+    const float4 *const c[1] = {t_c1};
+    ck_tiles<3 * FIN, 3 * FIN, 3 * FIN, NCT, 1, PQ, XL>(R, c, t_c2, A.conv2_b + bo, inl, xb, acc1);
+  }
 #pragma unroll
   for (int j = 0; j < NCT; j++) {
     const bool clr = ck_fc(fcs[cs[j]], cf[j]) < 1;
@@ -250,7 +311,10 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   /* conv2: 384 inputs -> 128, tanh; cleared while frame_count < FEATURES_DELAY (lpcnet.c:101) */
 #pragma unroll
   for (int j = 0; j < NCT; j++) xb[j] = cs[j] * G::C1_SS + cf[j] * CK_RS;
-  ck_tile<3 * COND, COND, CK_RS>(R, t_c2, t_d1, A.dense1_b + bo, c1, xb, acc);
+  {
+    const float4 *const c[1] = {t_c2};
+    ck_tiles<3 * COND, COND, CK_RS, NCT, 1, PQ, XL>(R, c, t_d1, A.dense1_b + bo, c1, xb, acc1);
+  }
 #pragma unroll
   for (int j = 0; j < NCT; j++) {
     const bool clr = ck_fc(fcs[cs[j]], cf[j]) < D;
@@ -267,14 +331,20 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   /* dense1, dense2 (lpcnet.c:104-105) */
 #pragma unroll
   for (int j = 0; j < NCT; j++) xb[j] = (16 * j + r) * CK_RS;
-  ck_tile<COND, COND, CK_RS>(R, t_d1, t_d2, A.dense2_b + bo, ya, xb, acc);
+  {
+    const float4 *const c[1] = {t_d1};
+    ck_tiles<COND, COND, CK_RS, NCT, 1, PQ, XL>(R, c, t_d2, A.dense2_b + bo, ya, xb, acc1);
+  }
 #pragma unroll
   for (int j = 0; j < NCT; j++)
     *(float4 *)&yb[(16 * j + r) * CK_RS + 16 * wave + 4 * g] =
         make_float4(tanh_x86<HWR>(acc[j][0], rcp), tanh_x86<HWR>(acc[j][1], rcp), tanh_x86<HWR>(acc[j][2], rcp),
                     tanh_x86<HWR>(acc[j][3], rcp));
   __syncthreads();
-  ck_tile<COND, COND, CK_RS>(R, t_d2, t_pj(wave), A.proj_b + bo, yb, xb, acc);
+  {
+    const float4 *const c[1] = {t_d2};
+    ck_tiles<COND, COND, CK_RS, NCT, 1, PQ, XL>(R, c, nullptr, nullptr, yb, xb, acc1);
+  }
 #pragma unroll
   for (int j = 0; j < NCT; j++)
     *(float4 *)&ya[(16 * j + r) * CK_RS + 16 * wave + 4 * g] =
@@ -311,25 +381,45 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   /* conditioning projections (lpcnet.c:106-107), linear: gadf | gbdf as one
    * [128][1200] matrix, 75 row tiles over the 8 waves; frame f's outputs go
    * to cond[f], the last frame's also to the stream state */
+  /* TP of this wave's tiles per pass (wave + 8 t, t < 10: the last pass of
+   * waves 3..7 carries one tile past the 75th, computed on a clamped copy
+   * and not stored) */
+  constexpr int WV = CK_THREADS / 64, NT = (CK_PROJ_TILES + WV - 1) / WV; /* 10 tiles at most per wave */
 #pragma unroll 1
-  for (int rt = wave; rt < CK_PROJ_TILES; rt += CK_THREADS / 64) {
-    const int rn = rt + CK_THREADS / 64;
-    ck_tile<COND, COND, CK_RS>(R, t_pj(rt), rn < CK_PROJ_TILES ? t_pj(rn) : nullptr,
-                               rn < CK_PROJ_TILES ? A.proj_b + 16 * rn + 4 * g : nullptr, ya, xb, acc);
+  for (int t0 = 0; t0 < NT; t0 += TP) {
+    const float4 *cur[TP];
+    const float *bia[TP];
+    int rts[TP];
 #pragma unroll
-    for (int j = 0; j < NCT; j++) {
-      const int sid = s0 + cs[j], f = cf[j];
-      if (sid >= B || f >= n) continue;
-      FrameCond *q = &A.cond[(size_t)f * B + sid];
-      StreamState *p = &A.st[sid];
-      /* this lane's 4 consecutive rows as one 16-byte store: the 4 lanes of
-       * a column write its 16 rows as one 64-byte run (GA_ROWS is a multiple
-       * of 16, so a row quad never straddles the two arrays) */
-      const int row = 16 * rt + 4 * g;
-      const float4 v = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
-      float *qd = row < GA_ROWS ? q->gru_a_cond + row : q->gru_b_cond + (row - GA_ROWS);
-      *(float4 *)qd = v;
-      if (f == n - 1) *(float4 *)(row < GA_ROWS ? p->gru_a_cond + row : p->gru_b_cond + (row - GA_ROWS)) = v;
+    for (int t = 0; t < TP; t++) {
+      const int rt = wave + WV * (t0 + t);
+      rts[t] = rt;
+      const int rc = rt < CK_PROJ_TILES ? rt : wave; /* clamped: in bounds, result dropped */
+      cur[t] = t_pj(rc);
+      bia[t] = A.proj_b + 16 * rc + 4 * g;
+    }
+    CkRing<TP, PQP> RP;
+    ck_prime(RP, cur, bia);
+    f32x4 pacc[TP][NCT];
+    ck_tiles<COND, COND, CK_RS, NCT, TP, PQP, XL>(RP, cur, nullptr, nullptr, ya, xb, pacc);
+#pragma unroll
+    for (int t = 0; t < TP; t++) {
+      if (rts[t] >= CK_PROJ_TILES) continue;
+#pragma unroll
+      for (int j = 0; j < NCT; j++) {
+        const int sid = s0 + cs[j], f = cf[j];
+        if (sid >= B || f >= n) continue;
+        FrameCond *q = &A.cond[(size_t)f * B + sid];
+        StreamState *p = &A.st[sid];
+        /* this lane's 4 consecutive rows as one 16-byte store: the 4 lanes of
+         * a column write its 16 rows as one 64-byte run (GA_ROWS is a multiple
+         * of 16, so a row quad never straddles the two arrays) */
+        const int row = 16 * rts[t] + 4 * g;
+        const float4 v = make_float4(pacc[t][j][0], pacc[t][j][1], pacc[t][j][2], pacc[t][j][3]);
+        float *qd = row < GA_ROWS ? q->gru_a_cond + row : q->gru_b_cond + (row - GA_ROWS);
+        *(float4 *)qd = v;
+        if (f == n - 1) *(float4 *)(row < GA_ROWS ? p->gru_a_cond + row : p->gru_b_cond + (row - GA_ROWS)) = v;
+      }
     }
   }
 

@@ -323,6 +323,9 @@ struct LPCNetBatch {
   bool mf = false;       /* mf_kernel (mode 4) */
   bool mf2 = false;      /* large batches: mf2_kernel (two staggered 4-stream groups per workgroup) for
                             launches without preload / trace / stamps */
+  bool mfw = false;      /* wider batches: mfw_kernel (three 4-stream groups, dedicated gather /
+                            recurrent / sampler waves) for the same launches, non-split models with the
+                            default rcpps */
   double mf_ga_ops = 0;  /* int8 matrix-core ops per workgroup per sample: the GRU_A recurrent pass */
   double mf_gb_ops = 0;  /* the GRU_B tiles of both sampler waves */
   bool fp_ok = false;    /* fp32 model fits the fp_kernel tables */
@@ -438,6 +441,14 @@ bool block_may_saturate(const int8_t *w)
   return false;
 }
 
+bool mfw_pays(int B, int cus)
+{
+  if (B < MFW_MIN_STREAMS || cus < 1) return false;
+  const long per_round = (long)MFW_STREAMS_PER_WG * cus;
+  const long padded = (B + per_round - 1) / per_round * per_round;
+  return (double)padded <= MFW_GAIN * B;
+}
+
 /* Sample-kernel choice (mode 0 = automatic):
  *   5  fp_kernel  -- fp32 models with a dense GRU_B within the FP_* limits
  *   4  mf_kernel  -- non-saturating int8 models within the MF_* limits
@@ -448,6 +459,7 @@ void choose_kernel(LPCNetBatch *b)
 {
   b->mf = false;
   b->mf2 = false;
+  b->mfw = false;
   b->fp = false;
   b->info.mfma_ops_per_group_sample = 0;
   int mode = b->kernel_mode;
@@ -480,6 +492,17 @@ void choose_kernel(LPCNetBatch *b)
       b->info.streams_per_workgroup = 8;
       b->info.lds_bytes = mf2_lds_bytes(4, b->sa.mf_split);
       b->info.quad_path = 6;
+      /* three groups with dedicated roles from MFW_MIN_STREAMS on
+       * (LPCNET_MFW=0 off, =1 at any batch size that takes mf2) */
+      const char *ew = getenv("LPCNET_MFW");
+      const bool wantw = ew ? atoi(ew) != 0 : mfw_pays(b->B, current_device_cus());
+      if (wantw && !b->sa.mf_split && b->sa.rcp_hw && mfw_lds_bytes() <= 160 * 1024) {
+        b->mfw = true;
+        b->info.mfma_ops_per_group_sample = 3 * (b->mf_ga_ops + b->mf_gb_ops);
+        b->info.streams_per_workgroup = MFW_STREAMS_PER_WG;
+        b->info.lds_bytes = mfw_lds_bytes();
+        b->info.quad_path = 7;
+      }
     }
     return;
   }
@@ -1776,6 +1799,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   const int lrc = N <= 0 ? 0
                 : b->fp    ? launch_fp(sa, b->stream)
+                : b->mfw && !sa.preload && !sa.trace_logits && !sa.stamps ? launch_mfw(sa, b->stream)
                 : b->mf2 && !sa.preload && !sa.trace_logits && !sa.stamps ? launch_mf2(sa, 4, b->stream)
                 : b->mf    ? launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream)
                              : launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream);
@@ -1839,6 +1863,7 @@ int launch_chunk_samples(LPCNetBatch *b, int f, short *d_pcm, int N, int nfr = 1
   }
   const int lrc = N <= 0                                  ? 0
                   : b->fp                                 ? launch_fp(sa, b->stream)
+                  : b->mfw && !sa.trace_logits && !sa.stamps ? launch_mfw(sa, b->stream)
                   : b->mf2 && !sa.trace_logits && !sa.stamps ? launch_mf2(sa, 4, b->stream)
                                                           : launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream);
   if (lrc) {
@@ -2174,6 +2199,7 @@ static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_fe
   sa.spin_limit = b->spin_limit;
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   const int lrc = b->fp ? launch_fp(sa, b->stream)
+                  : b->mfw ? launch_mfw(sa, b->stream)
                   : b->mf2 ? launch_mf2(sa, 4, b->stream)
                            : launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream);
   if (lrc) {

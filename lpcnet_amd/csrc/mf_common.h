@@ -42,6 +42,17 @@ __device__ __forceinline__ v4i mfma4(uint32_t x, uint32_t w, v4i acc)
   return __builtin_amdgcn_mfma_i32_4x4x4i8((int)x, (int)w, acc, 0, 0, 0);
 }
 
+/* an optional scheduling fence between a group's next-x reads and its
+ * MFMAs (-DMF_SCHED): without it the scheduler may sink the reads below the
+ * products.  Measured (same box, alternating): mf_kernel<4> at 1024 streams
+ * 3 % slower fenced, mf2_kernel unchanged, so it is off here; mfw_kernel
+ * fences its own loops (MFW_FENCE, 1.5-1.7 % faster). */
+#ifdef MF_SCHED
+#define MF_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define MF_FENCE() do { } while (0)
+#endif
+
 /* GRU_A z and r products over ng 4-slot groups (wave-uniform ng): the two
  * gates interleave, each over NC independent accumulators (slot k -> chain
  * k % NC; int32 sums, so any split is the same exact result), x words of
@@ -68,11 +79,13 @@ __device__ __forceinline__ void mf_zr(const unsigned char *lds, const uint32_t (
           nr[k] = mf_x(lds, orr, 4 * (g + 1) + k);
         }
       }
+      MF_FENCE();
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         az[k % NC] = mfma4(xz[k], wz[4 * g + k], az[k % NC]);
         ar[k % NC] = mfma4(xr[k], wr[4 * g + k], ar[k % NC]);
       }
+      MF_FENCE();
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         xz[k] = nz[k];
@@ -99,8 +112,10 @@ __device__ __forceinline__ void mf_run(const unsigned char *lds, const uint32_t 
 #pragma unroll
         for (int k = 0; k < 4; k++) n[k] = mf_x(lds, o, 4 * (g + 1) + k);
       }
+      MF_FENCE();
 #pragma unroll
       for (int k = 0; k < 4; k++) a[k % NC] = mfma4(x[k], w[4 * g + k], a[k % NC]);
+      MF_FENCE();
 #pragma unroll
       for (int k = 0; k < 4; k++) x[k] = n[k];
     }
@@ -131,6 +146,7 @@ __device__ __forceinline__ void mf_zr_ct(const unsigned char *lds, const uint32_
         nr[k] = mf_x(lds, orr, 4 * (g + 1) + k);
       }
     }
+    MF_FENCE();
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       if (g < NO) {
@@ -141,6 +157,7 @@ __device__ __forceinline__ void mf_zr_ct(const unsigned char *lds, const uint32_
         fr = mfma4(xr[k], wr[4 * g + k], fr);
       }
     }
+    MF_FENCE();
     if (g + 1 < NO + NF) {
 #pragma unroll
       for (int k = 0; k < 4; k++) {
@@ -165,6 +182,7 @@ __device__ __forceinline__ void mf_h_ct(const unsigned char *lds, const uint32_t
 #pragma unroll
       for (int k = 0; k < 4; k++) n[k] = mf_x(lds, o, 4 * (g + 1) + k);
     }
+    MF_FENCE();
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       if (g < NO)
@@ -172,6 +190,7 @@ __device__ __forceinline__ void mf_h_ct(const unsigned char *lds, const uint32_t
       else
         f[k & 1] = mfma4(x[k], w[4 * g + k], f[k & 1]);
     }
+    MF_FENCE();
     if (g + 1 < NO + NF) {
 #pragma unroll
       for (int k = 0; k < 4; k++) x[k] = n[k];

@@ -26,11 +26,20 @@ struct FcLane {
 
   __device__ __forceinline__ void init(const unsigned char *img, int lane)
   {
-    rcp = (const uint32_t *)(img + IMG_RCP);
-    ulaw = (const float *)(img + IMG_ULAW);
-    fcw = (const float *)(img + IMG_FCW);
-    fcb = (const float *)(img + IMG_FCB);
-    fcf = (const float *)(img + IMG_FCF);
+    init_sections((const uint32_t *)(img + IMG_RCP), (const float *)(img + IMG_ULAW), (const float *)(img + IMG_FCW),
+                  (const float *)(img + IMG_FCB), (const float *)(img + IMG_FCF), lane);
+  }
+
+  /* the same from the image's sections placed anywhere in LDS (mfw_kernel
+   * keeps no rcpps table: hardware reciprocal only, rcp_ = nullptr) */
+  __device__ __forceinline__ void init_sections(const uint32_t *rcp_, const float *ulaw_, const float *fcw_,
+                                                const float *fcb_, const float *fcf_, int lane)
+  {
+    rcp = rcp_;
+    ulaw = ulaw_;
+    fcw = fcw_;
+    fcb = fcb_;
+    fcf = fcf_;
     half = lane >> 5;
     hl = lane & 31;
     hb = 32 * half;

@@ -766,3 +766,40 @@ def test_live_single_frame_chunked_matches_oracle(require_gpu, monkeypatch, vari
     for s in sorted({0, 1, B // 2, B - 1}):
         o = O.Oracle(blob, variant)
         assert np.array_equal(got[s], np.stack([o.synthesize(allf[f, s]) for f in range(F)])), s
+
+
+@pytest.mark.parametrize("B,F", [(12, 5), (3073, 4), (4096, 6)])
+def test_wide_kernel_matches_oracle(require_gpu, monkeypatch, B, F):
+    """mfw_kernel (three 4-stream groups per workgroup, dedicated gather /
+    recurrent / sampler waves): every stream equals mf2_kernel's (LPCNET_MFW=0)
+    and sampled streams equal the oracle -- one workgroup (12 streams, forced
+    with LPCNET_MFW=1), a ragged last workgroup (3073), multi-frame launches
+    through the device-resident path (4096) and the host-I/O path (both)."""
+    blob = L.synthetic_model(1, 0)
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    monkeypatch.setenv("LPCNET_MF2", "1")
+    monkeypatch.setenv("LPCNET_MFW", "1")
+    b = L.LPCNetBatch(B, 0, blob)
+    assert b.info().quad_path == 7 and b.info().kernel_name == "mfw_kernel<true>"
+    got = np.stack([b.synthesize(allf[f]) for f in range(F)], 1)
+    b.reset()
+    d_f = b.device_alloc(allf.nbytes)
+    d_p = b.device_alloc(F * B * 160 * 2)
+    b.h2d(d_f, np.ascontiguousarray(allf))
+    b.synthesize_frames(None, d_f, d_p, F)
+    b.sync()
+    dev = np.zeros((F, B, 160), np.int16)
+    b.d2h(dev, d_p)
+    b.device_free(d_f)
+    b.device_free(d_p)
+    b.close()
+    assert np.array_equal(dev.transpose(1, 0, 2), got)
+    monkeypatch.setenv("LPCNET_MFW", "0")
+    b2 = L.LPCNetBatch(B, 0, blob)
+    assert b2.info().quad_path in (4, 6)
+    ref = np.stack([b2.synthesize(allf[f]) for f in range(F)], 1)
+    b2.close()
+    assert np.array_equal(got, ref)
+    for s in sorted({0, 5, 11, B // 2, B - 1}):
+        o = O.Oracle(blob, 0)
+        assert np.array_equal(got[s], np.stack([o.synthesize(allf[f, s]) for f in range(F)])), s
