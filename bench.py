@@ -524,11 +524,18 @@ def run_live(L, blob, B, warmup, steps, preheat_ms=0.0):
     return np.array(per), pcm
 
 
+def _json_scalar(o):
+    """numpy scalars (np.bool_, np.float64 ...) in the line as their Python values"""
+    if isinstance(o, np.generic):
+        return o.item()
+    raise TypeError(f"bench line: {type(o).__name__} is not JSON serialisable")
+
+
 def live_line(L, blob, B, args, device_resident_value):
     nf = max(args.steps, 20)
     per, _ = run_live(L, blob, B, args.warmup, nf, args.preheat_ms)
-    v = B * 160 * len(per) / per.sum()
-    return {"samples_per_s": v, "ms_per_frame": per.mean() * 1e3, "ms_per_frame_p50": float(np.median(per)) * 1e3,
+    v = float(B * 160 * len(per) / per.sum())
+    return {"samples_per_s": v, "ms_per_frame": float(per.mean()) * 1e3, "ms_per_frame_p50": float(np.median(per)) * 1e3,
             "ms_per_frame_max": float(per.max()) * 1e3, "frames": len(per),
             "vs_device_resident": v / device_resident_value if device_resident_value else None,
             "what": "host features in, host PCM out, one lpcnet_batch_synthesize per 10 ms frame "
@@ -546,8 +553,9 @@ def capacity_live(L, blob, ladder=(1024, 2048, 4096, 8192, 16384, 24576, 28672, 
     def run(B):
         per, _ = run_live(L, blob, B, 2, steps)
         ms = per.mean() * 1e3
+        ms = float(ms)
         rows[B] = {"frame_step_ms": ms, "frame_step_ms_max": float(per.max()) * 1e3,
-                   "samples_per_s": B * 160 / per.mean(), "realtime": ms <= 10.0}
+                   "samples_per_s": float(B * 160 / per.mean()), "realtime": bool(ms <= 10.0)}
         return ms
 
     ok, bad = 0, None
@@ -698,7 +706,7 @@ def main():
         # beside batch1_fp32 (configs[1]): the reference's fp32 build on the same cores
         out["cpu_baseline_fp32"] = cpu_baseline(args.cpu_seconds, 1)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out, default=_json_scalar), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -193,3 +193,16 @@ def test_placement_policy_without_gpu():
     finally:
         gc.collect()
         L.set_placement([])
+
+
+def test_bench_line_serialises_numpy_scalars():
+    """the bench line's ladders hold numpy-derived values (np.bool_ realtime
+    flags, np.float64 means): the line must still print as JSON"""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    row = {"realtime": np.float64(3.0) <= 10.0, "ms": np.float64(3.0), "n": np.int64(4)}
+    assert json.loads(json.dumps(row, default=bench._json_scalar)) == {"realtime": True, "ms": 3.0, "n": 4}
+    with pytest.raises(TypeError):
+        json.dumps({"x": object()}, default=bench._json_scalar)
