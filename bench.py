@@ -88,6 +88,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-latency", action="store_true", help="skip the stamped latency run")
     p.add_argument("--no-capacity", action="store_true", help="skip the measured real-time capacity ladder")
+    p.add_argument("--live-only", action="store_true",
+                   help="headline, then only the live (per-frame host I/O) line and its capacity ladder")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--preheat-ms", type=float, default=100.0,
                    help="untimed load before the warmup (DPM clock ramp), then every stream is reset")
@@ -494,32 +496,46 @@ def capacity(L, blob, args, ladder=(1024, 1025, 1536, 2048, 4096, 8192, 16384, 2
             "steps_per_point": steps, "ladder": {str(k): v for k, v in sorted(rows.items())}}
 
 
-def run_live(L, blob, B, warmup, steps, preheat_ms=0.0):
+def run_live(L, blob, B, warmup, steps, preheat_ms=0.0, engine_buffers=True):
     """A live server's tick, frame by frame: every 10 ms of audio the host
     hands over B feature frames (host memory) and takes back B x 160 PCM
     samples (host memory) -- lpcnet_batch_synthesize once per frame
     (lpcnet_demo.c:208-219's loop for B streams at once; PCIe copies, the
     LPC, frame and sample kernels and the synchronisation all inside the
-    timed region).  Returns (seconds per frame for each timed frame, pcm of
-    the last frame)."""
+    timed region).  engine_buffers: the features are written into the
+    batch's pinned feature buffer and the PCM is read from its pinned PCM
+    buffer (lpcnet_batch_host_features / _pcm: no staging copies, the
+    sample kernel stores the PCM over PCIe itself); otherwise the caller's
+    own numpy arrays in and out.  Returns (seconds per frame for each timed
+    frame, pcm of the last frame)."""
     F = warmup + steps
     feats = np.ascontiguousarray(np.stack([L.synthetic_features(s, F)[:, :20] for s in range(B)], 1), np.float32)
     b = L.LPCNetBatch(B, int(os.environ.get("LOCAL_RANK", "0")) % max(1, L.device_count()), blob)
+    if engine_buffers:
+        hf = b.host_features()
+
+        def tick(f):
+            np.copyto(hf, feats[f])
+            return b.synthesize_host()
+    else:
+        def tick(f):
+            return b.synthesize(feats[f])
     if preheat_ms > 0:
         t_end = time.perf_counter() + preheat_ms * 1e-3
         k = 0
         while time.perf_counter() < t_end:
-            b.synthesize(feats[k % F])
+            tick(k % F)
             k += 1
         b.reset()
     for f in range(warmup):
-        b.synthesize(feats[f])
+        tick(f)
     per = []
     pcm = None
     for f in range(warmup, F):
         t0 = time.perf_counter()
-        pcm = b.synthesize(feats[f])
+        pcm = tick(f)
         per.append(time.perf_counter() - t0)
+    pcm = np.array(pcm)
     b.close()
     return np.array(per), pcm
 
@@ -533,13 +549,21 @@ def _json_scalar(o):
 
 def live_line(L, blob, B, args, device_resident_value):
     nf = max(args.steps, 20)
-    per, _ = run_live(L, blob, B, args.warmup, nf, args.preheat_ms)
-    v = float(B * 160 * len(per) / per.sum())
-    return {"samples_per_s": v, "ms_per_frame": float(per.mean()) * 1e3, "ms_per_frame_p50": float(np.median(per)) * 1e3,
-            "ms_per_frame_max": float(per.max()) * 1e3, "frames": len(per),
-            "vs_device_resident": v / device_resident_value if device_resident_value else None,
-            "what": "host features in, host PCM out, one lpcnet_batch_synthesize per 10 ms frame "
-                    "(PCIe-inclusive; the headline `value` keeps the inputs resident in HBM)"}
+    out = {}
+    for key, eb in (("engine_buffers", True), ("caller_buffers", False)):
+        per, _ = run_live(L, blob, B, args.warmup, nf, args.preheat_ms, engine_buffers=eb)
+        v = float(B * 160 * len(per) / per.sum())
+        out[key] = {"samples_per_s": v, "ms_per_frame": float(per.mean()) * 1e3,
+                    "ms_per_frame_p50": float(np.median(per)) * 1e3, "ms_per_frame_max": float(per.max()) * 1e3,
+                    "frames": len(per),
+                    "vs_device_resident": v / device_resident_value if device_resident_value else None}
+    res = dict(out["engine_buffers"])
+    res["caller_buffers"] = out["caller_buffers"]
+    res["what"] = ("host features in, host PCM out, one lpcnet_batch_synthesize per 10 ms frame (PCIe-inclusive; "
+                   "the headline `value` keeps the inputs resident in HBM); top level: features written into and "
+                   "PCM read from the batch's pinned buffers (lpcnet_batch_host_features / _pcm); caller_buffers: "
+                   "the caller's own arrays, staged through pinned memory by the engine")
+    return res
 
 
 def capacity_live(L, blob, ladder=(1024, 2048, 4096, 8192, 16384, 24576, 28672, 32768, 36864, 40960, 49152, 57344)):
@@ -693,10 +717,12 @@ def main():
         out["skewed_int8"] = skewed_lines(L, args)
         out["lockstep"] = lockstep_lines(L, args)
         out["host_rcpps"] = host_rcpps_lines(L, args)
-    if rank == 0 and world == 1 and not args.no_batch1:
+    if rank == 0 and world == 1 and (not args.no_batch1 or args.live_only):
         # the same workload as a live server runs it: host I/O every frame
         out["live"] = live_line(L, blob, B, args, value)
-    if rank == 0 and world == 1 and not args.no_capacity:
+    if rank == 0 and world == 1 and args.live_only:
+        out["capacity_live"] = capacity_live(L, blob)
+    if rank == 0 and world == 1 and not args.no_capacity and not args.live_only:
         out["capacity"] = capacity(L, blob, args)
         out["capacity_live"] = capacity_live(L, blob)
         # the same ladder on the trained-like (Sparsify) sparsity pattern

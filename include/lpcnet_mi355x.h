@@ -103,6 +103,16 @@ LPCNET_EXPORT int lpcnet_batch_nb_streams(const LPCNetBatch *b);
  * Returns 0, or -1 on error (no model, bad N). */
 LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features, short *pcm, int N);
 
+/* The batch's own pinned host buffers for a live server's tick (features
+ * [B][NB_FEATURES], PCM [B][160]; allocated on first use, freed with the
+ * batch, NULL on error).  lpcnet_batch_synthesize with these pointers skips
+ * its host staging copies: the features go to the device in one DMA copy,
+ * and the sample kernel stores the PCM into the (mapped) PCM buffer itself
+ * where its write-out is coalesced -- no device-to-host copy.  The PCM
+ * buffer holds a frame's output until the next synthesis call. */
+LPCNET_EXPORT float *lpcnet_batch_host_features(LPCNetBatch *b);
+LPCNET_EXPORT short *lpcnet_batch_host_pcm(LPCNetBatch *b);
+
 /* lpcnet_synthesize_impl (src/lpcnet.c:273-277, the PLC entry point): as
  * above, but the first `preload` samples of every stream are teacher-forced
  * from pcm (input), exactly as lpcnet.c:256-259; pcm[s][preload..N) is output.

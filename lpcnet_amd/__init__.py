@@ -67,6 +67,8 @@ def _load():
         "lpcnet_batch_reset_stream": (i, [vp, i]),
         "lpcnet_batch_nb_streams": (i, [vp]),
         "lpcnet_batch_synthesize": (i, [vp, vp, vp, i]),
+        "lpcnet_batch_host_features": (C.POINTER(C.c_float), [vp]),
+        "lpcnet_batch_host_pcm": (C.POINTER(C.c_short), [vp]),
         "lpcnet_batch_synthesize_impl": (i, [vp, vp, vp, i, i]),
         "lpcnet_batch_state_size": (i, []),
         "lpcnet_batch_save_state": (i, [vp, i, vp]),
@@ -436,6 +438,31 @@ class LPCNetBatch:
             raise LPCNetError(last_error())
         return out
 
+    def host_features(self) -> np.ndarray:
+        """The batch's pinned feature buffer [B, 20] (lpcnet_batch_host_features):
+        fill it in place, then synthesize_host()."""
+        if getattr(self, "_hf", None) is None:
+            p = lib.lpcnet_batch_host_features(self._b)
+            if not p:
+                raise LPCNetError(last_error())
+            self._hf = np.ctypeslib.as_array(p, shape=(self.B, NB_FEATURES))
+            q = lib.lpcnet_batch_host_pcm(self._b)
+            if not q:
+                raise LPCNetError(last_error())
+            self._hp = np.ctypeslib.as_array(q, shape=(self.B * FRAME_SIZE,))
+        return self._hf
+
+    def synthesize_host(self, n: int = FRAME_SIZE) -> np.ndarray:
+        """One frame from host_features() into the batch's pinned PCM buffer
+        (lpcnet_batch_synthesize on the batch's own buffers: no host staging
+        copies; the sample kernel stores the PCM there itself where it can).
+        Returns a [B, n] view of that buffer, valid until the next call."""
+        f = self.host_features()
+        pcm = self._hp[:self.B * n]
+        if lib.lpcnet_batch_synthesize(self._b, f.ctypes.data, pcm.ctypes.data, n) != 0:
+            raise LPCNetError(last_error())
+        return pcm.reshape(self.B, n)
+
     def synthesize_impl(self, features: np.ndarray, pcm: np.ndarray, preload: int) -> np.ndarray:
         """lpcnet_synthesize_impl: pcm [B, N] int16, first ``preload`` samples teacher-forced."""
         f = np.ascontiguousarray(np.asarray(features, np.float32)[:, :NB_FEATURES])
@@ -582,6 +609,7 @@ class LPCNetBatch:
 
     def close(self) -> None:
         if self._b:
+            self._hf = self._hp = None  # views of the batch's pinned buffers die with it
             lib.lpcnet_batch_destroy(self._b)
             self._b = None
 

@@ -46,6 +46,12 @@ static_assert(CK_PROJ % 16 == 0 && GA_ROWS % 16 == 0 && COND == 8 * 16, "row til
 /* smallest stride >= v that is 32 mod 64 floats: a 16-column tile that spans
  * two streams (NFR = 8) then reads 64 distinct banks */
 constexpr int ck_stride32(int v) { return v + ((32 - v % 64) + 64) % 64; }
+/* stream stride of the conv windows: one-frame launches put 16 streams in a
+ * column tile, lane (r, g) reading stream r's input 4 kk + g -- a stride of
+ * 4 mod 64 floats gives the 64 lanes 64 distinct banks (at 32 mod 64 they
+ * fell on 8: ~250 cycles per conv k step stamped, against ~100 for the dense
+ * layers' 132-float rows) */
+constexpr int ck_sstride(int v, int nfr) { return nfr == 1 ? v + ((4 - v % 64) + 64) % 64 : ck_stride32(v); }
 constexpr int ck_max(int a, int b) { return a > b ? a : b; }
 
 template <int NFR, int SC_>
@@ -55,8 +61,8 @@ struct CkGeom {
   static constexpr int NCT = COLS / 16;                    /* column tiles */
   static_assert(COLS % 16 == 0, "whole column tiles");
   static constexpr int INF = NFR + 2;                      /* frames -2 .. NFR-1 */
-  static constexpr int IN_SS = ck_stride32(INF * FIN);     /* conv1 inputs: stream stride */
-  static constexpr int C1_SS = ck_stride32(INF * CK_RS);   /* conv1 outputs: stream stride */
+  static constexpr int IN_SS = ck_sstride(INF * FIN, NFR);   /* conv1 inputs: stream stride */
+  static constexpr int C1_SS = ck_sstride(INF * CK_RS, NFR); /* conv1 outputs: stream stride */
   static constexpr int R0 = ck_max(SC * IN_SS, COLS * CK_RS); /* conv1 inputs, then dense1 outputs */
   static constexpr int R1 = SC * C1_SS;
   static constexpr int R2 = COLS * CK_RS;                  /* conv2, then dense2 outputs */
@@ -180,6 +186,27 @@ __device__ __forceinline__ int ck_fc(int fc0, int f) { return fc0 >= 1000 ? fc0 
 #define CK_T(k) do { } while (0)
 #endif
 
+/* a one-frame launch's L2 warm-up: the workgroups of an XCD (workgroup b
+ * runs on XCD b % 8, tools/probes/xcc_probe.hip) split every re-tiled weight
+ * matrix and touch each 128-byte line of their share once; the XOR of the
+ * values only keeps the loads alive (placement changes speed, never
+ * results) */
+__device__ __forceinline__ uint32_t ck_warm_weights(const FrameArgs &A, int tid)
+{
+  const int x = blockIdx.x % 8, nx = ((int)gridDim.x - 1 - x) / 8 + 1, k = blockIdx.x / 8;
+  const uint32_t *m[5] = {(const uint32_t *)A.ck_conv1, (const uint32_t *)A.ck_conv2, (const uint32_t *)A.ck_dense1,
+                          (const uint32_t *)A.ck_dense2, (const uint32_t *)A.ck_proj};
+  const int lines[5] = {8 * ck_tq(3 * FIN) * 64 * 16 / 128, 8 * ck_tq(3 * COND) * 64 * 16 / 128,
+                        8 * ck_tq(COND) * 64 * 16 / 128, 8 * ck_tq(COND) * 64 * 16 / 128,
+                        CK_PROJ_TILES * ck_tq(COND) * 64 * 16 / 128};
+  uint32_t acc = 0;
+#pragma unroll
+  for (int t = 0; t < 5; t++)
+#pragma unroll 4
+    for (int o = k * CK_THREADS + tid; o < lines[t]; o += nx * CK_THREADS) acc ^= m[t][(size_t)o * 32];
+  return acc;
+}
+
 template <int NFR, int SC, bool HWR>
 __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
 {
@@ -205,46 +232,76 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   const float gamma = A.mc.lpc_gamma;
 
   /* inputs (lpcnet.c:91-99): frames -2, -1 from the conv1 memory, then
-   * features | pitch embedding of each frame of the chunk.  The pitch rows
-   * first (one feature read per (stream, frame)), so the element loop below
-   * issues only independent loads (unrolled: one round trip instead of one
-   * per iteration -- stamped, the prologue of a one-frame launch was ~15 K
-   * cycles) */
-  __shared__ int pit[G::SC * NFR];
-  for (int e = tid; e < G::SC * NFR; e += CK_THREADS) {
-    const int s = e / NFR, fr = e % NFR, sid = s0 + s;
-    int pitch = 0;
-    if (sid < B && fr < n) {
-      /* lpcnet.c:93-94: the 0.1 avoids rounding issues */
-      pitch = (int)floor(.1 + (double)(50.f * A.features[((size_t)fr * B + sid) * NF + 18]) + 100);
-      pitch = min(255, max(33, pitch));
-    }
-    pit[e] = pitch;
-  }
-  __syncthreads();
+   * features | pitch embedding of each frame of the chunk; the conv2
+   * memory, the LPC ring, frame_count.  Every global read that depends on
+   * nothing goes out in one batch into registers (the lane of a pitch
+   * embedding element reads its frame's pitch feature itself, no pitch
+   * pass and barrier), then the embedding rows, then the LDS stores:
+   * stamped (CK_STAMPS), the pass-by-pass form of a one-frame launch took
+   * ~15 K cycles of dependent round trips here. */
+  constexpr int NIN = (G::SC * G::INF * FIN + CK_THREADS - 1) / CK_THREADS;
+  constexpr int NC2 = (G::SC * 2 * COND + CK_THREADS - 1) / CK_THREADS;
+  float vin[NIN], vc2[NC2];
 #pragma unroll
-  for (int e0 = 0; e0 < G::SC * G::INF * FIN; e0 += CK_THREADS) {
-    const int e = e0 + tid;
+  for (int q = 0; q < NIN; q++) {
+    const int e = q * CK_THREADS + tid;
+    float v = 0.f;
     if (e < G::SC * G::INF * FIN) {
       const int s = e / (G::INF * FIN), rem = e % (G::INF * FIN);
       const int fr = rem / FIN - 2, j = rem % FIN, sid = s0 + s;
-      float v = 0.f;
       if (sid < B) {
         if (fr < 0)
           v = A.st[sid].conv1_mem[(fr + 2) * FIN + j];
         else if (fr < n)
-          v = j < NF ? A.features[((size_t)fr * B + sid) * NF + j] : A.embed_pitch[pit[s * NFR + fr] * EP + (j - NF)];
+          v = A.features[((size_t)fr * B + sid) * NF + (j < NF ? j : 18)];
       }
-      inl[s * G::IN_SS + rem] = v;
+    }
+    vin[q] = v;
+  }
+#pragma unroll
+  for (int q = 0; q < NC2; q++) {
+    const int e = q * CK_THREADS + tid, sid = s0 + e / (2 * COND);
+    vc2[q] = e < G::SC * 2 * COND && sid < B ? A.st[sid].conv2_mem[e % (2 * COND)] : 0.f;
+  }
+  /* -DCK_WARM (A/B only): one-frame launches first read the weights into
+   * each XCD's L2 (one load per 128-byte line, values discarded), beside the
+   * inputs -- stamped, the inputs phase grew by ~6 K cycles and the layers
+   * did not move (their k steps were bank-conflict bound, see CkGeom) */
+  uint32_t warm = 0;
+#ifdef CK_WARM
+  if constexpr (NFR == 1) warm = ck_warm_weights(A, tid);
+#endif
+  /* this frame's lpc_from_cepstrum output, for the LPC ring after the
+   * projection (read now: behind the projection's stores it waits for them) */
+  __shared__ float nlpc[NFR == 1 ? G::SC * NLPC : 1];
+  if constexpr (NFR == 1) {
+    if (!A.mc.end2end && tid < G::SC * NLPC) {
+      const int sid = s0 + tid / NLPC;
+      nlpc[tid] = sid < B ? A.lpc_new[(size_t)sid * NLPC + tid % NLPC] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NIN; q++) {
+    const int e = q * CK_THREADS + tid;
+    if (e < G::SC * G::INF * FIN) {
+      const int s = e / (G::INF * FIN), rem = e % (G::INF * FIN);
+      const int fr = rem / FIN - 2, j = rem % FIN, sid = s0 + s;
+      if (sid < B && fr >= 0 && fr < n && j >= NF) {
+        /* lpcnet.c:93-94: the 0.1 avoids rounding issues */
+        int pitch = (int)floor(.1 + (double)(50.f * vin[q]) + 100);
+        pitch = min(255, max(33, pitch));
+        vin[q] = A.embed_pitch[pitch * EP + (j - NF)];
+      }
+      inl[s * G::IN_SS + rem] = vin[q];
     }
   }
   /* conv1 outputs of frames -2, -1: the conv2 memory */
 #pragma unroll
-  for (int e0 = 0; e0 < G::SC * 2 * COND; e0 += CK_THREADS) {
-    const int e = e0 + tid;
+  for (int q = 0; q < NC2; q++) {
+    const int e = q * CK_THREADS + tid;
     if (e < G::SC * 2 * COND) {
-      const int s = e / (2 * COND), j = e % (2 * COND), sid = s0 + s;
-      c1[s * G::C1_SS + (j / COND) * CK_RS + j % COND] = sid < B ? A.st[sid].conv2_mem[j] : 0.f;
+      const int s = e / (2 * COND), j = e % (2 * COND);
+      c1[s * G::C1_SS + (j / COND) * CK_RS + j % COND] = vc2[q];
     }
   }
   /* (a loop: 16-32 streams x FEATURES_DELAY 4 x 16 exceed the 512 threads) */
@@ -253,6 +310,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
     olpc[s][q / NLPC][q % NLPC] = sid < B ? A.st[sid].old_lpc[q / NLPC][q % NLPC] : 0.f;
   }
   if (tid < G::SC) fcs[tid] = s0 + tid < B ? A.st[s0 + tid].frame_count : 1000;
+  asm volatile("" ::"v"(warm)); /* the warming loads land before the weights are used */
   __syncthreads();
   CK_T(1);
 
@@ -369,9 +427,11 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
         lp[k] = lp[k] * gi;
         gi *= gamma;
       }
-      FrameCond *q = &A.cond[(size_t)f * B + sid];
+      if (A.cond) {
+        FrameCond *q = &A.cond[(size_t)f * B + sid];
 #pragma unroll
-      for (int k = 0; k < NLPC; k++) q->lpc[k] = lp[k];
+        for (int k = 0; k < NLPC; k++) q->lpc[k] = lp[k];
+      }
       if (f == n - 1)
 #pragma unroll
         for (int k = 0; k < NLPC; k++) A.st[sid].lpc[k] = lp[k];
@@ -409,25 +469,33 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
       for (int j = 0; j < NCT; j++) {
         const int sid = s0 + cs[j], f = cf[j];
         if (sid >= B || f >= n) continue;
-        FrameCond *q = &A.cond[(size_t)f * B + sid];
         StreamState *p = &A.st[sid];
         /* this lane's 4 consecutive rows as one 16-byte store: the 4 lanes of
          * a column write its 16 rows as one 64-byte run (GA_ROWS is a multiple
          * of 16, so a row quad never straddles the two arrays) */
         const int row = 16 * rts[t] + 4 * g;
         const float4 v = make_float4(pacc[t][j][0], pacc[t][j][1], pacc[t][j][2], pacc[t][j][3]);
-        float *qd = row < GA_ROWS ? q->gru_a_cond + row : q->gru_b_cond + (row - GA_ROWS);
-        *(float4 *)qd = v;
+        if (A.cond) {
+          FrameCond *q = &A.cond[(size_t)f * B + sid];
+          float *qd = row < GA_ROWS ? q->gru_a_cond + row : q->gru_b_cond + (row - GA_ROWS);
+          *(float4 *)qd = v;
+        }
         if (f == n - 1) *(float4 *)(row < GA_ROWS ? p->gru_a_cond + row : p->gru_b_cond + (row - GA_ROWS)) = v;
       }
     }
   }
 
   CK_T(5);
+  /* lpc_from_cepstrum of frame t of the chunk (one-frame launches: t = 0,
+   * staged in LDS by the prologue) */
+  auto lpcn = [&](int t, int s, int sid, int k) {
+    if constexpr (NFR == 1) return nlpc[s * NLPC + k];
+    else return A.lpc_new[((size_t)t * B + sid) * NLPC + k];
+  };
   /* per frame: the LPC it synthesises with (lpcnet.c:110-118: the ring's
    * oldest slot, i.e. lpc_from_cepstrum of frame f - FEATURES_DELAY, then
    * lpc_weighting; END2END: written above) and frame_count after its update */
-  for (int e = tid; e < G::SC * NFR * (NLPC + 1); e += CK_THREADS) {
+  for (int e = tid; A.cond && e < G::SC * NFR * (NLPC + 1); e += CK_THREADS) {
     const int s = e / (NFR * (NLPC + 1)), rem = e % (NFR * (NLPC + 1));
     const int f = rem / (NLPC + 1), k = rem % (NLPC + 1), sid = s0 + s;
     if (sid >= B || f >= n) continue;
@@ -437,7 +505,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
       q->frame_count = fc < 1000 ? fc + 1 : fc;
     } else if (!A.mc.end2end) {
       const int t = f - D;
-      q->lpc[k] = lpc_weight(t >= 0 ? A.lpc_new[((size_t)t * B + sid) * NLPC + k] : olpc[s][-1 - t][k], k, gamma);
+      q->lpc[k] = lpc_weight(t >= 0 ? lpcn(t, s, sid, k) : olpc[s][-1 - t][k], k, gamma);
     }
   }
   /* the stream state after the chunk: conv2 memory = conv1 outputs of frames
@@ -449,7 +517,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   if (!A.mc.end2end && tid < G::SC * NLPC) {
     const int s = tid / NLPC, k = tid % NLPC, sid = s0 + s;
     if (sid < B) {
-      auto L = [&](int t) { return t >= 0 ? A.lpc_new[((size_t)t * B + sid) * NLPC + k] : olpc[s][-1 - t][k]; };
+      auto L = [&](int t) { return t >= 0 ? lpcn(t, s, sid, k) : olpc[s][-1 - t][k]; };
       StreamState *p = &A.st[sid];
       p->lpc[k] = lpc_weight(L(n - 1 - D), k, gamma);
       for (int j = 0; j < D; j++) p->old_lpc[j][k] = L(n - 1 - j);
@@ -501,7 +569,10 @@ static int launch_chunk_h(const FrameArgs &a, void *stream)
 
 int launch_chunk(const FrameArgs &a, void *stream)
 {
-  if (a.nframes < 1 || a.nframes > LPC_CHUNK || !a.cond) return -1;
+  /* one-frame launches may run without per-frame outputs (cond null): the
+   * stream state carries the frame's conditioning, LPC and frame_count, and
+   * the sample kernel reads them from there */
+  if (a.nframes < 1 || a.nframes > LPC_CHUNK || (!a.cond && a.nframes != 1)) return -1;
   /* tanh through the hardware reciprocal, or through the LDS table when the
    * batch carries another host's rcpps (same-box parity) */
   return a.rcp_hw ? launch_chunk_h<true>(a, stream) : launch_chunk_h<false>(a, stream);

@@ -358,9 +358,13 @@ struct LPCNetBatch {
   /* per-frame host-I/O path of large batches (synth_first): one frame's
    * chunk_kernel outputs [B], and pinned staging of the caller's features and
    * PCM (so both copies are asynchronous, behind one synchronisation) */
-  FrameCond *d_cond1 = nullptr;
   float *h_io_feat = nullptr;
   short *h_io_pcm = nullptr;
+  short *d_io_pcm = nullptr; /* h_io_pcm's device address (mapped) */
+  float *d_io_feat = nullptr; /* h_io_feat's device address (mapped) */
+  float *h_stg_feat = nullptr; /* pinned staging of the caller's own buffers */
+  short *h_stg_pcm = nullptr;
+  hipEvent_t ev_tick = nullptr; /* end of a host-I/O tick (spin-polled) */
   /* trace */
   bool trace = false;
   float *d_trace_logits = nullptr;
@@ -2036,9 +2040,11 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
   (void)hipFree(b->d_lpc);
   (void)hipFree(b->d_lpc_tab);
   (void)hipFree(b->d_chunk);
-  (void)hipFree(b->d_cond1);
   (void)hipHostFree(b->h_io_feat);
   (void)hipHostFree(b->h_io_pcm);
+  (void)hipHostFree(b->h_stg_feat);
+  (void)hipHostFree(b->h_stg_pcm);
+  if (b->ev_tick) (void)hipEventDestroy(b->ev_tick);
   (void)hipFree(b->d_packets);
   (void)hipFree(b->d_dfeat);
   (void)hipFree(b->d_dpcm);
@@ -2149,7 +2155,9 @@ using PreSync = std::function<int()>;
  * stream-only columns (weights fetched once per 16-32 streams instead of the
  * per-frame frame_kernel's once per 4: at 1024 streams ~44 -> ~20 us, at
  * 28 K streams 28 rounds of workgroups -> 2-4), then the sample kernel
- * reading the outputs from d_cond1.  Same arithmetic as every other frame
+ * reading the frame's conditioning, LPC and frame_count from the stream
+ * state (no per-frame output copy: half the chunk kernel's stores).  Same
+ * arithmetic as every other frame
  * path (the chunk kernel is bit-identical to the frame kernel). */
 static bool single_frame_chunked(const LPCNetBatch *b, int nB, int N, int preload)
 {
@@ -2159,7 +2167,6 @@ static bool single_frame_chunked(const LPCNetBatch *b, int nB, int N, int preloa
 
 static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_features, short *d_pcm, int N)
 {
-  if (!b->d_cond1) HIPCHK(hipMalloc(&b->d_cond1, sizeof(FrameCond) * (size_t)b->B));
   if (!b->mc.end2end && launch_lpc(d_features, b->d_lpc, nB, b->d_lpc_tab, b->stream)) {
     set_err("lpc kernel launch failed");
     return -1;
@@ -2171,7 +2178,7 @@ static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_fe
   fa.features = d_features;
   fa.lpc_new = b->d_lpc;
   fa.nframes = 1;
-  fa.cond = b->d_cond1;
+  fa.cond = nullptr;
   fa.stamps = nullptr;
   hipEvent_t e[3] = {nullptr, nullptr, nullptr};
   if (b->timing >= 2) e[0] = get_event(b);
@@ -2188,7 +2195,7 @@ static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_fe
   SampleArgs sa = b->sa;
   sa.st = b->d_state;
   sa.delay = b->mc.delay;
-  sa.cond = b->d_cond1;
+  sa.cond = nullptr;
   sa.nstreams = nB;
   sa.N = N;
   sa.nframes = 1;
@@ -2222,6 +2229,57 @@ static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_fe
   return 0;
 }
 
+/* the batch's pinned host I/O buffers ([B][NF] features, [B][FRAME] PCM,
+ * mapped: the kernels read and store them over PCIe) and the pinned staging
+ * of callers' own buffers (cached, DMA) */
+static int ensure_host_io(LPCNetBatch *b)
+{
+  if (!b->h_io_feat) {
+    HIPCHK(hipHostMalloc(&b->h_io_feat, sizeof(float) * NF * (size_t)b->B, hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer((void **)&b->d_io_feat, b->h_io_feat, 0));
+  }
+  if (!b->h_io_pcm) {
+    HIPCHK(hipHostMalloc(&b->h_io_pcm, sizeof(short) * FRAME * (size_t)b->B, hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer((void **)&b->d_io_pcm, b->h_io_pcm, 0));
+  }
+  if (!b->h_stg_feat) HIPCHK(hipHostMalloc(&b->h_stg_feat, sizeof(float) * NF * (size_t)b->B, hipHostMallocDefault));
+  if (!b->h_stg_pcm) HIPCHK(hipHostMalloc(&b->h_stg_pcm, sizeof(short) * FRAME * (size_t)b->B, hipHostMallocDefault));
+  return 0;
+}
+
+/* the end of a host-I/O tick: the calling thread polls the tick's event
+ * (no sleep/wake-up between the last kernel and the caller's next frame),
+ * handing over to a blocking wait after TICK_SPIN_MS.  LPCNET_SYNC_BLOCK=1:
+ * hipStreamSynchronize. */
+static int tick_sync(LPCNetBatch *b)
+{
+  if (getenv("LPCNET_SYNC_BLOCK")) {
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return 0;
+  }
+  if (!b->ev_tick) HIPCHK(hipEventCreateWithFlags(&b->ev_tick, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(b->ev_tick, b->stream));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipEventQuery(b->ev_tick);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) HIPCHK(q);
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(TICK_SPIN_MS)) break;
+  }
+  HIPCHK(hipEventSynchronize(b->ev_tick));
+  return 0;
+}
+
+/* sample kernels whose PCM write-out is wide (a frame's samples, or 16 of
+ * them, per stream in consecutive lanes): mf_kernel at the end of the
+ * launch, mfw_kernel every 16 samples, fp_kernel at the end.  mf2_kernel
+ * stores every sample as it is drawn (2-byte stores: over PCIe, one
+ * transaction each), so its PCM goes through device memory and one copy. */
+static bool pcm_store_coalesced(const LPCNetBatch *b)
+{
+  return !getenv("LPCNET_NO_DIRECT_PCM") && (b->fp || b->mfw || (b->mf && !b->mf2));
+}
+
 /* one frame for the first nB streams of a batch, host I/O ([nB][NF] in,
  * [nB][N] out) */
 static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm, int N, int preload,
@@ -2233,16 +2291,32 @@ static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm
   if (ensure_trace(b, N)) return -1;
   if (!staged && !pre && single_frame_chunked(b, nB, N, preload)) {
     /* the caller's buffers through pinned staging: both copies truly
-     * asynchronous, one synchronisation per frame */
-    if (!b->h_io_feat) HIPCHK(hipHostMalloc(&b->h_io_feat, sizeof(float) * NF * (size_t)b->B, hipHostMallocDefault));
-    if (!b->h_io_pcm) HIPCHK(hipHostMalloc(&b->h_io_pcm, sizeof(short) * FRAME * (size_t)b->B, hipHostMallocDefault));
-    memcpy(b->h_io_feat, features, sizeof(float) * NF * nB);
-    HIPCHK(hipMemcpyAsync(b->d_feat, b->h_io_feat, sizeof(float) * NF * nB, hipMemcpyHostToDevice, b->stream));
-    if (launch_single_frame_chunked(b, nB, b->d_feat, b->d_pcm, N)) return -1;
-    HIPCHK(hipMemcpyAsync(b->h_io_pcm, b->d_pcm, sizeof(short) * N * nB, hipMemcpyDeviceToHost, b->stream));
-    HIPCHK(hipStreamSynchronize(b->stream));
+     * asynchronous, one synchronisation per frame.  Features already in the
+     * batch's own pinned buffer (lpcnet_batch_host_features) skip the host
+     * copy; PCM into the batch's own pinned buffer (lpcnet_batch_host_pcm)
+     * is stored there by the sample kernel itself when its write-out is
+     * coalesced (no device-to-host copy, no host copy) */
+    if (ensure_host_io(b)) return -1;
+    /* the batch's own buffers (mapped): up to ZC_FEAT_MAX streams the LPC
+     * and chunk kernels read the features straight from host memory (80 B
+     * per stream over PCIe, no copy command and its start latency), larger
+     * batches take one DMA copy; the caller's buffers: host copy into the
+     * cached pinned staging, one DMA copy each way */
+    const bool own_feat = features == b->h_io_feat, own_pcm = pcm == b->h_io_pcm;
+    const bool zc_feat = own_feat && nB <= ZC_FEAT_MAX && !getenv("LPCNET_FEAT_DMA");
+    if (!own_feat) memcpy(b->h_stg_feat, features, sizeof(float) * NF * nB);
+    if (!zc_feat)
+      HIPCHK(hipMemcpyAsync(b->d_feat, own_feat ? b->h_io_feat : b->h_stg_feat, sizeof(float) * NF * nB,
+                            hipMemcpyHostToDevice, b->stream));
+    const bool direct = own_pcm && pcm_store_coalesced(b);
+    if (launch_single_frame_chunked(b, nB, zc_feat ? b->d_io_feat : b->d_feat, direct ? b->d_io_pcm : b->d_pcm, N))
+      return -1;
+    if (!direct)
+      HIPCHK(hipMemcpyAsync(own_pcm ? b->h_io_pcm : b->h_stg_pcm, b->d_pcm, sizeof(short) * N * nB,
+                            hipMemcpyDeviceToHost, b->stream));
+    if (tick_sync(b)) return -1;
     if (check_status(b)) return -1;
-    memcpy(pcm, b->h_io_pcm, sizeof(short) * N * nB);
+    if (!own_pcm) memcpy(pcm, b->h_stg_pcm, sizeof(short) * N * nB);
     return 0;
   }
   /* everything below is ordered after work already queued on b->stream
@@ -2267,6 +2341,18 @@ LPCNET_EXPORT int lpcnet_batch_synthesize_impl(LPCNetBatch *b, const float *feat
 LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features, short *pcm, int N)
 {
   return lpcnet_batch_synthesize_impl(b, features, pcm, N, 0);
+}
+
+LPCNET_EXPORT float *lpcnet_batch_host_features(LPCNetBatch *b)
+{
+  if (!b || b->set_device() || ensure_host_io(b)) return nullptr;
+  return b->h_io_feat;
+}
+
+LPCNET_EXPORT short *lpcnet_batch_host_pcm(LPCNetBatch *b)
+{
+  if (!b || b->set_device() || ensure_host_io(b)) return nullptr;
+  return b->h_io_pcm;
 }
 
 static int ensure_decode_bufs(LPCNetBatch *b, bool host_io)

@@ -803,3 +803,44 @@ def test_wide_kernel_matches_oracle(require_gpu, monkeypatch, B, F):
     for s in sorted({0, 5, 11, B // 2, B - 1}):
         o = O.Oracle(blob, 0)
         assert np.array_equal(got[s], np.stack([o.synthesize(allf[f, s]) for f in range(F)])), s
+
+
+@pytest.mark.parametrize("variant,B,n,mfw", [(0, 1024, 160, "0"), (0, 1024, 80, "0"), (0, 2100, 160, "0"),
+                                             (0, 3073, 160, "1"), (1, 200, 160, "0"), (0, 64, 160, "0"),
+                                             (0, 4100, 160, "0")])
+def test_live_engine_buffers_match_caller_buffers(require_gpu, monkeypatch, variant, B, n, mfw):
+    """lpcnet_batch_synthesize on the batch's own pinned buffers
+    (lpcnet_batch_host_features / _pcm): the sample kernel stores the PCM into
+    the mapped host buffer itself (mf_kernel at 1024 streams, mfw_kernel at
+    3073, fp_kernel at 200; N = 80 packs [B][80]), mf2_kernel (2100, 4100)
+    and the small-batch path (64) go through device memory and one copy; up
+    to 4096 streams the LPC and chunk kernels read the features from the
+    mapped buffer -- PCM identical to the caller-buffer path with DMA-copied
+    features on every stream and frame, and to the oracle on sampled
+    streams."""
+    monkeypatch.setenv("LPCNET_MFW", mfw)
+    blob = L.synthetic_model(1, variant)
+    F = 5
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    b = L.LPCNetBatch(B, 0, blob)
+    hf = b.host_features()
+    assert hf.shape == (B, 20)
+    got = []
+    for f in range(F):
+        np.copyto(hf, allf[f])
+        got.append(np.array(b.synthesize_host(n)))
+    got = np.stack(got, 1)
+    b.close()
+    # the caller-buffer path with the features in one DMA copy and a blocking
+    # wait (the zero-copy feature reads and the polled tick end off)
+    monkeypatch.setenv("LPCNET_FEAT_DMA", "1")
+    monkeypatch.setenv("LPCNET_SYNC_BLOCK", "1")
+    b2 = L.LPCNetBatch(B, 0, blob)
+    ref = np.stack([b2.synthesize(allf[f], n) for f in range(F)], 1)
+    b2.close()
+    assert got.shape == (B, F, n)
+    assert np.array_equal(got, ref)
+    if n == 160:
+        for s in sorted({0, B // 2, B - 1}):
+            o = O.Oracle(blob, variant)
+            assert np.array_equal(got[s], np.stack([o.synthesize(allf[f, s]) for f in range(F)])), s
