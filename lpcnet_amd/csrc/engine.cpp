@@ -323,6 +323,7 @@ struct LPCNetBatch {
   bool mf = false;       /* mf_kernel (mode 4) */
   bool mf2 = false;      /* large batches: mf2_kernel (two staggered 4-stream groups per workgroup) for
                             launches without preload / trace / stamps */
+  int mfw_g = 3;         /* mfw_kernel's four-stream groups per workgroup (2 or 3) */
   bool mfw = false;      /* wider batches: mfw_kernel (three 4-stream groups, dedicated gather /
                             recurrent / sampler waves) for the same launches, non-split models with the
                             default rcpps */
@@ -445,12 +446,12 @@ bool block_may_saturate(const int8_t *w)
   return false;
 }
 
-bool mfw_pays(int B, int cus)
+int mfw_groups(int B, int cus)
 {
-  if (B < MFW_MIN_STREAMS || cus < 1) return false;
-  const long per_round = (long)MFW_STREAMS_PER_WG * cus;
-  const long padded = (B + per_round - 1) / per_round * per_round;
-  return (double)padded <= MFW_GAIN * B;
+  if (cus < 1 || B <= 4 * cus) return 0;
+  const double c2 = (double)((B + 8 * cus - 1) / (8 * cus)) * 2;
+  const double c3 = (double)((B + 12 * cus - 1) / (12 * cus)) * 3 * MFW_G3_PHASE;
+  return c3 < c2 ? 3 : 2;
 }
 
 /* Sample-kernel choice (mode 0 = automatic):
@@ -487,24 +488,29 @@ void choose_kernel(LPCNetBatch *b)
     b->info.lds_bytes = mf_lds_bytes(b->S, b->sa.mf_split);
     b->info.quad_path = 4;
     /* two staggered 4-stream groups per workgroup from MF2_MIN_STREAMS on
-     * (LPCNET_MF2=0 off, =1 at any batch size) */
+     * (LPCNET_MF2=0 off, =1 at any batch size); above one mf_kernel<4>
+     * round, mfw_kernel (two or three groups with dedicated roles) where the
+     * model allows it (LPCNET_MFW=0/1 off / on wherever mf2 runs,
+     * LPCNET_MFW_G=2/3 forces the group count) */
+    const int gauto = mfw_groups(b->B, current_device_cus());
+    const bool mfw_ok = !b->sa.mf_split && b->sa.rcp_hw;
+    const char *ew = getenv("LPCNET_MFW");
+    const bool wantw = ew ? atoi(ew) != 0 : gauto > 0;
     const char *e2 = getenv("LPCNET_MF2");
-    const bool want2 = e2 ? atoi(e2) != 0 : b->B >= MF2_MIN_STREAMS;
+    const bool want2 = e2 ? atoi(e2) != 0 : b->B >= MF2_MIN_STREAMS || (wantw && mfw_ok);
     if (want2 && mf2_lds_bytes(4, b->sa.mf_split) <= 160 * 1024) {
       b->mf2 = true;
       b->info.mfma_ops_per_group_sample = 2 * (b->mf_ga_ops + b->mf_gb_ops);
       b->info.streams_per_workgroup = 8;
       b->info.lds_bytes = mf2_lds_bytes(4, b->sa.mf_split);
       b->info.quad_path = 6;
-      /* three groups with dedicated roles from MFW_MIN_STREAMS on
-       * (LPCNET_MFW=0 off, =1 at any batch size that takes mf2) */
-      const char *ew = getenv("LPCNET_MFW");
-      const bool wantw = ew ? atoi(ew) != 0 : mfw_pays(b->B, current_device_cus());
-      if (wantw && !b->sa.mf_split && b->sa.rcp_hw && mfw_lds_bytes() <= 160 * 1024) {
+      const char *eg = getenv("LPCNET_MFW_G");
+      b->mfw_g = eg ? (atoi(eg) == 2 ? 2 : 3) : (gauto ? gauto : 2);
+      if (wantw && mfw_ok && mfw_lds_bytes(b->mfw_g) <= 160 * 1024) {
         b->mfw = true;
-        b->info.mfma_ops_per_group_sample = 3 * (b->mf_ga_ops + b->mf_gb_ops);
-        b->info.streams_per_workgroup = MFW_STREAMS_PER_WG;
-        b->info.lds_bytes = mfw_lds_bytes();
+        b->info.mfma_ops_per_group_sample = b->mfw_g * (b->mf_ga_ops + b->mf_gb_ops);
+        b->info.streams_per_workgroup = 4 * b->mfw_g;
+        b->info.lds_bytes = mfw_lds_bytes(b->mfw_g);
         b->info.quad_path = 7;
       }
     }
@@ -1803,7 +1809,7 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   const int lrc = N <= 0 ? 0
                 : b->fp    ? launch_fp(sa, b->stream)
-                : b->mfw && !sa.preload && !sa.trace_logits && !sa.stamps ? launch_mfw(sa, b->stream)
+                : b->mfw && !sa.preload && !sa.trace_logits && !sa.stamps ? launch_mfw(sa, b->mfw_g, b->stream)
                 : b->mf2 && !sa.preload && !sa.trace_logits && !sa.stamps ? launch_mf2(sa, 4, b->stream)
                 : b->mf    ? launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream)
                              : launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream);
@@ -1867,7 +1873,7 @@ int launch_chunk_samples(LPCNetBatch *b, int f, short *d_pcm, int N, int nfr = 1
   }
   const int lrc = N <= 0                                  ? 0
                   : b->fp                                 ? launch_fp(sa, b->stream)
-                  : b->mfw && !sa.trace_logits && !sa.stamps ? launch_mfw(sa, b->stream)
+                  : b->mfw && !sa.trace_logits && !sa.stamps ? launch_mfw(sa, b->mfw_g, b->stream)
                   : b->mf2 && !sa.trace_logits && !sa.stamps ? launch_mf2(sa, 4, b->stream)
                                                           : launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream);
   if (lrc) {
@@ -2206,7 +2212,7 @@ static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_fe
   sa.spin_limit = b->spin_limit;
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   const int lrc = b->fp ? launch_fp(sa, b->stream)
-                  : b->mfw ? launch_mfw(sa, b->stream)
+                  : b->mfw ? launch_mfw(sa, b->mfw_g, b->stream)
                   : b->mf2 ? launch_mf2(sa, 4, b->stream)
                            : launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream);
   if (lrc) {

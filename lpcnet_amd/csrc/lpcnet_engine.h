@@ -333,20 +333,22 @@ int launch_mf(const SampleArgs &a, int S, int lds_bytes, void *stream);
 constexpr int MF2_MIN_STREAMS = 2048; /* automatic choice of mf2_kernel from this batch size */
 int mf2_lds_bytes(int S, int split);
 int launch_mf2(const SampleArgs &a, int S, void *stream);
-/* wide-batch kernel (mfw_kernel.hip): three 4-stream groups per 896-thread
- * workgroup with dedicated gather/elementwise, recurrent and sampler waves;
- * non-split int8 models with the default (Intel) rcpps, no preload / trace /
- * stamps (-1 otherwise) */
-constexpr int MFW_STREAMS_PER_WG = 12;
-constexpr int MFW_MIN_STREAMS = 3072; /* automatic choice from this batch size on (LPCNET_MFW=0/1 overrides) */
-/* mfw_kernel runs in rounds of one 12-stream workgroup per CU: it is taken
- * when those rounds, padded to whole, cost less than mf2_kernel's nearly
- * continuous per-stream cost -- measured per stream at whole rounds (24576
- * streams, same box) mf2 / mfw = 1.077 */
-constexpr double MFW_GAIN = 1.077;
-bool mfw_pays(int B, int cus);
-int mfw_lds_bytes();
-int launch_mfw(const SampleArgs &a, void *stream);
+/* wide-batch kernel (mfw_kernel.hip): 2 or 3 four-stream groups per
+ * 896-thread workgroup with dedicated gather/elementwise, recurrent and
+ * sampler waves; non-split int8 models with the default (Intel) rcpps, no
+ * preload / trace / stamps (-1 otherwise) */
+/* mfw_kernel runs in rounds of one workgroup per CU.  Per stream at whole
+ * rounds (24,576 streams, same box, profiles/r05): two groups 7.07 ms per
+ * frame, three 7.36 (per-phase time 1.04x), mf2_kernel 8.02 -- so two
+ * groups replace mf2_kernel wherever both apply (same 8-stream rounds), and
+ * three groups are taken where their 12-stream rounds save more than the 4 %
+ * (3,072 streams: one round against two).  Above 4 streams per CU only:
+ * below, mf_kernel's one-group latency wins. */
+constexpr double MFW_G3_PHASE = 1.04;
+/* 0 (batch within one mf_kernel<4> round), 2 or 3 */
+int mfw_groups(int B, int cus);
+int mfw_lds_bytes(int groups);
+int launch_mfw(const SampleArgs &a, int groups, void *stream);
 /* fp32 latency kernel: one stream per workgroup, LDS flags instead of
  * workgroup barriers (fp32 models within the FP_* limits, dense GRU_B). */
 int fp_lds_bytes();

@@ -48,13 +48,13 @@
 namespace lpcnet_mi355x {
 
 constexpr int MFW_S = 4;                 /* streams per group */
-constexpr int MFW_G = 3;                 /* groups per workgroup */
-constexpr int MFW_GS = MFW_S * MFW_G;    /* streams per workgroup */
 constexpr int MFW_THREADS = 64 * 14;     /* 6 E + 2 S + 6 R waves */
 constexpr int MFW_S_WAVE0 = 6, MFW_R_WAVE0 = 8;
-static_assert(MFW_STREAMS_PER_WG == MFW_GS, "lpcnet_engine.h");
 
+/* MFW_G groups of MFW_S streams per workgroup (2 or 3, see the header) */
+template <int MFW_G>
 struct MfwLds {
+  static constexpr int MFW_GS = MFW_S * MFW_G;                  /* streams per workgroup */
   static constexpr int x = MFW_GS * MF_XSTR;                    /* q(h_A) [group][stream][MF_XSTR] (signed) */
   static constexpr int xb = MFW_GS * NB;                        /* q(h_B) [group][stream][16] */
   static constexpr int sb = MFW_GS * NB * 4;                    /* float h_B [group][stream][16] (walk broadcast) */
@@ -74,11 +74,12 @@ struct MfwLds {
 };
 /* the image sections without the rcpps table: u-law, logit, dual_fc */
 constexpr int MFW_IMG = IMG_VAR - IMG_ULAW;
-static_assert(MfwLds::total + MFW_IMG <= 160 * 1024, "mfw_kernel LDS");
+static_assert(MfwLds<3>::total + MFW_IMG <= 160 * 1024, "mfw_kernel LDS");
 
-int mfw_lds_bytes() { return MfwLds::total + MFW_IMG; }
+int mfw_lds_bytes(int groups) { return (groups == 2 ? MfwLds<2>::total : MfwLds<3>::total) + MFW_IMG; }
 
-__device__ __forceinline__ int mod3(int p) { return (p % 3 + 3) % 3; }
+template <int G>
+__device__ __forceinline__ int modg(int p) { return (p % G + G) % G; }
 
 /* keeps the next group's / K tile's LDS reads ahead of the current MFMAs
  * (the scheduler otherwise sinks them to their use) */
@@ -117,7 +118,7 @@ __device__ __forceinline__ int mod3(int p) { return (p % 3 + 3) % 3; }
   do {                                                                                                        \
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0)                                                           \
       printf("mfw wave %d %s: work %llu wait %llu per phase %.0f / %.0f\n", (int)(threadIdx.x >> 6), role,   \
-             st_work, st_wait, (double)st_work / (3.0 * total + 1), (double)st_wait / (3.0 * total + 1));    \
+             st_work, st_wait, (double)st_work / (MFW_G * total + 1.0), (double)st_wait / (MFW_G * total + 1.0)); \
   } while (0)
 #else
 #define MFW_BAR() __syncthreads()
@@ -136,34 +137,37 @@ __device__ __forceinline__ uint32_t mfw_x(const unsigned char *xg, const uint32_
   return *(const uint32_t *)(xg + ((__builtin_amdgcn_ubfe(cw[t >> 2], 8 * (t & 3), 8) << 2) + mo));
 }
 
+/* x words of 4-slot groups in flight ahead of the MFMAs (the R waves' LDS
+ * reads; -DMFW_XD=n for A/B) */
+#ifndef MFW_XD
+#define MFW_XD 1
+#endif
+
 /* one gate's product over NG 4-slot groups, NC accumulators (slot k -> k %
- * NC; exact int32, any split), x words of group g + 1 read while group g's
- * MFMAs run (mf_common.h mf_run with compile-time counts) */
+ * NC; exact int32, any split), the x words of group g + MFW_XD read while
+ * group g's MFMAs run (mf_common.h mf_run with compile-time counts) */
 template <int NG, int NC>
 __device__ __forceinline__ void mfw_gate(const unsigned char *xg, const uint32_t (&w)[4 * NG],
                                          const uint32_t (&cw)[NG], uint32_t mo, v4i (&a)[NC])
 {
-  uint32_t x[4];
+  uint32_t x[NG][4];
 #pragma unroll
-  for (int k = 0; k < 4; k++) x[k] = mfw_x(xg, cw, k, mo);
+  for (int d = 0; d < MFW_XD && d < NG; d++)
+#pragma unroll
+    for (int k = 0; k < 4; k++) x[d][k] = mfw_x(xg, cw, 4 * d + k, mo);
 #pragma unroll
   for (int g = 0; g < NG; g++) {
-    uint32_t n[4];
-    if (g + 1 < NG) {
+    if (g + MFW_XD < NG) {
 #pragma unroll
-      for (int k = 0; k < 4; k++) n[k] = mfw_x(xg, cw, 4 * (g + 1) + k, mo);
+      for (int k = 0; k < 4; k++) x[g + MFW_XD][k] = mfw_x(xg, cw, 4 * (g + MFW_XD) + k, mo);
     }
-    /* the next group's reads stay ahead of this group's products (the
+    /* the next groups' reads stay ahead of this group's products (the
      * scheduler otherwise sinks them below, one exposed LDS round trip per
      * group) */
     MFW_FENCE();
 #pragma unroll
-    for (int k = 0; k < 4; k++) a[k % NC] = mfma4(x[k], w[4 * g + k], a[k % NC]);
+    for (int k = 0; k < 4; k++) a[k % NC] = mfma4(x[g][k], w[4 * g + k], a[k % NC]);
     MFW_FENCE();
-    if (g + 1 < NG) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) x[k] = n[k];
-    }
   }
 }
 
@@ -172,41 +176,35 @@ template <int NG>
 __device__ __forceinline__ void mfw_zr(const unsigned char *xg, const uint32_t (&wz)[4 * NG], const uint32_t (&wr)[4 * NG],
                                        const uint32_t (&cz)[NG], const uint32_t (&cr)[NG], uint32_t mo, v4i &az, v4i &ar)
 {
-  uint32_t xz[4], xr[4];
+  uint32_t xz[NG][4], xr[NG][4];
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    xz[k] = mfw_x(xg, cz, k, mo);
-    xr[k] = mfw_x(xg, cr, k, mo);
-  }
+  for (int d = 0; d < MFW_XD && d < NG; d++)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      xz[d][k] = mfw_x(xg, cz, 4 * d + k, mo);
+      xr[d][k] = mfw_x(xg, cr, 4 * d + k, mo);
+    }
 #pragma unroll
   for (int g = 0; g < NG; g++) {
-    uint32_t nz[4], nr[4];
-    if (g + 1 < NG) {
+    if (g + MFW_XD < NG) {
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        nz[k] = mfw_x(xg, cz, 4 * (g + 1) + k, mo);
-        nr[k] = mfw_x(xg, cr, 4 * (g + 1) + k, mo);
+        xz[g + MFW_XD][k] = mfw_x(xg, cz, 4 * (g + MFW_XD) + k, mo);
+        xr[g + MFW_XD][k] = mfw_x(xg, cr, 4 * (g + MFW_XD) + k, mo);
       }
     }
     MFW_FENCE(); /* as mfw_gate */
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      az = mfma4(xz[k], wz[4 * g + k], az);
-      ar = mfma4(xr[k], wr[4 * g + k], ar);
+      az = mfma4(xz[g][k], wz[4 * g + k], az);
+      ar = mfma4(xr[g][k], wr[4 * g + k], ar);
     }
     MFW_FENCE();
-    if (g + 1 < NG) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        xz[k] = nz[k];
-        xr[k] = nr[k];
-      }
-    }
   }
 }
 
 /* ---- R role: GRU_A recurrent products (nnet.c:441) ------------------------ */
-template <int Z, int H>
+template <int MFW_G, int Z, int H>
 __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *xa, int *trm, int r, int lane, int total)
 {
   /* this lane's weight words and packed column quads (engine.cpp mf tables:
@@ -235,8 +233,10 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
   __syncthreads(); /* image in LDS */
   __syncthreads(); /* initial q(h_A) of every group */
   MFW_STAMP_DECL;
-  for (int p = -1; p <= 3 * total; p++) {
-    const int g = mod3(p + 1), tn = (p - 2 - g) / 3 + 1; /* group, sample whose sums these are */
+  /* group (p - (G - 1)) mod G: three groups, the group E left two phases
+   * ago (S walks it in between); two groups, the group S walks beside */
+  for (int p = -1; p <= MFW_G * total; p++) {
+    const int g = modg<MFW_G>(p - (MFW_G - 1)), tn = (p - (MFW_G - 1) - g) / MFW_G + 1; /* group, sample whose sums these are */
     if (p >= 0) MFW_BAR(); /* phase p */
     if (tn < 0 || tn >= total) continue;
     const unsigned char *xg = xa + g * MFW_S * MF_XSTR;
@@ -262,13 +262,15 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
   MFW_STAMP_PRINT("R");
 }
 
-template <bool HWR>
+template <bool HWR, int MFW_G>
 __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
 {
   static_assert(HWR, "mfw_kernel: hardware reciprocal only (no rcpps table in LDS)");
+  static_assert(MFW_G == 2 || MFW_G == 3, "two or three groups");
   extern __shared__ uint4 lds4[];
   unsigned char *lds = (unsigned char *)lds4;
-  using L = MfwLds;
+  using L = MfwLds<MFW_G>;
+  constexpr int MFW_GS = L::MFW_GS;
   constexpr int S = MFW_S;
   unsigned char *xa = lds; /* first: every x address fits 16 bits */
   unsigned char *xb = xa + L::x;
@@ -331,7 +333,7 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
     const int r = wv - MFW_R_WAVE0;
     switch (A.mf_nzr[r] * 16 + A.mf_nh[r]) {
 #define MFW_CASE(Z, H) \
-  case Z * 16 + H: mfw_r_role<Z, H>(A, xa, trm, r, lane, total); break;
+  case Z * 16 + H: mfw_r_role<MFW_G, Z, H>(A, xa, trm, r, lane, total); break;
 #define MFW_CASES(Z) MFW_CASE(Z, 1) MFW_CASE(Z, 2) MFW_CASE(Z, 3) MFW_CASE(Z, 4) MFW_CASE(Z, 5) MFW_CASE(Z, 6) MFW_CASE(Z, 7) MFW_CASE(Z, 8)
       MFW_CASES(1)
       MFW_CASES(2)
@@ -339,7 +341,7 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
       MFW_CASES(4)
 #undef MFW_CASES
 #undef MFW_CASE
-      default: mfw_r_role<MF_ZMAX / 4, MF_HMAX / 4>(A, xa, trm, r, lane, total); break;
+      default: mfw_r_role<MFW_G, MF_ZMAX / 4, MF_HMAX / 4>(A, xa, trm, r, lane, total); break;
     }
     return;
   }
@@ -380,7 +382,9 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
 #pragma unroll
       for (int s = 0; s < S; s++) xa[(g * S + s) * MF_XSTR + i] = (unsigned char)quant_s8_state(st[g][s]);
     __syncthreads(); /* initial q(h_A) of every group */
-    bool fast[MFW_G] = {true, true, true};
+    bool fast[MFW_G];
+#pragma unroll
+    for (int g = 0; g < MFW_G; g++) fast[g] = true;
     MFW_STAMP_DECL;
     /* one group's gathers (nnet.c:484-491) and elementwise step (nnet.c:431-447) */
     auto step = [&](auto gc, int t, int p) {
@@ -437,15 +441,15 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
     using G0 = std::integral_constant<int, 0>;
     using G1 = std::integral_constant<int, 1>;
     using G2 = std::integral_constant<int, 2>;
-    for (int p = -1; p <= 3 * total; p++) {
+    for (int p = -1; p <= MFW_G * total; p++) {
       if (p >= 0) MFW_BAR(); /* phase p */
-      const int g = mod3(p), t = (p - g) / 3;
+      const int g = modg<MFW_G>(p), t = (p - g) / MFW_G;
       if (p < 0 || t >= total) continue;
       if (g == 0)
         step(G0{}, t, p);
-      else if (g == 1)
+      else if (MFW_G == 2 || g == 1)
         step(G1{}, t, p);
-      else
+      else if constexpr (MFW_G > 2)
         step(G2{}, t, p);
       if (t % A.N == A.N - 1 && t + 1 < total) {
         /* the next frame's conditioning of this group (its last elementwise
@@ -682,15 +686,15 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
   using G1 = std::integral_constant<int, 1>;
   using G2 = std::integral_constant<int, 2>;
   MFW_STAMP_DECL;
-  for (int p = -1; p <= 3 * total; p++) {
+  for (int p = -1; p <= MFW_G * total; p++) {
     if (p >= 0) MFW_BAR(); /* phase p */
-    const int g = mod3(p - 1), t = (p - 1 - g) / 3;
+    const int g = modg<MFW_G>(p - 1), t = (p - 1 - g) / MFW_G;
     if (p < 1 || t >= total) continue;
     if (g == 0)
       walk(G0{}, t);
-    else if (g == 1)
+    else if (MFW_G == 2 || g == 1)
       walk(G1{}, t);
-    else
+    else if constexpr (MFW_G > 2)
       walk(G2{}, t);
     const int n = t % A.N;
     if ((n & 15) == 15 || n == A.N - 1) flush(g, t / A.N, n & ~15, (n & 15) + 1);
@@ -716,13 +720,22 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
   }
 }
 
-int launch_mfw(const SampleArgs &a, void *stream)
+template <int G>
+static int launch_mfw_g(const SampleArgs &a, void *stream)
+{
+  using L = MfwLds<G>;
+  if (ensure_dyn_lds((const void *)mfw_kernel<true, G>, L::total)) return -1;
+  const int grid = (a.nstreams + L::MFW_GS - 1) / L::MFW_GS;
+  hipLaunchKernelGGL((mfw_kernel<true, G>), dim3(grid), dim3(MFW_THREADS), L::total, (hipStream_t)stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_mfw(const SampleArgs &a, int groups, void *stream)
 {
   if (!a.rcp_hw || a.mf_split || a.preload || a.trace_logits || a.stamps) return -1;
-  if (ensure_dyn_lds((const void *)mfw_kernel<true>, MfwLds::total)) return -1;
-  const int grid = (a.nstreams + MFW_GS - 1) / MFW_GS;
-  hipLaunchKernelGGL((mfw_kernel<true>), dim3(grid), dim3(MFW_THREADS), MfwLds::total, (hipStream_t)stream, a);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  if (groups == 2) return launch_mfw_g<2>(a, stream);
+  if (groups == 3) return launch_mfw_g<3>(a, stream);
+  return -1;
 }
 
 }  // namespace lpcnet_mi355x

@@ -137,11 +137,11 @@ def test_two_rank_engine_shard_invariance(require_gpu, world, per_rank, frames):
             ref = O.synth_stream(blob, L.synthetic_features(sid, frames)[:, :20], 0)
             assert np.array_equal(single[:, sid], ref), sid
     if per_rank >= 1024:
-        # the single-process 2048-stream run takes mf2_kernel (two staggered
-        # 4-stream groups per workgroup), each rank's 1024 streams mf_kernel<4>:
-        # two different kernels agree on every stream; one multi-frame launch
-        # of the timed frames
-        assert info.quad_path == 6 and info.streams_per_workgroup == 8
+        # the single-process 2048-stream run takes mfw_kernel (two 4-stream
+        # groups per workgroup, dedicated roles), each rank's 1024 streams
+        # mf_kernel<4>: two different kernels agree on every stream; one
+        # multi-frame launch of the timed frames
+        assert info.quad_path == 7 and info.streams_per_workgroup == 8
         assert kn == 1 and kf == frames - 2, (kn, kf)
         # and both agree with the CPU oracle on streams from each shard
         import oracle_lib as O

@@ -103,11 +103,13 @@ def test_large_batch_streams_match_oracle(require_gpu, blobs, B, check, kernel):
     assert np.abs(out[:, 2:]).mean() > 100
 
 
-def test_matrix_core_kernel_edge_cases_at_bench_size(require_gpu, blobs):
+def test_matrix_core_kernel_edge_cases_at_bench_size(require_gpu, blobs, monkeypatch):
     """mf_kernel at 4 streams per workgroup (1026 streams: ragged last
-    workgroup) through odd N, teacher forcing, a per-stream reset and the
-    per-sample trace (logits bit for bit, excitation), against the oracle on
-    streams of the first, a middle and the ragged workgroup; final GRU states."""
+    workgroup; LPCNET_MFW=0, the wide kernel would take this batch) through
+    odd N, teacher forcing, a per-stream reset and the per-sample trace
+    (logits bit for bit, excitation), against the oracle on streams of the
+    first, a middle and the ragged workgroup; final GRU states."""
+    monkeypatch.setenv("LPCNET_MFW", "0")
     B, F = 1026, 7
     blob = blobs["streams_int8"]
     allf = np.stack([feats(s, F) for s in range(B)], 1)
@@ -429,8 +431,8 @@ def test_restore_refuses_out_of_range_last_exc(require_gpu, blobs):
 
 def test_8192_streams_one_gpu_match_oracle(require_gpu, blobs):
     """BASELINE configs[4]'s total stream count on one GPU: LPCNetBatch(8192)
-    through the device-resident multi-frame path (mf2_kernel: 1024
-    workgroups of two staggered 4-stream groups, chunked frame network), against the
+    through the device-resident multi-frame path (mfw_kernel: 1024
+    workgroups of two 4-stream groups, chunked frame network), against the
     CPU oracle on two streams of every 1024-stream shard (PCM and final GRU
     states bit for bit), and shard 3 run alone as a 1024-stream batch gives
     the same PCM for its streams."""
@@ -438,7 +440,7 @@ def test_8192_streams_one_gpu_match_oracle(require_gpu, blobs):
     blob = blobs["streams_int8"]
     allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
     b = L.LPCNetBatch(B, 0, blob)
-    assert b.info().quad_path == 6 and b.info().streams_per_workgroup == 8  # mf2_kernel from 2048 streams
+    assert b.info().quad_path == 7 and b.info().streams_per_workgroup == 8  # mfw_kernel, two groups
     b.reset_timers(1)
     got = np.concatenate([_frames(b, allf, 0, 2), _frames(b, allf, 2, F)], 0)
     assert b.kernel_frames(0) == F and b.kernel_ms(0)[1] == 3  # 2 single-frame launches + one of 6
@@ -472,6 +474,7 @@ def test_mf2_kernel_equals_mf_kernel(require_gpu, blobs, monkeypatch, B):
     blob = blobs["streams_int8"]
     allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
     outs, states = [], []
+    monkeypatch.setenv("LPCNET_MFW", "0")  # mf2_kernel itself, not the wide kernel that replaces it
     for mf2 in ("0", "1"):
         monkeypatch.setenv("LPCNET_MF2", mf2)
         b = L.LPCNetBatch(B, 0, blob)
@@ -495,15 +498,18 @@ def test_mf2_kernel_equals_mf_kernel(require_gpu, blobs, monkeypatch, B):
     assert np.array_equal(outs[1][:, 0], np.stack(ref))
 
 
-def test_mf2_batch_falls_back_for_preload_and_trace(require_gpu, blobs, monkeypatch):
-    """A 2048-stream batch (mf2_kernel) takes mf_kernel for a teacher-forced
-    call and for a traced call: PCM, logits and excitation against the oracle."""
+@pytest.mark.parametrize("mfw", ["0", "1"])
+def test_mf2_batch_falls_back_for_preload_and_trace(require_gpu, blobs, monkeypatch, mfw):
+    """A 2048-stream batch (mf2_kernel, or the mfw_kernel that replaces it by
+    default) takes mf_kernel for a teacher-forced call and for a traced call:
+    PCM, logits and excitation against the oracle."""
     monkeypatch.delenv("LPCNET_MF2", raising=False)
+    monkeypatch.setenv("LPCNET_MFW", mfw)
     B, F = 2048, 5
     blob = blobs["streams_int8"]
     allf = np.stack([feats(s, F) for s in range(B)], 1)
     b = L.LPCNetBatch(B, 0, blob)
-    assert b.info().quad_path == 6
+    assert b.info().quad_path == (7 if mfw == "1" else 6)
     check = (0, 1500, 2047)
     refs = {s: O.Oracle(blob, 0) for s in check}
     t = np.arange(160)
@@ -596,8 +602,8 @@ def test_chunked_frame_network_equals_per_frame(require_gpu, blobs, B, name):
     assert not bad, bad[:8]
 
 
-@pytest.mark.parametrize("B", [1, 2, 70, 256, 1030])
-def test_multi_frame_sample_launches_match_per_frame(require_gpu, blobs, monkeypatch, B):
+@pytest.mark.parametrize("B,mfw", [(1, "0"), (2, "0"), (70, "0"), (256, "0"), (1030, "0"), (1030, "1"), (2100, "1")])
+def test_multi_frame_sample_launches_match_per_frame(require_gpu, blobs, monkeypatch, B, mfw):
     """lpcnet_batch_synthesize_frames on the matrix-core kernel launches the
     sample kernel once per chunk of frames (SampleArgs::nframes), carrying the
     states in registers across frames.  Against the per-frame launches
@@ -605,7 +611,9 @@ def test_multi_frame_sample_launches_match_per_frame(require_gpu, blobs, monkeyp
     frames go to single-frame launches), follow a per-stream reset and a
     state restore mid-run, and span chunk boundaries: the PCM and the complete
     stream state byte for byte, every stream; stream 0 also against the
-    oracle.  The timers count one launch per multi-frame run."""
+    oracle.  The timers count one launch per multi-frame run.  mfw = 1: the
+    same on the wide kernel (two groups per workgroup at 1030 and 2100)."""
+    monkeypatch.setenv("LPCNET_MFW", mfw)
     F = 44
     blob = blobs["streams_int8"]
     allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
@@ -617,7 +625,7 @@ def test_multi_frame_sample_launches_match_per_frame(require_gpu, blobs, monkeyp
         else:
             monkeypatch.setenv("LPCNET_NO_MULTIFRAME", "1")
         b = L.LPCNetBatch(B, 0, blob)
-        assert b.info().quad_path == 4
+        assert b.info().quad_path == (7 if mfw == "1" else 4)
         parts = []
         for i, (f0, f1) in enumerate(runs):
             if i == 1:
@@ -768,19 +776,22 @@ def test_live_single_frame_chunked_matches_oracle(require_gpu, monkeypatch, vari
         assert np.array_equal(got[s], np.stack([o.synthesize(allf[f, s]) for f in range(F)])), s
 
 
-@pytest.mark.parametrize("B,F", [(12, 5), (3073, 4), (4096, 6)])
-def test_wide_kernel_matches_oracle(require_gpu, monkeypatch, B, F):
-    """mfw_kernel (three 4-stream groups per workgroup, dedicated gather /
-    recurrent / sampler waves): every stream equals mf2_kernel's (LPCNET_MFW=0)
-    and sampled streams equal the oracle -- one workgroup (12 streams, forced
-    with LPCNET_MFW=1), a ragged last workgroup (3073), multi-frame launches
-    through the device-resident path (4096) and the host-I/O path (both)."""
+@pytest.mark.parametrize("groups,B,F", [(3, 12, 5), (3, 3073, 4), (3, 4096, 6), (2, 8, 5), (2, 2049, 4),
+                                        (2, 4096, 6)])
+def test_wide_kernel_matches_oracle(require_gpu, monkeypatch, groups, B, F):
+    """mfw_kernel (two or three 4-stream groups per workgroup, dedicated
+    gather / recurrent / sampler waves): every stream equals mf2_kernel's
+    (LPCNET_MFW=0) and sampled streams equal the oracle -- one workgroup (12
+    or 8 streams, forced with LPCNET_MFW=1), a ragged last workgroup (3073,
+    2049), multi-frame launches through the device-resident path (4096) and
+    the host-I/O path (all)."""
     blob = L.synthetic_model(1, 0)
     allf = np.stack([feats(s, F) for s in range(B)], 1)
     monkeypatch.setenv("LPCNET_MF2", "1")
     monkeypatch.setenv("LPCNET_MFW", "1")
+    monkeypatch.setenv("LPCNET_MFW_G", str(groups))
     b = L.LPCNetBatch(B, 0, blob)
-    assert b.info().quad_path == 7 and b.info().kernel_name == "mfw_kernel<true>"
+    assert b.info().quad_path == 7 and b.info().kernel_name == f"mfw_kernel<true, {groups}>"
     got = np.stack([b.synthesize(allf[f]) for f in range(F)], 1)
     b.reset()
     d_f = b.device_alloc(allf.nbytes)
@@ -800,7 +811,7 @@ def test_wide_kernel_matches_oracle(require_gpu, monkeypatch, B, F):
     ref = np.stack([b2.synthesize(allf[f]) for f in range(F)], 1)
     b2.close()
     assert np.array_equal(got, ref)
-    for s in sorted({0, 5, 11, B // 2, B - 1}):
+    for s in sorted(x for x in {0, 5, 11, B // 2, B - 1} if x < B):
         o = O.Oracle(blob, 0)
         assert np.array_equal(got[s], np.stack([o.synthesize(allf[f, s]) for f in range(F)])), s
 
