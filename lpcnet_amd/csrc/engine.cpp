@@ -324,6 +324,8 @@ struct LPCNetBatch {
   bool mf2 = false;      /* large batches: mf2_kernel (two staggered 4-stream groups per workgroup) for
                             launches without preload / trace / stamps */
   int mfw_g = 3;         /* mfw_kernel's four-stream groups per workgroup (2 or 3) */
+  bool mfw_forced = false; /* LPCNET_MFW=1: mfw_kernel for every launch, however narrow */
+  int cus = 256;           /* compute units of the batch's device */
   bool mfw = false;      /* wider batches: mfw_kernel (three 4-stream groups, dedicated gather /
                             recurrent / sampler waves) for the same launches, non-split models with the
                             default rcpps */
@@ -454,6 +456,13 @@ int mfw_groups(int B, int cus)
   return c3 < c2 ? 3 : 2;
 }
 
+/* Per launch: a batch that runs mfw_kernel gives its launches of at most
+ * one mf_kernel<4> round (nB <= 4 streams per CU: a drop-in pool's work
+ * batch is sized for its widest launch, a partial step of a batch) to
+ * mf_kernel, whose one-group sample is the shorter chain there. */
+static bool wide_for(const LPCNetBatch *b, int nB) { return b->mfw && (b->mfw_forced || nB > 4 * b->cus); }
+static bool mf2_for(const LPCNetBatch *b, int nB) { return b->mf2 && (!b->mfw || wide_for(b, nB)); }
+
 /* Sample-kernel choice (mode 0 = automatic):
  *   5  fp_kernel  -- fp32 models with a dense GRU_B within the FP_* limits
  *   4  mf_kernel  -- non-saturating int8 models within the MF_* limits
@@ -492,10 +501,12 @@ void choose_kernel(LPCNetBatch *b)
      * round, mfw_kernel (two or three groups with dedicated roles) where the
      * model allows it (LPCNET_MFW=0/1 off / on wherever mf2 runs,
      * LPCNET_MFW_G=2/3 forces the group count) */
-    const int gauto = mfw_groups(b->B, current_device_cus());
+    b->cus = current_device_cus();
+    const int gauto = mfw_groups(b->B, b->cus);
     const bool mfw_ok = !b->sa.mf_split && b->sa.rcp_hw;
     const char *ew = getenv("LPCNET_MFW");
     const bool wantw = ew ? atoi(ew) != 0 : gauto > 0;
+    b->mfw_forced = ew && atoi(ew) != 0;
     const char *e2 = getenv("LPCNET_MF2");
     const bool want2 = e2 ? atoi(e2) != 0 : b->B >= MF2_MIN_STREAMS || (wantw && mfw_ok);
     if (want2 && mf2_lds_bytes(4, b->sa.mf_split) <= 160 * 1024) {
@@ -1809,8 +1820,8 @@ int launch_frame_step(LPCNetBatch *b, const float *d_features, float *d_lpc_fram
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   const int lrc = N <= 0 ? 0
                 : b->fp    ? launch_fp(sa, b->stream)
-                : b->mfw && !sa.preload && !sa.trace_logits && !sa.stamps ? launch_mfw(sa, b->mfw_g, b->stream)
-                : b->mf2 && !sa.preload && !sa.trace_logits && !sa.stamps ? launch_mf2(sa, 4, b->stream)
+                : wide_for(b, sa.nstreams) && !sa.preload && !sa.trace_logits && !sa.stamps ? launch_mfw(sa, b->mfw_g, b->stream)
+                : mf2_for(b, sa.nstreams) && !sa.preload && !sa.trace_logits && !sa.stamps ? launch_mf2(sa, 4, b->stream)
                 : b->mf    ? launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream)
                              : launch_sample(sa, b->S, b->variant, b->sat ? 1 : 0, b->reg ? 1 : 0, b->lds_bytes, b->stream);
   if (lrc) {
@@ -1873,8 +1884,8 @@ int launch_chunk_samples(LPCNetBatch *b, int f, short *d_pcm, int N, int nfr = 1
   }
   const int lrc = N <= 0                                  ? 0
                   : b->fp                                 ? launch_fp(sa, b->stream)
-                  : b->mfw && !sa.trace_logits && !sa.stamps ? launch_mfw(sa, b->mfw_g, b->stream)
-                  : b->mf2 && !sa.trace_logits && !sa.stamps ? launch_mf2(sa, 4, b->stream)
+                  : wide_for(b, sa.nstreams) && !sa.trace_logits && !sa.stamps ? launch_mfw(sa, b->mfw_g, b->stream)
+                  : mf2_for(b, sa.nstreams) && !sa.trace_logits && !sa.stamps ? launch_mf2(sa, 4, b->stream)
                                                           : launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream);
   if (lrc) {
     set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -2212,8 +2223,8 @@ static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_fe
   sa.spin_limit = b->spin_limit;
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   const int lrc = b->fp ? launch_fp(sa, b->stream)
-                  : b->mfw ? launch_mfw(sa, b->mfw_g, b->stream)
-                  : b->mf2 ? launch_mf2(sa, 4, b->stream)
+                  : wide_for(b, nB) ? launch_mfw(sa, b->mfw_g, b->stream)
+                  : mf2_for(b, nB) ? launch_mf2(sa, 4, b->stream)
                            : launch_mf(sa, b->S, mf_lds_bytes(b->S, b->sa.mf_split), b->stream);
   if (lrc) {
     set_err(std::string("sample kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -2283,7 +2294,7 @@ static int tick_sync(LPCNetBatch *b)
  * transaction each), so its PCM goes through device memory and one copy. */
 static bool pcm_store_coalesced(const LPCNetBatch *b)
 {
-  return !getenv("LPCNET_NO_DIRECT_PCM") && (b->fp || b->mfw || (b->mf && !b->mf2));
+  return !getenv("LPCNET_NO_DIRECT_PCM") && (b->fp || b->mfw || (b->mf && !b->mf2));  /* mfw batches: mfw or mf_kernel */
 }
 
 /* one frame for the first nB streams of a batch, host I/O ([nB][NF] in,

@@ -142,6 +142,18 @@ __device__ __forceinline__ uint32_t mfw_x(const unsigned char *xg, const uint32_
 #ifndef MFW_XD
 #define MFW_XD 1
 #endif
+/* issue priority of the R waves (s_setprio; the S waves run at 3) */
+#ifndef MFW_R_PRIO
+#define MFW_R_PRIO 0
+#endif
+/* issue priority of the S waves */
+#ifndef MFW_S_PRIO
+#define MFW_S_PRIO 3
+#endif
+/* issue priority of the E waves */
+#ifndef MFW_E_PRIO
+#define MFW_E_PRIO 0
+#endif
 
 /* one gate's product over NG 4-slot groups, NC accumulators (slot k -> k %
  * NC; exact int32, any split), the x words of group g + MFW_XD read while
@@ -232,6 +244,11 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
   const int row = r * 64 + lane;
   __syncthreads(); /* image in LDS */
   __syncthreads(); /* initial q(h_A) of every group */
+#if MFW_R_PRIO > 0
+  /* the R waves' few VALU ops (x addresses) ahead of the E waves' stream on
+   * the shared SIMDs: the MFMAs then run beside the elementwise step */
+  __builtin_amdgcn_s_setprio(MFW_R_PRIO);
+#endif
   MFW_STAMP_DECL;
   /* group (p - (G - 1)) mod G: three groups, the group E left two phases
    * ago (S walks it in between); two groups, the group S walks beside */
@@ -382,6 +399,9 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
 #pragma unroll
       for (int s = 0; s < S; s++) xa[(g * S + s) * MF_XSTR + i] = (unsigned char)quant_s8_state(st[g][s]);
     __syncthreads(); /* initial q(h_A) of every group */
+#if MFW_E_PRIO > 0
+    __builtin_amdgcn_s_setprio(MFW_E_PRIO);
+#endif
     bool fast[MFW_G];
 #pragma unroll
     for (int g = 0; g < MFW_G; g++) fast[g] = true;
@@ -540,7 +560,7 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
 #pragma unroll
   for (int g = 0; g < MFW_G; g++) restart(g);
   __syncthreads(); /* initial */
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MFW_S_PRIO);
 
   MFW_SEC_DECL;
   /* group g's GRU_B step and walk of sample t (lpcnet.c:244-270) */
