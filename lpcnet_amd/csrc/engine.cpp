@@ -2264,24 +2264,30 @@ static int ensure_host_io(LPCNetBatch *b)
   return 0;
 }
 
-/* the end of a host-I/O tick: the calling thread polls the tick's event
- * (no sleep/wake-up between the last kernel and the caller's next frame),
- * handing over to a blocking wait after TICK_SPIN_MS.  LPCNET_SYNC_BLOCK=1:
- * hipStreamSynchronize. */
-static int tick_sync(LPCNetBatch *b)
+/* the end of a synchronous call.  poll: the calling thread polls the
+ * call's event (no sleep / wake-up between the last kernel and the thread's
+ * next step), handing over to a blocking wait after TICK_SPIN_MS -- the
+ * drop-in pool's combiner (64 C threads: 19-20 -> 27.5 M samples/s, 256:
+ * 58-60 -> 69-84 M); otherwise hipStreamSynchronize, 2-3 % faster for one
+ * caller driving a batch (tools/sync_ab.sh, profiles/r05/sync_ab.log).
+ * LPCNET_SYNC_BLOCK=1 / LPCNET_SYNC_POLL=1 force one form everywhere. */
+static int tick_sync(LPCNetBatch *b, bool poll)
 {
-  if (getenv("LPCNET_SYNC_BLOCK")) {
+  if (getenv("LPCNET_SYNC_POLL")) poll = true;
+  if (!poll || getenv("LPCNET_SYNC_BLOCK")) {
     HIPCHK(hipStreamSynchronize(b->stream));
     return 0;
   }
   if (!b->ev_tick) HIPCHK(hipEventCreateWithFlags(&b->ev_tick, hipEventDisableTiming));
   HIPCHK(hipEventRecord(b->ev_tick, b->stream));
+  static const int pause = getenv("LPCNET_SYNC_PAUSE") ? atoi(getenv("LPCNET_SYNC_PAUSE")) : TICK_POLL_PAUSE;
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t q = hipEventQuery(b->ev_tick);
     if (q == hipSuccess) return 0;
     if (q != hipErrorNotReady) HIPCHK(q);
     if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(TICK_SPIN_MS)) break;
+    for (int k = 0; k < pause; k++) __builtin_ia32_pause(); /* fewer runtime queries */
   }
   HIPCHK(hipEventSynchronize(b->ev_tick));
   return 0;
@@ -2331,7 +2337,7 @@ static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm
     if (!direct)
       HIPCHK(hipMemcpyAsync(own_pcm ? b->h_io_pcm : b->h_stg_pcm, b->d_pcm, sizeof(short) * N * nB,
                             hipMemcpyDeviceToHost, b->stream));
-    if (tick_sync(b)) return -1;
+    if (tick_sync(b, false)) return -1;
     if (check_status(b)) return -1;
     if (!own_pcm) memcpy(pcm, b->h_stg_pcm, sizeof(short) * N * nB);
     return 0;
@@ -2346,7 +2352,7 @@ static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm
   if (launch_frame_step(b, b->d_feat, b->d_lpc, true, b->d_pcm, N, preload, -1, nB)) return -1;
   if (pre && pre()) return -1;
   if (N > 0) HIPCHK(hipMemcpyAsync(pcm, b->d_pcm, sizeof(short) * N * nB, hipMemcpyDeviceToHost, b->stream));
-  HIPCHK(hipStreamSynchronize(b->stream));
+  if (tick_sync(b, pre || staged)) return -1;
   return check_status(b);
 }
 

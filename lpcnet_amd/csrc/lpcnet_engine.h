@@ -121,6 +121,7 @@ constexpr int IMG_VAR = IMG_FCF + 512 * 4;       /* start of the variable sectio
  * and frame_count after this frame's update. */
 constexpr int ZC_FEAT_MAX = 4096; /* host-I/O ticks up to this size read the features from mapped host memory */
 constexpr int TICK_SPIN_MS = 20;  /* a host-I/O tick polls its end this long before a blocking wait */
+constexpr int TICK_POLL_PAUSE = 0; /* x86 pause instructions between two polls */
 constexpr int OVERLAP_MAX_STREAMS = 128; /* batches up to this size get the overlapped multi-frame path (sample + frame workgroups fit the 256 CUs) */
 
 struct alignas(16) FrameCond {
