@@ -41,7 +41,13 @@ namespace lpcnet_mi355x {
 
 constexpr int FP_SLOTS = NA / 4 + 1; /* column quads of the GRU_A state + one +0 quad (padding) */
 constexpr int FP_HD = 8;             /* h-gate weight blocks in flight per lane */
-constexpr int FP_XD = 3;             /* GRU_A state quads in flight per chain (LDS) */
+#ifndef FP_XD_N
+#define FP_XD_N 8
+#endif
+/* GRU_A state quads in flight per chain (LDS): the z/r chains' x reads at
+ * 8 slots ahead instead of 3, batch-1 fp32 sample kernel -2.2 % (5, 12, 16:
+ * -1.2 %, +2.6 %, +29 %; same box, three alternating rounds, r05) */
+constexpr int FP_XD = FP_XD_N;
 #ifndef FP_SAMPLER_HW
 #define FP_SAMPLER_HW 3
 #endif
@@ -57,7 +63,10 @@ __device__ __forceinline__ int fp_gru_a_wave(int hw)
   if (FP_SAMPLER_HW == 3) return hw < 3 ? hw : 9 - hw;
   return hw == 3 ? 0 : (hw < 3 ? hw : 9 - hw);
 }
-constexpr int GB_RING = 8;           /* GRU_B column quads in flight (LDS) */
+#ifndef FP_GB_RING
+#define FP_GB_RING 8
+#endif
+constexpr int GB_RING = FP_GB_RING;  /* GRU_B column quads in flight (LDS) */
 
 struct FpLds {
   static constexpr int xs = 2 * FP_SLOTS * 16;        /* fp32 GRU_A state, [2][FP_SLOTS] float4 */
