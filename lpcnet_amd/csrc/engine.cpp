@@ -838,12 +838,15 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
  * cycles per MFMA of a wave pair): those SIMDs weighted 3.3x and a longer
  * search (same box, 1024 streams: -0.6 to -1.1 % frame step).  2:
  * mf2_kernel (from 2048 streams), whose samplers idle half of each phase:
- * 2.0x (2048 streams -2.1 %, 8192 -0.7 %).  0: 2.7x, one and two streams
- * per workgroup. */
+ * 2.0x (2048 streams -2.1 %, 8192 -0.7 %).  3: mfw_kernel (its R waves
+ * on SIMDs 2/3 share them with a sampler and an E wave): 2.5x (8192 and
+ * 24,576 streams -1.0 / -0.8 % against 2.0x; 1.0, 1.4, 1.7, 2.3, 2.8, 3.3x
+ * measured, profiles/r05/simdw_ab*.log).  0: 2.7x, one and two streams per
+ * workgroup.  Split plans: 3.3x on mf_kernel<4>, 2.7x otherwise. */
 bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, int cls = 0)
 {
   const bool S4 = cls == 1;
-  const int w_unsplit = cls == 1 ? 33 : cls == 2 ? 20 : MF_SAMPLER_SIMD_WEIGHT;
+  const int w_unsplit = cls == 1 ? 33 : cls == 2 ? 20 : cls == 3 ? 25 : MF_SAMPLER_SIMD_WEIGHT;
   constexpr int NUB = NA / 8;
   int kmax[3] = {0, 0, 0};
   for (int g = 0; g < 3; g++)
@@ -857,7 +860,7 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, int cls = 0)
   /* split plans weight the sampler SIMDs 3.3x on mf_kernel (1-4 streams per
    * workgroup: measured best plans at 256 and 1024 streams) and 2.7x on
    * mf2_kernel (best at 8192) */
-  const int w_split = cls == 2 ? MF_SAMPLER_SIMD_WEIGHT : 33;
+  const int w_split = cls >= 2 ? MF_SAMPLER_SIMD_WEIGHT : 33;
   /* split: every own cap / piece size pair, screened with a short
    * assignment search, the best re-laid-out in full (LPCNET_MF_FORCE_SPLIT:
    * split even a model that fits -- pieces required -- for tests) */
@@ -1226,7 +1229,14 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     if (std::adjacent_find(pos.begin(), pos.end()) != pos.end()) mf_ok = false;
   }
   MfPlan plan;
-  if (mf_ok) mf_ok = mf_plan(ga_blocks, plan, b->B >= MF2_MIN_STREAMS ? 2 : b->B >= 1024 ? 1 : 0);
+  if (mf_ok) {
+    /* the plan's SIMD weights follow the kernel the batch will run (see
+     * mf_plan): the wide kernel above one mf_kernel<4> round unless turned
+     * off */
+    const char *ew = getenv("LPCNET_MFW");
+    const bool wide = mfw_groups(b->B, current_device_cus()) > 0 && !(ew && atoi(ew) == 0);
+    mf_ok = mf_plan(ga_blocks, plan, wide ? 3 : b->B >= MF2_MIN_STREAMS ? 2 : b->B >= 1024 ? 1 : 0);
+  }
   if (getenv("LPCNET_VERBOSE")) {
     fprintf(stderr, "lpcnet: mf_kernel plan: %s", !mf_ok ? "not applicable" : plan.split ? "split" : "unsplit");
     if (mf_ok) {
