@@ -75,8 +75,12 @@ struct MfwLds {
 /* the image sections without the rcpps table: u-law, logit, dual_fc */
 constexpr int MFW_IMG = IMG_VAR - IMG_ULAW;
 static_assert(MfwLds<3>::total + MFW_IMG <= 160 * 1024, "mfw_kernel LDS");
+/* two groups leave room for the rcpps table too: the E waves' activations
+ * read it (the VALU-cheaper form mf_kernel<4> / mf2_kernel use at 4
+ * streams per lane) instead of the hardware reciprocal */
+static_assert(MfwLds<2>::total + IMG_VAR <= 160 * 1024, "mfw_kernel LDS (two groups, table)");
 
-int mfw_lds_bytes(int groups) { return (groups == 2 ? MfwLds<2>::total : MfwLds<3>::total) + MFW_IMG; }
+int mfw_lds_bytes(int groups) { return groups == 2 ? MfwLds<2>::total + IMG_VAR : MfwLds<3>::total + MFW_IMG; }
 
 template <int G>
 __device__ __forceinline__ int modg(int p) { return (p % G + G) % G; }
@@ -145,6 +149,11 @@ __device__ __forceinline__ uint32_t mfw_x(const unsigned char *xg, const uint32_
 /* issue priority of the R waves (s_setprio; the S waves run at 3) */
 #ifndef MFW_R_PRIO
 #define MFW_R_PRIO 0
+#endif
+/* two groups: the E waves' activations through the LDS rcpps table (1) or
+ * the hardware reciprocal (0) */
+#ifndef MFW_TAB
+#define MFW_TAB 1
 #endif
 /* issue priority of the S waves */
 #ifndef MFW_S_PRIO
@@ -282,6 +291,8 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
 template <bool HWR, int MFW_G>
 __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
 {
+  /* the rcpps table in LDS for the E waves (two groups; see mfw_lds_bytes) */
+  constexpr bool TAB = MFW_G == 2 && MFW_TAB;
   static_assert(HWR, "mfw_kernel: hardware reciprocal only (no rcpps table in LDS)");
   static_assert(MFW_G == 2 || MFW_G == 3, "two or three groups");
   extern __shared__ uint4 lds4[];
@@ -303,9 +314,11 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
   v4i *gbw = (v4i *)(okw + 2 * MFW_G * 8);
   uint32_t *sst = (uint32_t *)(gbw + MF_GB_TILES * 64);
   short *pcms = (short *)(sst + MFW_GS * 8);
-  __shared__ uint4 img_s[MFW_IMG / 16];
-  const unsigned char *img = (const unsigned char *)img_s - IMG_ULAW; /* section offsets as in the full image */
-  const float *ulaw = (const float *)((const unsigned char *)img_s);
+  constexpr int IMG0 = TAB ? 0 : IMG_ULAW; /* first image byte held in LDS */
+  __shared__ uint4 img_s[(IMG_VAR - IMG0) / 16];
+  const unsigned char *img = (const unsigned char *)img_s - IMG0; /* section offsets as in the full image */
+  const float *ulaw = (const float *)(img + IMG_ULAW);
+  const uint32_t *rcpt = TAB ? (const uint32_t *)(img + IMG_RCP) : nullptr;
   const float *logit_tab = ulaw + 256;
   const float *fcw = logit_tab + 256;
   const float *fcb = fcw + 256 * 32;
@@ -343,7 +356,7 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
     }
     return;
   }
-  for (int o = tid; o < MFW_IMG / 16; o += MFW_THREADS) img_s[o] = A.image[IMG_ULAW / 16 + o];
+  for (int o = tid; o < (IMG_VAR - IMG0) / 16; o += MFW_THREADS) img_s[o] = A.image[IMG0 / 16 + o];
 
   if (wv >= MFW_R_WAVE0) {
     /* ======================= R role ====================================== */
@@ -454,9 +467,9 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
       auto nostamp = [&](int) { (void)stub; };
       const float *cg = cnd + g * GA_ROWS * S;
       if (__builtin_amdgcn_readfirstlane((int)fast[g]))
-        ga_elementwise<S, true, true>(st[g], e, cg, tid, az, ar, tz, tr, hpre, nullptr, xa + g * S * MF_XSTR + i, false, nostamp);
+        ga_elementwise<S, true, !TAB>(st[g], e, cg, tid, az, ar, tz, tr, hpre, rcpt, xa + g * S * MF_XSTR + i, false, nostamp);
       else
-        ga_elementwise<S, false, true>(st[g], e, cg, tid, az, ar, tz, tr, hpre, nullptr, xa + g * S * MF_XSTR + i, false, nostamp);
+        ga_elementwise<S, false, !TAB>(st[g], e, cg, tid, az, ar, tz, tr, hpre, rcpt, xa + g * S * MF_XSTR + i, false, nostamp);
     };
     using G0 = std::integral_constant<int, 0>;
     using G1 = std::integral_constant<int, 1>;
