@@ -345,7 +345,7 @@ int launch_mf2(const SampleArgs &a, int S, void *stream);
  * three groups are taken where their 12-stream rounds save more than the 4 %
  * (3,072 streams: one round against two).  Above 4 streams per CU only:
  * below, mf_kernel's one-group latency wins. */
-constexpr double MFW_G3_PHASE = 1.04;
+constexpr double MFW_G3_PHASE = 1.08; /* 1.04 before two groups took the LDS rcpps table (-3.4 %) */
 /* 0 (batch within one mf_kernel<4> round), 2 or 3 */
 int mfw_groups(int B, int cus);
 int mfw_lds_bytes(int groups);
