@@ -843,8 +843,9 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
  * 24,576 streams -1.0 / -0.8 % against 2.0x; 1.0, 1.4, 1.7, 2.3, 2.8, 3.3x
  * measured, profiles/r05/simdw_ab*.log).  0: 2.7x, one and two streams per
  * workgroup.  Split plans: 3.3x on mf_kernel<4>, 2.7x otherwise. */
-bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, int cls = 0)
+bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, int cls = 0, int cls_split = -1)
 {
+  if (cls_split < 0) cls_split = cls;
   const bool S4 = cls == 1;
   const int w_unsplit = cls == 1 ? 33 : cls == 2 ? 20 : cls == 3 ? 25 : MF_SAMPLER_SIMD_WEIGHT;
   constexpr int NUB = NA / 8;
@@ -858,9 +859,10 @@ bool mf_plan(const std::vector<std::vector<int>> &ga, MfPlan &P, int cls = 0)
     return mf_layout(ga, P, T, F, S4 ? 400000 : 40000, w_unsplit) >= 0;
   }
   /* split plans weight the sampler SIMDs 3.3x on mf_kernel (1-4 streams per
-   * workgroup: measured best plans at 256 and 1024 streams) and 2.7x on
-   * mf2_kernel (best at 8192) */
-  const int w_split = cls >= 2 ? MF_SAMPLER_SIMD_WEIGHT : 33;
+   * workgroup: measured best plans at 256 and 1024 streams) and 2.0x on
+   * mf2_kernel (skewed model, 8192 / 2048 streams -3.3 / -1.2 % against
+   * 2.7x; 1.5, 1.7, 2.2, 2.4, 3.3x measured, profiles/r05/simdw_skew*.log) */
+  const int w_split = cls_split == 2 ? 20 : 33;
   /* split: every own cap / piece size pair, screened with a short
    * assignment search, the best re-laid-out in full (LPCNET_MF_FORCE_SPLIT:
    * split even a model that fits -- pieces required -- for tests) */
@@ -1235,7 +1237,9 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
      * off */
     const char *ew = getenv("LPCNET_MFW");
     const bool wide = mfw_groups(b->B, current_device_cus()) > 0 && !(ew && atoi(ew) == 0);
-    mf_ok = mf_plan(ga_blocks, plan, wide ? 3 : b->B >= MF2_MIN_STREAMS ? 2 : b->B >= 1024 ? 1 : 0);
+    const int cls = b->B >= MF2_MIN_STREAMS ? 2 : b->B >= 1024 ? 1 : 0;
+    /* split plans never run the wide kernel */
+    mf_ok = mf_plan(ga_blocks, plan, wide ? 3 : cls, cls);
   }
   if (getenv("LPCNET_VERBOSE")) {
     fprintf(stderr, "lpcnet: mf_kernel plan: %s", !mf_ok ? "not applicable" : plan.split ? "split" : "unsplit");
