@@ -87,7 +87,11 @@ __device__ __forceinline__ int modg(int p) { return (p % G + G) % G; }
 
 /* keeps the next group's / K tile's LDS reads ahead of the current MFMAs
  * (the scheduler otherwise sinks them to their use) */
+#ifdef MFW_NOFENCE
+#define MFW_FENCE() do { } while (0)
+#else
 #define MFW_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
 
 /* diagnostics (MFW_STAMPS builds only, tools/ab_build.sh): per wave of
  * workgroup 0, the s_memtime cycles spent working vs waiting at the phase
