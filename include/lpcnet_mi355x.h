@@ -40,8 +40,10 @@ typedef struct {
                                      LDS layout), 4 mf_kernel (matrix cores), 5 fp_kernel (fp32),
                                      6 mf2_kernel (matrix cores, two staggered 4-stream groups per
                                      workgroup; batches >= 2048; launches with preload or trace
-                                     take mf_kernel), 7 mfw_kernel (three 4-stream groups with dedicated
-                                     gather/elementwise, recurrent and sampler waves; batches >= 3072,
+                                     take mf_kernel), 7 mfw_kernel (two or three 4-stream groups per
+                                     workgroup, chosen by cost -- two in the common case -- with dedicated
+                                     gather/elementwise, recurrent and sampler waves; batches above one
+                                     mf_kernel<4> round (> 4 streams per CU, i.e. > 1024 streams),
                                      non-split models, default rcpps; the same launches as 6) */
   int lds_bytes;                  /* dynamic LDS of the sample kernel */
   double mfma_ops_per_group_sample; /* int8 matrix-core ops issued per workgroup per sample
@@ -285,13 +287,18 @@ LPCNET_EXPORT int lpcnet_mi355x_device_count(void);
  * bound.  -1 if st is not bound. */
 LPCNET_EXPORT int lpcnet_mi355x_pool_stats(const LPCNetState *st, long *launches, long *requests, int *streams);
 /* Placement of drop-in handles (lpcnet_init / lpcnet_create /
- * lpcnet_decoder_init take no device, lpcnet.c:184-219): each new handle
- * goes to the placement with the fewest live handles, over every visible
- * device by default or over `devices[0..n)` (env LPCNET_DEVICES="0,1,...";
- * a device may appear twice: two placements, two pools on one GPU).  Live
- * handles keep their device; handles initialised afterwards are placed over
- * the new list; n = 0 restores the default.  LPCNET_DEVICE=d pins every new
- * handle to device d instead.  0 / -1. */
+ * lpcnet_decoder_init take no device, lpcnet.c:184-219).  Default: every
+ * handle on one device -- LOCAL_RANK mod the visible devices when LOCAL_RANK
+ * is set (one process per GPU), device 0 otherwise -- resolved at the first
+ * lpcnet_load_model, so creating handles never starts the HIP runtime.
+ * Spreading is opt-in: over `devices[0..n)` here, or over env
+ * LPCNET_DEVICES="0,1,..." / "all" (checked against the visible devices at
+ * the first lpcnet_init: a bad list fails it), each new handle goes to the
+ * placement with the fewest live handles (a device may appear twice: two
+ * placements, two pools on one GPU).  Live handles keep their device;
+ * handles initialised afterwards are placed over the new list; n = 0
+ * restores the default.  LPCNET_DEVICE=d pins every new handle to device d
+ * instead.  0 / -1. */
 LPCNET_EXPORT int lpcnet_mi355x_set_placement(const int *devices, int n);
 /* The device and placement index (-1: pinned by LPCNET_DEVICE) of handle st. */
 LPCNET_EXPORT int lpcnet_mi355x_handle_placement(const LPCNetState *st, int *device, int *placement);

@@ -370,6 +370,28 @@ class LPCNetDecoder:
             pass
 
 
+class _BatchOwner:
+    """Owns the native batch: lpcnet_batch_destroy runs when the last
+    reference goes -- the LPCNetBatch (until close()) or an array handed out
+    by host_features() / synthesize_host(), whose buffer object holds this
+    owner, so such an array never outlives the pinned memory it views."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __del__(self):
+        if self.ptr:
+            lib.lpcnet_batch_destroy(self.ptr)
+            self.ptr = None
+
+
+def _owned_view(owner: _BatchOwner, addr: int, ctype, dtype, shape) -> np.ndarray:
+    n = int(np.prod(shape))
+    buf = (ctype * n).from_address(addr)
+    buf._owner = owner  # the array's base keeps the native batch alive
+    return np.frombuffer(buf, dtype=dtype).reshape(shape)
+
+
 class LPCNetBatch:
     """B independent streams on one MI355X (include/lpcnet_mi355x.h)."""
 
@@ -377,6 +399,7 @@ class LPCNetBatch:
         self._b = lib.lpcnet_batch_create(nb_streams, device)
         if not self._b:
             raise LPCNetError(f"lpcnet_batch_create failed: {last_error()}")
+        self._owner = _BatchOwner(self._b)
         self.B = nb_streams
         if blob is not None:
             self.load_model(blob)
@@ -445,18 +468,20 @@ class LPCNetBatch:
             p = lib.lpcnet_batch_host_features(self._b)
             if not p:
                 raise LPCNetError(last_error())
-            self._hf = np.ctypeslib.as_array(p, shape=(self.B, NB_FEATURES))
+            self._hf = _owned_view(self._owner, C.cast(p, C.c_void_p).value, C.c_float, np.float32, (self.B, NB_FEATURES))
             q = lib.lpcnet_batch_host_pcm(self._b)
             if not q:
                 raise LPCNetError(last_error())
-            self._hp = np.ctypeslib.as_array(q, shape=(self.B * FRAME_SIZE,))
+            self._hp = _owned_view(self._owner, C.cast(q, C.c_void_p).value, C.c_int16, np.int16, (self.B * FRAME_SIZE,))
         return self._hf
 
     def synthesize_host(self, n: int = FRAME_SIZE) -> np.ndarray:
         """One frame from host_features() into the batch's pinned PCM buffer
         (lpcnet_batch_synthesize on the batch's own buffers: no host staging
         copies; the sample kernel stores the PCM there itself where it can).
-        Returns a [B, n] view of that buffer, valid until the next call."""
+        Returns a [B, n] view of that buffer, overwritten by the next call
+        (copy it to keep it); the view keeps the batch's pinned memory alive
+        past close()."""
         f = self.host_features()
         pcm = self._hp[:self.B * n]
         if lib.lpcnet_batch_synthesize(self._b, f.ctypes.data, pcm.ctypes.data, n) != 0:
@@ -608,10 +633,12 @@ class LPCNetBatch:
                 "frame_count": fc.value}
 
     def close(self) -> None:
+        """Release the batch: destroyed now, or when the last array handed
+        out by host_features() / synthesize_host() goes."""
         if self._b:
-            self._hf = self._hp = None  # views of the batch's pinned buffers die with it
-            lib.lpcnet_batch_destroy(self._b)
+            self._hf = self._hp = None
             self._b = None
+            self._owner = None
 
     def __del__(self):
         try:

@@ -329,6 +329,8 @@ struct LPCNetBatch {
   bool mfw = false;      /* wider batches: mfw_kernel (three 4-stream groups, dedicated gather /
                             recurrent / sampler waves) for the same launches, non-split models with the
                             default rcpps */
+  bool plan_wide = false; /* the register tables were planned for mfw_kernel (plan class 3) */
+  std::vector<unsigned char> blob; /* the loaded model's blob: replanned when the kernel choice moves */
   double mf_ga_ops = 0;  /* int8 matrix-core ops per workgroup per sample: the GRU_A recurrent pass */
   double mf_gb_ops = 0;  /* the GRU_B tiles of both sampler waves */
   bool fp_ok = false;    /* fp32 model fits the fp_kernel tables */
@@ -460,6 +462,19 @@ int mfw_groups(int B, int cus)
  * one mf_kernel<4> round (nB <= 4 streams per CU: a drop-in pool's work
  * batch is sized for its widest launch, a partial step of a batch) to
  * mf_kernel, whose one-group sample is the shorter chain there. */
+/* whether choose_kernel will run mfw_kernel on this batch, the model's own
+ * limits (split plan, LDS) aside: the plan class of its register tables
+ * follows the same predicate */
+static bool mfw_planned(const LPCNetBatch *b, int cus)
+{
+  if ((b->kernel_mode != 0 && b->kernel_mode != 4) || b->rcp_custom) return false;
+  const char *e2 = getenv("LPCNET_MF2");
+  if (e2 && atoi(e2) == 0) return false;
+  const char *ew = getenv("LPCNET_MFW");
+  if (ew) return atoi(ew) != 0;
+  return mfw_groups(b->B, cus) > 0;
+}
+
 static bool wide_for(const LPCNetBatch *b, int nB) { return b->mfw && (b->mfw_forced || nB > 4 * b->cus); }
 static bool mf2_for(const LPCNetBatch *b, int nB) { return b->mf2 && (!b->mfw || wide_for(b, nB)); }
 
@@ -1235,8 +1250,8 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     /* the plan's SIMD weights follow the kernel the batch will run (see
      * mf_plan): the wide kernel above one mf_kernel<4> round unless turned
      * off */
-    const char *ew = getenv("LPCNET_MFW");
-    const bool wide = mfw_groups(b->B, current_device_cus()) > 0 && !(ew && atoi(ew) == 0);
+    const bool wide = mfw_planned(b, current_device_cus());
+    b->plan_wide = wide;
     const int cls = b->B >= MF2_MIN_STREAMS ? 2 : b->B >= 1024 ? 1 : 0;
     /* split plans never run the wide kernel */
     mf_ok = mf_plan(ga_blocks, plan, wide ? 3 : cls, cls);
@@ -2098,7 +2113,21 @@ LPCNET_EXPORT int lpcnet_batch_load_model(LPCNetBatch *b, const unsigned char *d
   if (!b) return -1;
   if (b->set_device()) return -1;
   (void)hipStreamSynchronize(b->stream);
-  return load_model(b, data, len);
+  const int rc = load_model(b, data, len);
+  if (rc == 0) b->blob.assign(data, data + len);
+  return rc;
+}
+
+/* after a change of the kernel mode or the rcpps table: re-plan the register
+ * tables when the wide kernel's plan class no longer matches the choice
+ * (speed only; the stream states stay) */
+static int replan_if_needed(LPCNetBatch *b)
+{
+  if (!b->have_model || !b->mf_ok || b->blob.empty() || mfw_planned(b, b->cus) == b->plan_wide) return 0;
+  if (b->set_device()) return -1;
+  (void)hipStreamSynchronize(b->stream);
+  const std::vector<unsigned char> blob = b->blob;
+  return load_model(b, blob.data(), (int)blob.size());
 }
 
 LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode)
@@ -2109,7 +2138,7 @@ LPCNET_EXPORT int lpcnet_batch_set_kernel(LPCNetBatch *b, int mode)
   }
   b->kernel_mode = mode;
   if (b->have_model) choose_kernel(b);
-  return 0;
+  return replan_if_needed(b);
 }
 
 LPCNET_EXPORT int lpcnet_batch_set_model_constants(LPCNetBatch *b, float lpc_gamma, int features_delay, int end2end)
@@ -2142,7 +2171,7 @@ LPCNET_EXPORT int lpcnet_batch_set_rcp_table(LPCNetBatch *b, const uint32_t *tab
   b->rcp_dev = dev;
   b->rcp_custom = dev != dflt;
   choose_kernel(b);
-  return 0;
+  return replan_if_needed(b);
 }
 
 LPCNET_EXPORT int lpcnet_batch_model_info(const LPCNetBatch *b, LPCNetModelInfo *info)
@@ -3439,15 +3468,19 @@ static Handle *live_handle(const LPCNetState *st)
 
 /* ---- placement of drop-in handles over the visible GPUs ------------------
  * The reference's lpcnet_init/lpcnet_create take no device (lpcnet.c:184-219),
- * so placement is library policy: each new handle goes to the placement with
- * the fewest live handles (one slot each once a model is bound), over every
- * visible device by default, over the list LPCNET_DEVICES="0,1,..." names, or
- * over lpcnet_mi355x_set_placement()'s list (handles initialised afterwards).
- * A list may name a device twice: two placements, two pools, one GPU (the
- * tests use this to exercise placement on a one-GPU box).  LPCNET_DEVICE=d
- * pins every new handle to device d, as before. */
+ * so placement is library policy.  By default every handle goes to one
+ * device: LOCAL_RANK mod the device count in a one-process-per-GPU job
+ * (torchrun ranks), device 0 otherwise -- resolved when a model is first
+ * bound, so lpcnet_init/lpcnet_create never start the HIP runtime.
+ * Spreading is opt-in: LPCNET_DEVICES="0,1,..." (or "all") or
+ * lpcnet_mi355x_set_placement() name a list of placements, and each new
+ * handle goes to the placement with the fewest live handles (one slot each
+ * once a model is bound).  A list may name a device twice: two placements,
+ * two pools, one GPU (the tests use this to exercise placement on a one-GPU
+ * box).  LPCNET_DEVICE=d pins every new handle to device d. */
 constexpr int kMaxPlace = 64;
 constexpr int kPinned = 1 << 20;
+constexpr int kDevDefault = -1; /* placement device resolved at the first model bind */
 static std::mutex g_place_mu;
 static std::vector<int> g_place_dev; /* placement -> device (empty: not set up yet) */
 static int g_place_load[kMaxPlace];  /* live handles per placement (of generation g_place_gen) */
@@ -3467,20 +3500,47 @@ static bool parse_device_list(const char *v, std::vector<int> &out)
   return !out.empty() && out.size() <= (size_t)kMaxPlace;
 }
 
-/* the placement of a new handle (g_place_mu held) */
-static void place_new_handle(Handle *h)
+/* the device of the default placement (starts the HIP runtime only under
+ * LOCAL_RANK, to take the rank's device modulo the visible count) */
+static int default_device()
+{
+  const char *lr = getenv("LOCAL_RANK");
+  if (!lr || !*lr) return 0;
+  const int r = atoi(lr), n = lpcnet_mi355x_device_count();
+  return n > 0 && r > 0 ? r % n : 0;
+}
+
+/* the placement of a new handle (g_place_mu held); -1 (error set) when
+ * LPCNET_DEVICES is malformed or names a device that is not visible */
+static int place_new_handle(Handle *h)
 {
   h->place_gen = g_place_gen;
   if (const char *d = getenv("LPCNET_DEVICE")) {
     h->device = atoi(d);
     h->place = kPinned + h->device;
-    return;
+    return 0;
   }
   if (g_place_dev.empty()) {
-    if (!parse_device_list(getenv("LPCNET_DEVICES"), g_place_dev)) {
-      const int n = std::min(std::max(lpcnet_mi355x_device_count(), 1), kMaxPlace);
-      g_place_dev.clear();
-      for (int k = 0; k < n; k++) g_place_dev.push_back(k);
+    const char *env = getenv("LPCNET_DEVICES");
+    if (env && *env) {
+      /* opt-in spreading: the list is checked against the visible devices
+       * here, as lpcnet_mi355x_set_placement checks its own */
+      std::vector<int> list;
+      const int ndev = lpcnet_mi355x_device_count();
+      if (strcmp(env, "all") == 0) {
+        for (int k = 0; k < std::min(std::max(ndev, 1), kMaxPlace); k++) list.push_back(k);
+      } else if (!parse_device_list(env, list)) {
+        set_err("LPCNET_DEVICES: expected \"all\" or a comma-separated list of at most 64 device indices");
+        return -1;
+      }
+      for (int d : list)
+        if (d >= std::max(ndev, 1)) {
+          set_err("LPCNET_DEVICES: device index outside the visible devices");
+          return -1;
+        }
+      g_place_dev = list;
+    } else {
+      g_place_dev.assign(1, kDevDefault);
     }
   }
   int best = 0;
@@ -3489,6 +3549,7 @@ static void place_new_handle(Handle *h)
   g_place_load[best]++;
   h->place = best;
   h->device = g_place_dev[best];
+  return 0;
 }
 
 static void unplace_handle(const Handle *h)
@@ -3548,6 +3609,7 @@ LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
 {
   if (!st) return -1;
   Handle *stale = nullptr, *live = nullptr;
+  bool failed = false;
   {
     LiveShard &sh = live_shard(st);
     std::lock_guard<std::mutex> lk(sh.mu);
@@ -3563,17 +3625,26 @@ LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
     if (!live) {
       Handle *h = new Handle();
       h->token = new_token();
+      int prc;
       {
         std::lock_guard<std::mutex> plk(g_place_mu);
-        place_new_handle(h);
+        prc = place_new_handle(h);
       }
-      sh.map[st] = h;
-      st->magic = kMagic;
-      st->reserved = 0;
-      st->token = h->token;
+      if (prc) {
+        delete h;
+        st->magic = 0;
+        st->token = 0;
+        failed = true;
+      } else {
+        sh.map[st] = h;
+        st->magic = kMagic;
+        st->reserved = 0;
+        st->token = h->token;
+      }
     }
   }
   if (stale) handle_free(stale);
+  if (failed) return -1;
   if (live) {
     /* src/lpcnet.c:184-200 ends with lpcnet_reset(): re-initialising a live
      * handle resets its stream and keeps its device binding and model */
@@ -3590,7 +3661,10 @@ LPCNET_EXPORT int lpcnet_init(LPCNetState *st)
 LPCNET_EXPORT LPCNetState *lpcnet_create(void)
 {
   LPCNetState *st = (LPCNetState *)calloc(1, sizeof(LPCNetState));
-  if (st) lpcnet_init(st);
+  if (st && lpcnet_init(st) != 0) {
+    free(st);
+    return nullptr;
+  }
   return st;
 }
 
@@ -3621,6 +3695,7 @@ LPCNET_EXPORT int lpcnet_load_model(LPCNetState *st, const unsigned char *data, 
 {
   Handle *h = live_handle(st);
   if (!h) { set_err("lpcnet_load_model: not an initialised LPCNetState"); return -1; }
+  if (h->device == kDevDefault) h->device = default_device();
   /* pools per (model, placement, device): a placement index of a later
    * list may name another device */
   StatePool *p = pool_acquire(data, len, h->device, h->place >= kPinned ? h->place : h->place * 1024 + h->device);
@@ -3740,7 +3815,9 @@ LPCNET_EXPORT int lpcnet_mi355x_handle_placement(const LPCNetState *st, int *dev
 {
   Handle *h = live_handle(st);
   if (!h) { set_err("not an initialised LPCNetState"); return -1; }
-  if (device) *device = h->device;
+  /* before the first model bind the default placement's device is the one
+   * lpcnet_load_model will take */
+  if (device) *device = h->device == kDevDefault ? default_device() : h->device;
   if (placement) *placement = h->place >= kPinned ? -1 : h->place;
   return 0;
 }
@@ -3811,8 +3888,9 @@ struct LPCNetDecState {
 
 LPCNET_EXPORT int lpcnet_decoder_get_size(void) { return (int)sizeof(LPCNetDecState); }
 
-/* lpcnet.c:290-295: memset + lpcnet_init (a zeroed embedded handle is a
- * fresh one; a live one at the same address is dropped as stale) */
+/* lpcnet.c:290-295: memset + lpcnet_init.  A never-initialised (or stale)
+ * decoder is zeroed and gets a fresh handle; a live one is re-initialised in
+ * place (stream reset, model kept), as below */
 LPCNET_EXPORT int lpcnet_decoder_init(LPCNetDecState *st)
 {
   if (!st) return -1;
@@ -3827,7 +3905,10 @@ LPCNET_EXPORT int lpcnet_decoder_init(LPCNetDecState *st)
 LPCNET_EXPORT LPCNetDecState *lpcnet_decoder_create(void)
 {
   LPCNetDecState *st = (LPCNetDecState *)malloc(sizeof(LPCNetDecState));
-  if (st) lpcnet_decoder_init(st);
+  if (st && lpcnet_decoder_init(st) != 0) {
+    free(st);
+    return nullptr;
+  }
   return st;
 }
 

@@ -855,3 +855,28 @@ def test_live_engine_buffers_match_caller_buffers(require_gpu, monkeypatch, vari
         for s in sorted({0, B // 2, B - 1}):
             o = O.Oracle(blob, variant)
             assert np.array_equal(got[s], np.stack([o.synthesize(allf[f, s]) for f in range(F)])), s
+
+
+def test_host_views_outlive_close(require_gpu):
+    """arrays handed out by host_features() / synthesize_host()
+    keep the batch's pinned memory alive past close() (no use-after-free):
+    the last PCM view still reads what the frame wrote, the feature view
+    stays writable, and the batch is destroyed once they go."""
+    import gc
+    import weakref
+    blob = L.synthetic_model(1, 0)
+    B = 64
+    b = L.LPCNetBatch(B, 0, blob)
+    hf = b.host_features()
+    np.copyto(hf, np.stack([feats(s, 1)[0] for s in range(B)]))
+    pcm = b.synthesize_host()
+    want = np.array(pcm)
+    owner = weakref.ref(b._owner)
+    b.close()
+    gc.collect()
+    assert owner() is not None  # the views hold the native batch
+    assert np.array_equal(pcm, want)
+    hf[:] = 0.0
+    del pcm, hf
+    gc.collect()
+    assert owner() is None  # destroyed with the last view

@@ -195,6 +195,60 @@ def test_placement_policy_without_gpu():
         L.set_placement([])
 
 
+INIT_NO_HIP = r"""
+import os, sys
+sys.path.insert(0, sys.argv[1])
+os.environ.pop("LOCAL_RANK", None)
+os.environ.pop("LPCNET_DEVICES", None)
+import lpcnet_amd as L
+
+
+def kfd_open():
+    fds = os.listdir("/proc/self/fd")
+    out = []
+    for fd in fds:
+        try:
+            out.append(os.readlink("/proc/self/fd/" + fd))
+        except OSError:
+            pass
+    return any(p.startswith("/dev/kfd") or p.startswith("/dev/dri") for p in out)
+
+
+nets = [L.LPCNet() for _ in range(4)]
+assert [n.placement() for n in nets] == [(0, 0)] * 4, [n.placement() for n in nets]
+assert not kfd_open(), "lpcnet_init / lpcnet_create started the HIP runtime"
+for n in nets:
+    n.close()
+print("ok")
+"""
+
+
+def test_init_leaves_hip_uninitialised():
+    """lpcnet_init / lpcnet_create with the default placement
+    must not start the HIP runtime (a caller may fork workers or exec after
+    creating handles, before binding a model): a fresh process creates
+    handles, queries their placement (one placement, device 0 without
+    LOCAL_RANK) and has not opened /dev/kfd."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", INIT_NO_HIP, ROOT], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
+
+
+def test_bad_device_list_fails_init():
+    """LPCNET_DEVICES is checked when the first handle is placed: a malformed
+    list makes lpcnet_init fail (lpcnet_create returns NULL) instead of being
+    ignored."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, sys.argv[1]); import lpcnet_amd as L\n"
+            "assert not L.lib.lpcnet_create()\n"
+            "assert 'LPCNET_DEVICES' in L.last_error(), L.last_error()\nprint('ok')")
+    env = dict(os.environ, LPCNET_DEVICES="0,x")
+    r = subprocess.run([sys.executable, "-c", code, ROOT], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
+
+
 def test_bench_line_serialises_numpy_scalars():
     """the bench line's ladders hold numpy-derived values (np.bool_ realtime
     flags, np.float64 means): the line must still print as JSON"""
@@ -206,3 +260,30 @@ def test_bench_line_serialises_numpy_scalars():
     assert json.loads(json.dumps(row, default=bench._json_scalar)) == {"realtime": True, "ms": 3.0, "n": 4}
     with pytest.raises(TypeError):
         json.dumps({"x": object()}, default=bench._json_scalar)
+
+
+def test_owned_view_keeps_owner_alive():
+    """lpcnet_amd._owned_view: the array (and any slice of it) holds its
+    owner; the owner's release runs only when the last view is gone."""
+    import ctypes as C
+    import gc
+    released = []
+
+    class Owner(L._BatchOwner):
+        def __del__(self):
+            released.append(True)
+
+    mem = (C.c_int16 * 64)()
+    o = Owner(None)
+    v = L._owned_view(o, C.addressof(mem), C.c_int16, np.int16, (4, 16))
+    del o
+    gc.collect()
+    s = v[1:3]
+    del v
+    gc.collect()
+    assert not released
+    s[:] = 5
+    assert mem[16] == 5
+    del s
+    gc.collect()
+    assert released == [True]
