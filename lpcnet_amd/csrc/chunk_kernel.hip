@@ -254,6 +254,9 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
           v = A.st[sid].conv1_mem[(fr + 2) * FIN + j];
         else if (fr < n)
           v = A.features[((size_t)fr * B + sid) * NF + (j < NF ? j : 18)];
+        /* deferred LPC: the frame's features for the lpc_kernel that runs
+         * after the sample kernel (the host may refill its buffer by then) */
+        if (NFR == 1 && A.lpc_feat && fr == 0 && j < NF) A.lpc_feat[(size_t)sid * NF + j] = v;
       }
     }
     vin[q] = v;
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
    * projection (read now: behind the projection's stores it waits for them) */
   __shared__ float nlpc[NFR == 1 ? G::SC * NLPC : 1];
   if constexpr (NFR == 1) {
-    if (!A.mc.end2end && tid < G::SC * NLPC) {
+    if (!A.mc.end2end && !A.lpc_defer && tid < G::SC * NLPC) {
       const int sid = s0 + tid / NLPC;
       nlpc[tid] = sid < B ? A.lpc_new[(size_t)sid * NLPC + tid % NLPC] : 0.f;
     }
@@ -520,7 +523,10 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
       auto L = [&](int t) { return t >= 0 ? lpcn(t, s, sid, k) : olpc[s][-1 - t][k]; };
       StreamState *p = &A.st[sid];
       p->lpc[k] = lpc_weight(L(n - 1 - D), k, gamma);
-      for (int j = 0; j < D; j++) p->old_lpc[j][k] = L(n - 1 - j);
+      /* deferred LPC (one frame, D >= 1): the frame read the ring's oldest
+       * slot; lpc_kernel pushes this frame's LPC after the sample kernel */
+      if (NFR != 1 || !A.lpc_defer)
+        for (int j = 0; j < D; j++) p->old_lpc[j][k] = L(n - 1 - j);
     }
   }
   if (tid < G::SC && s0 + tid < B) A.st[s0 + tid].frame_count = ck_fc(fcs[tid], n);

@@ -2225,9 +2225,26 @@ static bool single_frame_chunked(const LPCNetBatch *b, int nB, int N, int preloa
          !b->sa.trace_logits && !getenv("LPCNET_NO_CHUNK");
 }
 
-static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_features, short *d_pcm, int N)
+/* Deferred LPC (one-frame ticks of models with FEATURES_DELAY >= 1): a
+ * frame synthesises with the LPC of frame f - FEATURES_DELAY (lpcnet.c:
+ * 110-118), already in the stream's ring, so lpc_from_cepstrum of this
+ * frame's features is off the tick's critical path: the chunk kernel reads
+ * the ring's oldest slot only, and lpc_kernel pushes the new LPC into the
+ * ring after the sample kernel, while the caller consumes the PCM and
+ * refills its features (the tick's end is the sample kernel's).
+ * LPCNET_LPC_EAGER=1 keeps the LPC before the chunk kernel. */
+static bool lpc_deferred(const LPCNetBatch *b)
 {
-  if (!b->mc.end2end && launch_lpc(d_features, b->d_lpc, nB, b->d_lpc_tab, b->stream)) {
+  const char *e = getenv("LPCNET_LPC_EAGER");
+  return !b->mc.end2end && b->mc.delay >= 1 && !(e && atoi(e) != 0);
+}
+
+/* d_features: device memory, or the mapped host buffer (mapped = true: a
+ * deferred LPC then reads the chunk kernel's copy in b->d_feat) */
+static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_features, short *d_pcm, int N,
+                                       bool defer = false, bool mapped = false)
+{
+  if (!b->mc.end2end && !defer && launch_lpc(d_features, b->d_lpc, nB, b->d_lpc_tab, b->stream)) {
     set_err("lpc kernel launch failed");
     return -1;
   }
@@ -2240,6 +2257,8 @@ static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_fe
   fa.nframes = 1;
   fa.cond = nullptr;
   fa.stamps = nullptr;
+  fa.lpc_defer = defer ? 1 : 0;
+  fa.lpc_feat = defer && mapped ? b->d_feat : nullptr;
   hipEvent_t e[3] = {nullptr, nullptr, nullptr};
   if (b->timing >= 2) e[0] = get_event(b);
   if (b->timing >= 1) {
@@ -2314,15 +2333,22 @@ static int ensure_host_io(LPCNetBatch *b)
  * 58-60 -> 69-84 M); otherwise hipStreamSynchronize, 2-3 % faster for one
  * caller driving a batch (tools/sync_ab.sh, profiles/r05/sync_ab.log).
  * LPCNET_SYNC_BLOCK=1 / LPCNET_SYNC_POLL=1 force one form everywhere. */
-static int tick_sync(LPCNetBatch *b, bool poll)
+static int tick_sync(LPCNetBatch *b, bool poll, const std::function<int()> &after = std::function<int()>())
 {
   if (getenv("LPCNET_SYNC_POLL")) poll = true;
-  if (!poll || getenv("LPCNET_SYNC_BLOCK")) {
+  const bool block = !poll || getenv("LPCNET_SYNC_BLOCK");
+  if (block && !after) {
     HIPCHK(hipStreamSynchronize(b->stream));
     return 0;
   }
   if (!b->ev_tick) HIPCHK(hipEventCreateWithFlags(&b->ev_tick, hipEventDisableTiming));
   HIPCHK(hipEventRecord(b->ev_tick, b->stream));
+  /* work queued behind the tick's end (the deferred LPC): not waited for */
+  if (after && after()) return -1;
+  if (block) {
+    HIPCHK(hipEventSynchronize(b->ev_tick));
+    return 0;
+  }
   static const int pause = getenv("LPCNET_SYNC_PAUSE") ? atoi(getenv("LPCNET_SYNC_PAUSE")) : TICK_POLL_PAUSE;
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
@@ -2375,12 +2401,21 @@ static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm
       HIPCHK(hipMemcpyAsync(b->d_feat, own_feat ? b->h_io_feat : b->h_stg_feat, sizeof(float) * NF * nB,
                             hipMemcpyHostToDevice, b->stream));
     const bool direct = own_pcm && pcm_store_coalesced(b);
-    if (launch_single_frame_chunked(b, nB, zc_feat ? b->d_io_feat : b->d_feat, direct ? b->d_io_pcm : b->d_pcm, N))
+    const bool defer = lpc_deferred(b);
+    if (launch_single_frame_chunked(b, nB, zc_feat ? b->d_io_feat : b->d_feat, direct ? b->d_io_pcm : b->d_pcm, N,
+                                    defer, zc_feat))
       return -1;
     if (!direct)
       HIPCHK(hipMemcpyAsync(own_pcm ? b->h_io_pcm : b->h_stg_pcm, b->d_pcm, sizeof(short) * N * nB,
                             hipMemcpyDeviceToHost, b->stream));
-    if (tick_sync(b, false)) return -1;
+    auto lpc_after = [&]() -> int {
+      if (launch_lpc(b->d_feat, nullptr, nB, b->d_lpc_tab, b->stream, b->d_state, b->mc.delay)) {
+        set_err("deferred lpc kernel launch failed");
+        return -1;
+      }
+      return 0;
+    };
+    if (tick_sync(b, false, defer ? std::function<int()>(lpc_after) : std::function<int()>())) return -1;
     if (check_status(b)) return -1;
     if (!own_pcm) memcpy(pcm, b->h_stg_pcm, sizeof(short) * N * nB);
     return 0;

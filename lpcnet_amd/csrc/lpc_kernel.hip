@@ -98,7 +98,7 @@ __device__ __forceinline__ void bfly5(C2 *f, int u, const C2 *tw)
 }  // namespace
 
 __global__ __launch_bounds__(64 * LPC_STREAMS) void lpc_kernel(const float *features, float *lpc_out, int nstreams,
-                                                               const LpcTables *T)
+                                                               const LpcTables *T, StreamState *ring, int ring_depth)
 {
   __shared__ C2 ybuf[LPC_STREAMS][WIN];
   __shared__ C2 tw[WIN];
@@ -207,17 +207,31 @@ __global__ __launch_bounds__(64 * LPC_STREAMS) void lpc_kernel(const float *feat
         if (err < .001f * ac[0]) break;
       }
     }
+    if (ring) {
+      /* deferred form (one-frame ticks, FEATURES_DELAY >= 1): push this
+       * frame's LPC into the stream's ring (lpcnet.c:110-114: the oldest slot
+       * was read by the frame's chunk_kernel already) */
+      float4 *q = (float4 *)ring[lsid].old_lpc[0];
+      for (int j = ring_depth - 1; j > 0; j--)
+#pragma unroll
+        for (int i = 0; i < NLPC / 4; i++) q[j * (NLPC / 4) + i] = q[(j - 1) * (NLPC / 4) + i];
+#pragma unroll
+      for (int i = 0; i < NLPC / 4; i++) q[i] = make_float4(lpc[4 * i], lpc[4 * i + 1], lpc[4 * i + 2], lpc[4 * i + 3]);
+      return;
+    }
     float4 *o = (float4 *)(lpc_out + (size_t)lsid * NLPC);
 #pragma unroll
     for (int i = 0; i < NLPC / 4; i++) o[i] = make_float4(lpc[4 * i], lpc[4 * i + 1], lpc[4 * i + 2], lpc[4 * i + 3]);
   }
 }
 
-int launch_lpc(const float *features, float *lpc_out, int nstreams, const LpcTables *tables, void *stream)
+int launch_lpc(const float *features, float *lpc_out, int nstreams, const LpcTables *tables, void *stream,
+               StreamState *ring, int ring_depth)
 {
+  if (ring && (ring_depth < 1 || ring_depth > MAX_FEATURES_DELAY)) return -1;
   const int grid = (nstreams + LPC_STREAMS - 1) / LPC_STREAMS;
   hipLaunchKernelGGL(lpc_kernel, dim3(grid), dim3(64 * LPC_STREAMS), 0, (hipStream_t)stream, features, lpc_out, nstreams,
-                     tables);
+                     tables, ring, ring_depth);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -169,6 +169,12 @@ struct FrameArgs {
    * lane l = (g, r) = (l / 16, l % 16), element j of quad q = W[4 (4q + j) +
    * g][16 rt + r] (0 past K), CK_WPAD zero quads after each row tile's last */
   const float4 *ck_conv1, *ck_conv2, *ck_dense1, *ck_dense2, *ck_proj;
+  /* one-frame chunk_kernel, deferred LPC (FEATURES_DELAY >= 1): the frame's
+   * LPC comes from the ring only, the ring is advanced later by lpc_kernel
+   * (launch_lpc with a ring), and the frame's features are copied to
+   * lpc_feat ([B][NF], device memory) for it when non-null */
+  int lpc_defer;
+  float *lpc_feat;
 };
 constexpr int CK_WPAD = 8; /* chunk_kernel: k quads in flight per wave (zero padding of each row tile) */
 
@@ -381,7 +387,8 @@ struct LpcTables {
   LpcSlot slot[LPC_WIN];
 };
 /* features [nstreams][NF] -> lpc_out [nstreams][NLPC] */
-int launch_lpc(const float *features, float *lpc_out, int nstreams, const LpcTables *tables, void *stream);
+int launch_lpc(const float *features, float *lpc_out, int nstreams, const LpcTables *tables, void *stream,
+               StreamState *ring = nullptr, int ring_depth = 0);
 
 /* decode_packet (lpcnet_dec.c:81-156) on the device (decode_kernel.hip):
  * packets [npackets][nstreams][8] -> features [4 npackets][nstreams][NF],

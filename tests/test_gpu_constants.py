@@ -122,3 +122,43 @@ def test_constants_setter_and_environment(require_gpu, monkeypatch):
     net = L.LPCNet(blob)
     for fr in range(G2["pcm"].shape[1]):
         assert np.array_equal(net.synthesize(G2["features"][0, fr]), G2["pcm"][0, fr]), fr
+
+
+@pytest.mark.parametrize("delay", [1, 2, 4])
+@pytest.mark.parametrize("B", [300, 1100])
+def test_deferred_lpc_ticks_match_eager_and_oracle(require_gpu, monkeypatch, delay, B):
+    """One-frame ticks (lpcnet_batch_synthesize, > 128 streams: chunked frame
+    network) with FEATURES_DELAY >= 1 push the frame's LPC into the ring
+    after the sample kernel (deferred lpc_kernel); ticks on the batch's own
+    pinned buffers (the chunk kernel's feature copy) and on caller arrays,
+    interleaved with a multi-frame device-resident call and snapshots taken
+    right after a tick, equal the eager order (LPCNET_LPC_EAGER=1) bit for
+    bit on every stream, and the oracle on sampled streams."""
+    c = (0.92, delay, 0)
+    blob = blob_with(0, c)
+    F = 9
+    allf = np.ascontiguousarray(np.stack([L.synthetic_features(s, F)[:, :20] for s in range(B)], 1))
+
+    def run():
+        b = L.LPCNetBatch(B, 0, blob)
+        hf = b.host_features()
+        out, snaps = [], []
+        for f in range(3):  # engine buffers (mapped features: the chunk kernel's copy feeds the LPC)
+            np.copyto(hf, allf[f])
+            out.append(np.array(b.synthesize_host()))
+        snaps.append(bytes(b.save_state(B - 1)))
+        out.extend(_frames(b, allf, 3, 6))  # multi-frame launch after deferred ticks
+        for f in range(6, F):  # caller arrays (DMA-copied features)
+            out.append(b.synthesize(allf[f]))
+            snaps.append(bytes(b.save_state(0)))
+        b.close()
+        return np.stack(out, 0), snaps
+
+    got, sg = run()
+    monkeypatch.setenv("LPCNET_LPC_EAGER", "1")
+    ref, sr = run()
+    assert np.array_equal(got, ref)
+    assert sg == sr
+    for s in (0, B // 2, B - 1):
+        exp = O.synth_stream(L.synthetic_model(1, 0), allf[:, s], 0, constants=c)
+        assert np.array_equal(got[:, s], exp), s

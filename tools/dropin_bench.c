@@ -2,6 +2,7 @@
  * dropin_bench.c -- aggregate throughput of the drop-in API from C threads.
  *
  *   dropin_bench <threads> <frames> [pool]
+ *   dropin_bench <threads> <frames> rt [burst|spread]
  *
  * T pthreads, one LPCNetState each (include/lpcnet.h: lpcnet_create,
  * lpcnet_load_model, lpcnet_synthesize -- the reference's own calling
@@ -12,6 +13,15 @@
  * (lpcnet_batch_synthesize_frames).  One JSON object on stdout.  The C
  * driver separates the pool's own cost from a Python caller's turnaround.
  * With "pool" only the drop-in part runs (for a kernel trace of it alone).
+ *
+ * "rt": real-time pacing, the way lpcnet_demo.c:208-219 drives one stream
+ * per 10 ms of audio: each thread calls lpcnet_synthesize once per 10 ms
+ * tick (absolute deadlines, CLOCK_MONOTONIC), "burst" with every thread on
+ * the same tick phase, "spread" (default) with the T phases spaced evenly
+ * over the 10 ms; per call the latency (call start to return) and whether
+ * it returned after its tick's end (a missed deadline: the stream's next
+ * frame is late).  One JSON object: latency p50 / p99 / max, misses,
+ * coalesced launches.
  */
 #define _POSIX_C_SOURCE 200809L
 #include <pthread.h>
@@ -34,6 +44,46 @@ static double now(void)
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+/* rt mode */
+static double rt_t0;      /* first tick (CLOCK_MONOTONIC seconds) */
+static int rt_spread = 1; /* phases spread over the tick */
+static float *rt_lat;     /* [T][F] call latency, ms */
+static int *rt_miss;      /* [T] calls that returned after their tick's end */
+#define TICK_S 0.010
+
+static void sleep_until(double t)
+{
+  struct timespec ts;
+  ts.tv_sec = (time_t)t;
+  ts.tv_nsec = (long)((t - (double)ts.tv_sec) * 1e9);
+  while (clock_nanosleep(CLOCK_MONOTONIC, TIMER_ABSTIME, &ts, NULL) != 0) {
+  }
+}
+
+static void *run_rt(void *arg)
+{
+  const int t = (int)(size_t)arg;
+  short pcm[LPCNET_FRAME_SIZE];
+  const double phase = rt_spread ? TICK_S * t / T : 0.0;
+  pthread_barrier_wait(&go);
+  for (int f = 0; f < F; f++) {
+    const double tick = rt_t0 + phase + TICK_S * f;
+    sleep_until(tick);
+    const double a = now();
+    lpcnet_synthesize(nets[t], &feats[((size_t)t * F + f) * NB_TOTAL_FEATURES], pcm, LPCNET_FRAME_SIZE);
+    const double e = now();
+    rt_lat[(size_t)t * F + f] = (float)((e - a) * 1e3);
+    if (e > tick + TICK_S) rt_miss[t]++;
+  }
+  return NULL;
+}
+
+static int cmpf(const void *x, const void *y)
+{
+  const float a = *(const float *)x, b = *(const float *)y;
+  return (a > b) - (a < b);
 }
 
 static void *run(void *arg)
@@ -85,6 +135,32 @@ int main(int argc, char **argv)
     for (int t = 0; t < T; t++) lpcnet_reset(nets[t]);
   }
   (void)warm;
+  if (argc > 3 && !strcmp(argv[3], "rt")) {
+    rt_spread = !(argc > 4 && !strcmp(argv[4], "burst"));
+    rt_lat = calloc((size_t)T * F, sizeof(float));
+    rt_miss = calloc(T, sizeof(int));
+    long a0 = 0, q0 = 0;
+    int nsb = 0;
+    lpcnet_mi355x_pool_stats(nets[0], &a0, &q0, &nsb);
+    pthread_barrier_init(&go, NULL, T + 1);
+    rt_t0 = now() + 0.05 + 0.001 * T / 64.0; /* every thread started and asleep before the first tick */
+    for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, run_rt, (void *)(size_t)t);
+    pthread_barrier_wait(&go);
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    long a1 = 0, q1 = 0;
+    lpcnet_mi355x_pool_stats(nets[0], &a1, &q1, &nsb);
+    long misses = 0;
+    for (int t = 0; t < T; t++) misses += rt_miss[t];
+    const size_t n = (size_t)T * F;
+    qsort(rt_lat, n, sizeof(float), cmpf);
+    printf("{\"threads\": %d, \"frames\": %d, \"mode\": \"%s\", \"latency_ms_p50\": %.4f, \"latency_ms_p99\": %.4f, "
+           "\"latency_ms_max\": %.4f, \"deadline_misses\": %ld, \"calls\": %zu, \"launches\": %ld, "
+           "\"mean_coalesced_streams\": %.2f, \"realtime_p99\": %s}\n",
+           T, F, rt_spread ? "spread" : "burst", rt_lat[n / 2], rt_lat[(size_t)(0.99 * (n - 1))], rt_lat[n - 1], misses, n,
+           a1 - a0, (double)(q1 - q0) / (a1 - a0 > 0 ? a1 - a0 : 1), rt_lat[(size_t)(0.99 * (n - 1))] <= 10.0 ? "true" : "false");
+    for (int t = 0; t < T; t++) lpcnet_destroy(nets[t]);
+    return 0;
+  }
   long la0 = 0, rq0 = 0;
   int ns = 0;
   lpcnet_mi355x_pool_stats(nets[0], &la0, &rq0, &ns);
