@@ -207,9 +207,20 @@ __device__ __forceinline__ uint32_t ck_warm_weights(const FrameArgs &A, int tid)
   return acc;
 }
 
-template <int NFR, int SC, bool HWR>
+/* PS > 1 (one-frame launches without per-frame outputs): each 16-stream
+ * group runs as PS workgroups ("slices", consecutive blockIdx) that each
+ * compute the frame network up to dense2 and the projection row tiles
+ * rt = PS k + slice -- the projection (75 row tiles, issue-bound on the f32
+ * matrix cores: 19.2 K cycles per SIMD at one slice) spread over PS CUs
+ * instead of one.  The stream state (conv memories, LPC ring, frame_count)
+ * is read by every slice and written by the last one only, after the
+ * others have counted their arrival in ck_sync[group] past their prologue
+ * reads: the writer has the highest blockIdx of its group, so the slices
+ * it waits for were dispatched before it and the wait ends. */
+template <int NFR, int SC, bool HWR, int PS = 1>
 __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
 {
+  static_assert(PS == 1 || NFR == 1, "row slices: one-frame launches only");
 #ifdef CK_STAMPS
   unsigned long long ck_t[10] = {};
 #endif
@@ -225,7 +236,10 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   __shared__ int fcs[G::SC];
   __shared__ float olpc[G::SC][MAX_FEATURES_DELAY][NLPC];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, g = l >> 4, r = l & 15;
-  const int s0 = blockIdx.x * G::SC;
+  const int grp = PS > 1 ? (int)blockIdx.x / PS : (int)blockIdx.x;
+  const int slice = PS > 1 ? (int)blockIdx.x % PS : 0;
+  const bool writer = slice == PS - 1; /* workgroup-uniform */
+  const int s0 = grp * G::SC;
   const int n = A.nframes, B = A.nstreams;
   const uint32_t *rcp = A.rcp;
   const int D = A.mc.delay;
@@ -256,7 +270,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
           v = A.features[((size_t)fr * B + sid) * NF + (j < NF ? j : 18)];
         /* deferred LPC: the frame's features for the lpc_kernel that runs
          * after the sample kernel (the host may refill its buffer by then) */
-        if (NFR == 1 && A.lpc_feat && fr == 0 && j < NF) A.lpc_feat[(size_t)sid * NF + j] = v;
+        if (NFR == 1 && writer && A.lpc_feat && fr == 0 && j < NF) A.lpc_feat[(size_t)sid * NF + j] = v;
       }
     }
     vin[q] = v;
@@ -316,6 +330,13 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   asm volatile("" ::"v"(warm)); /* the warming loads land before the weights are used */
   __syncthreads();
   CK_T(1);
+  if constexpr (PS > 1) {
+    /* every state read of this slice has landed (LDS / registers) */
+    if (!writer && tid == 0) {
+      __threadfence();
+      atomicAdd(&A.ck_sync[grp], 1);
+    }
+  }
 
   /* this lane's column of each column tile */
   int cs[NCT], cf[NCT];
@@ -364,8 +385,26 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   __syncthreads();
 
   CK_T(2);
+  if constexpr (PS > 1) {
+    /* the writer: the other slices have read the state (bounded wait: on a
+     * timeout the status word reports the call invalid) */
+    if (writer) {
+      if (tid == 0) {
+        int polls = 0;
+        while (__hip_atomic_load(&A.ck_sync[grp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < PS - 1) {
+          if (++polls > (1 << 22)) {
+            A.status[0] = STATUS_SLICE_TIMEOUT; /* plain vector store to the pinned host word */
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        atomicExch(&A.ck_sync[grp], 0);
+      }
+      __syncthreads();
+    }
+  }
   /* the conv1 memory after the chunk: inputs of frames n-2, n-1 (nnet.c:469) */
-  for (int e = tid; e < G::SC * 2 * FIN; e += CK_THREADS) {
+  for (int e = tid; writer && e < G::SC * 2 * FIN; e += CK_THREADS) {
     const int s = e / (2 * FIN), j = e % (2 * FIN), sid = s0 + s;
     if (sid < B) A.st[sid].conv1_mem[j] = inl[s * G::IN_SS + n * FIN + j];
   }
@@ -435,7 +474,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
 #pragma unroll
         for (int k = 0; k < NLPC; k++) q->lpc[k] = lp[k];
       }
-      if (f == n - 1)
+      if (f == n - 1 && writer)
 #pragma unroll
         for (int k = 0; k < NLPC; k++) A.st[sid].lpc[k] = lp[k];
     }
@@ -447,26 +486,29 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   /* TP of this wave's tiles per pass (wave + 8 t, t < 10: the last pass of
    * waves 3..7 carries one tile past the 75th, computed on a clamped copy
    * and not stored) */
-  constexpr int WV = CK_THREADS / 64, NT = (CK_PROJ_TILES + WV - 1) / WV; /* 10 tiles at most per wave */
+  /* sliced: this slice's tiles rt = PS lt + slice, lt = wave + 8 t */
+  constexpr int WV = CK_THREADS / 64, NTS = (CK_PROJ_TILES + PS - 1) / PS, NT = (NTS + WV - 1) / WV;
+  constexpr int TPS = PS > 1 ? NT : TP; /* all of a slice's tiles in one pass */
 #pragma unroll 1
-  for (int t0 = 0; t0 < NT; t0 += TP) {
-    const float4 *cur[TP];
-    const float *bia[TP];
-    int rts[TP];
+  for (int t0 = 0; t0 < NT; t0 += TPS) {
+    const float4 *cur[TPS];
+    const float *bia[TPS];
+    int rts[TPS];
 #pragma unroll
-    for (int t = 0; t < TP; t++) {
-      const int rt = wave + WV * (t0 + t);
+    for (int t = 0; t < TPS; t++) {
+      const int rt = (wave + WV * (t0 + t)) * PS + slice;
       rts[t] = rt;
-      const int rc = rt < CK_PROJ_TILES ? rt : wave; /* clamped: in bounds, result dropped */
+      const int rc = rt < CK_PROJ_TILES ? rt : slice; /* clamped: in bounds, result dropped */
       cur[t] = t_pj(rc);
       bia[t] = A.proj_b + 16 * rc + 4 * g;
     }
-    CkRing<TP, PQP> RP;
+    constexpr int PQS = PS > 1 ? ck_pqp(TPS, NCT) : PQP;
+    CkRing<TPS, PQS> RP;
     ck_prime(RP, cur, bia);
-    f32x4 pacc[TP][NCT];
-    ck_tiles<COND, COND, CK_RS, NCT, TP, PQP, XL>(RP, cur, nullptr, nullptr, ya, xb, pacc);
+    f32x4 pacc[TPS][NCT];
+    ck_tiles<COND, COND, CK_RS, NCT, TPS, PQS, XL>(RP, cur, nullptr, nullptr, ya, xb, pacc);
 #pragma unroll
-    for (int t = 0; t < TP; t++) {
+    for (int t = 0; t < TPS; t++) {
       if (rts[t] >= CK_PROJ_TILES) continue;
 #pragma unroll
       for (int j = 0; j < NCT; j++) {
@@ -498,7 +540,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   /* per frame: the LPC it synthesises with (lpcnet.c:110-118: the ring's
    * oldest slot, i.e. lpc_from_cepstrum of frame f - FEATURES_DELAY, then
    * lpc_weighting; END2END: written above) and frame_count after its update */
-  for (int e = tid; A.cond && e < G::SC * NFR * (NLPC + 1); e += CK_THREADS) {
+  for (int e = tid; writer && A.cond && e < G::SC * NFR * (NLPC + 1); e += CK_THREADS) {
     const int s = e / (NFR * (NLPC + 1)), rem = e % (NFR * (NLPC + 1));
     const int f = rem / (NLPC + 1), k = rem % (NLPC + 1), sid = s0 + s;
     if (sid >= B || f >= n) continue;
@@ -513,11 +555,11 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   }
   /* the stream state after the chunk: conv2 memory = conv1 outputs of frames
    * n-2, n-1; LPC ring; lpc of the last frame; frame_count */
-  for (int e = tid; e < G::SC * 2 * COND; e += CK_THREADS) {
+  for (int e = tid; writer && e < G::SC * 2 * COND; e += CK_THREADS) {
     const int s = e / (2 * COND), j = e % (2 * COND), sid = s0 + s;
     if (sid < B) A.st[sid].conv2_mem[j] = c1[s * G::C1_SS + (n + j / COND) * CK_RS + j % COND];
   }
-  if (!A.mc.end2end && tid < G::SC * NLPC) {
+  if (!A.mc.end2end && writer && tid < G::SC * NLPC) {
     const int s = tid / NLPC, k = tid % NLPC, sid = s0 + s;
     if (sid < B) {
       auto L = [&](int t) { return t >= 0 ? lpcn(t, s, sid, k) : olpc[s][-1 - t][k]; };
@@ -529,7 +571,7 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
         for (int j = 0; j < D; j++) p->old_lpc[j][k] = L(n - 1 - j);
     }
   }
-  if (tid < G::SC && s0 + tid < B) A.st[s0 + tid].frame_count = ck_fc(fcs[tid], n);
+  if (writer && tid < G::SC && s0 + tid < B) A.st[s0 + tid].frame_count = ck_fc(fcs[tid], n);
 #ifdef CK_STAMPS
   CK_T(6);
   if (blockIdx.x == 0 && tid == 0)
@@ -539,14 +581,14 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
 #endif
 }
 
-template <int NFR, int SC, bool HWR>
+template <int NFR, int SC, bool HWR, int PS = 1>
 static int launch_chunk_t(const FrameArgs &a, void *stream)
 {
   using G = CkGeom<NFR, SC>;
   const int bytes = G::FLOATS * 4;
-  if (ensure_dyn_lds((const void *)chunk_kernel<NFR, SC, HWR>, bytes)) return -1;
-  const int grid = (a.nstreams + G::SC - 1) / G::SC;
-  hipLaunchKernelGGL((chunk_kernel<NFR, SC, HWR>), dim3(grid), dim3(CK_THREADS), bytes, (hipStream_t)stream, a);
+  if (ensure_dyn_lds((const void *)chunk_kernel<NFR, SC, HWR, PS>, bytes)) return -1;
+  const int grid = (a.nstreams + G::SC - 1) / G::SC * PS;
+  hipLaunchKernelGGL((chunk_kernel<NFR, SC, HWR, PS>), dim3(grid), dim3(CK_THREADS), bytes, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -564,8 +606,18 @@ static int launch_chunk_h(const FrameArgs &a, void *stream)
    * 10 ms tick): stream-only columns, 16 or 32 streams per workgroup -- a
    * workgroup's time is mostly its pass over the 1.08 MB of weights, so the
    * smaller tile while the grid fits two rounds */
-  if (a.nframes == 1)
-    return (a.nstreams + 15) / 16 <= 2 * cus ? launch_chunk_t<1, 16, HWR>(a, stream) : launch_chunk_t<1, 32, HWR>(a, stream);
+  if (a.nframes == 1) {
+    /* row slices while the groups leave CUs idle (1024 streams: 64 groups x 4
+     * slices = one workgroup per CU) */
+    const int groups = (a.nstreams + 15) / 16;
+    static const int ps_env = getenv("LPCNET_CK_SLICES") ? atoi(getenv("LPCNET_CK_SLICES")) : -1;
+    const int ps = !a.ck_sync || !a.status || a.cond ? 1
+                   : ps_env >= 1 ? ps_env
+                   : 4 * groups <= cus ? 4 : 2 * groups <= cus ? 2 : 1;
+    if (ps >= 4) return launch_chunk_t<1, 16, HWR, 4>(a, stream);
+    if (ps == 2) return launch_chunk_t<1, 16, HWR, 2>(a, stream);
+    return groups <= 2 * cus ? launch_chunk_t<1, 16, HWR>(a, stream) : launch_chunk_t<1, 32, HWR>(a, stream);
+  }
   if (a.nframes <= 8) return launch_chunk_t<8, 8, HWR>(a, stream);
   if (a.nframes <= 16) return launch_chunk_t<16, 4, HWR>(a, stream);
   if (a.nframes <= 20 && cost(4, 5) < cost(2, 4)) return launch_chunk_t<20, 4, HWR>(a, stream);

@@ -379,6 +379,7 @@ struct LPCNetBatch {
    * STATUS_* bits; every synchronising entry point checks and clears it */
   int *h_status = nullptr;
   int *d_status = nullptr;
+  int *d_ck_sync = nullptr; /* [ceil(B / 16)] arrival counters of the sliced one-frame chunk kernel */
   int spin_limit = FLAG_SPIN_LIMIT_DEFAULT;
   /* 1.6 kb/s decoder (decode_kernel.hip): the model's ceps codebooks (optional
    * blob records), packets and decoded features of up to DEC_MAX_PACKETS
@@ -1974,6 +1975,9 @@ int check_status(LPCNetBatch *b)
   __atomic_store_n(b->h_status, 0, __ATOMIC_RELEASE);
   if (st & STATUS_FLAG_TIMEOUT)
     set_err("device abort: an LDS flag wait in the sample kernel exceeded its spin limit; the PCM of this call is invalid");
+  else if (st & STATUS_SLICE_TIMEOUT)
+    set_err("device abort: a sliced one-frame chunk kernel waited too long for its sibling workgroups; the PCM of "
+            "this call is invalid");
   else if (st & STATUS_ACTIVITY)
     set_err("device abort: a multi-frame sample launch saw a stream turn active mid-launch (frame_count bound out of "
             "date); the PCM of this call is invalid");
@@ -2043,6 +2047,8 @@ LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
   ok = ok && hipHostGetDevicePointer((void **)&b->d_status, b->h_status, 0) == hipSuccess;
   if (ok) *b->h_status = 0;
   ok = ok && hipMalloc(&b->d_lpc, sizeof(float) * NLPC * (size_t)nb_streams * LPC_CHUNK) == hipSuccess;
+  ok = ok && hipMalloc(&b->d_ck_sync, sizeof(int) * (size_t)((nb_streams + 15) / 16)) == hipSuccess;
+  ok = ok && hipMemset(b->d_ck_sync, 0, sizeof(int) * (size_t)((nb_streams + 15) / 16)) == hipSuccess;
   ok = ok && hipMalloc(&b->d_lpc_tab, sizeof(LpcTables)) == hipSuccess;
   /* d_chunk (the chunked path's frame outputs, LPC_CHUNK x 4.9 KB per
    * stream) is allocated by the first call that takes that path */
@@ -2078,6 +2084,7 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
   if (b->fstream) (void)hipStreamSynchronize(b->fstream);
   free_model(b);
   (void)hipFree(b->d_state);
+  (void)hipFree(b->d_ck_sync);
   (void)hipFree(b->d_feat);
   (void)hipFree(b->d_pcm);
   (void)hipFree(b->d_trace_logits);
@@ -2259,6 +2266,8 @@ static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_fe
   fa.stamps = nullptr;
   fa.lpc_defer = defer ? 1 : 0;
   fa.lpc_feat = defer && mapped ? b->d_feat : nullptr;
+  fa.ck_sync = b->d_ck_sync;
+  fa.status = b->d_status;
   hipEvent_t e[3] = {nullptr, nullptr, nullptr};
   if (b->timing >= 2) e[0] = get_event(b);
   if (b->timing >= 1) {

@@ -175,6 +175,12 @@ struct FrameArgs {
    * lpc_feat ([B][NF], device memory) for it when non-null */
   int lpc_defer;
   float *lpc_feat;
+  /* one-frame chunk_kernel with its projection split over row slices
+   * (launch_chunk picks the slice count): per 16-stream group an arrival
+   * counter (zeroed, [groups]); a timed-out wait sets STATUS_SLICE_TIMEOUT
+   * in *status (the batch's status word) */
+  int *ck_sync;
+  int *status;
 };
 constexpr int CK_WPAD = 8; /* chunk_kernel: k quads in flight per wave (zero padding of each row tile) */
 
@@ -268,6 +274,7 @@ constexpr int FLAG_SPIN_LIMIT_MAX = 1 << 30;     /* larger requests are clamped 
 /* Status bits a sample kernel reports to the host (SampleArgs::status). */
 constexpr int STATUS_FLAG_TIMEOUT = 1; /* an LDS flag wait exceeded spin_limit: output invalid */
 constexpr int STATUS_ACTIVITY = 2;     /* a multi-frame launch saw a stream become active mid-launch */
+constexpr int STATUS_SLICE_TIMEOUT = 4; /* a sliced chunk_kernel's writer waited too long for its siblings */
 
 /* The frame step's outputs as a sample kernel reads them: the FrameCond
  * copy when the launch has one, else the stream state. */

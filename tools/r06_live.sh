@@ -9,13 +9,13 @@ mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_constants.py tests/test_gpu.py tests/test_gpu_dropin.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "${TESTK:-live or deferred or constants or host_views or dropin or placement or thread}" > gpurun_out/r06_live_pytest.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/r06_live_pytest.log; exit 1; }
 tail -2 gpurun_out/r06_live_pytest.log
 for k in 1 2 3; do
-  for m in 0 1; do
-    timeout -k 10 120 python tools/live_probe.py ${LIVEB:-1024} 300 host LPCNET_LPC_EAGER=$m >> gpurun_out/r06_live_ab.log 2>&1 || { echo "live probe rc=$?"; exit 1; }
-    echo "eager=$m" >> gpurun_out/r06_live_ab.log
+  for m in ${LIVE_AB:-LPCNET_LPC_EAGER=0 LPCNET_LPC_EAGER=1}; do
+    timeout -k 10 120 python tools/live_probe.py ${LIVEB:-1024} 300 host $m >> gpurun_out/r06_live_ab.log 2>&1 || { echo "live probe rc=$?"; exit 1; }
+    echo "$m" >> gpurun_out/r06_live_ab.log
   done
 done
 cat gpurun_out/r06_live_ab.log
-for T in ${RT_THREADS:-256 960}; do
+for T in ${RT_THREADS-256 960}; do
   for mode in spread burst; do
     timeout -k 10 120 ./tools/dropin_bench $T 300 rt $mode >> gpurun_out/r06_dropin_rt.jsonl 2>gpurun_out/r06_dropin_rt.err || { echo "dropin rt rc=$?"; cat gpurun_out/r06_dropin_rt.err; exit 1; }
   done
