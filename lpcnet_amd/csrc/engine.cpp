@@ -367,6 +367,7 @@ struct LPCNetBatch {
   short *h_io_pcm = nullptr;
   short *d_io_pcm = nullptr; /* h_io_pcm's device address (mapped) */
   float *d_io_feat = nullptr; /* h_io_feat's device address (mapped) */
+  bool io_feat_vram = false;  /* h_io_feat is host-visible device memory (fine-grained VRAM, large BAR) */
   float *h_stg_feat = nullptr; /* pinned staging of the caller's own buffers */
   short *h_stg_pcm = nullptr;
   hipEvent_t ev_tick = nullptr; /* end of a host-I/O tick (spin-polled) */
@@ -2093,7 +2094,8 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
   (void)hipFree(b->d_lpc);
   (void)hipFree(b->d_lpc_tab);
   (void)hipFree(b->d_chunk);
-  (void)hipHostFree(b->h_io_feat);
+  if (b->io_feat_vram) (void)hipFree(b->h_io_feat);
+  else (void)hipHostFree(b->h_io_feat);
   (void)hipHostFree(b->h_io_pcm);
   (void)hipHostFree(b->h_stg_feat);
   (void)hipHostFree(b->h_stg_pcm);
@@ -2323,8 +2325,24 @@ static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_fe
 static int ensure_host_io(LPCNetBatch *b)
 {
   if (!b->h_io_feat) {
-    HIPCHK(hipHostMalloc(&b->h_io_feat, sizeof(float) * NF * (size_t)b->B, hipHostMallocMapped));
-    HIPCHK(hipHostGetDevicePointer((void **)&b->d_io_feat, b->h_io_feat, 0));
+    /* features: host-visible device memory where the device has a large BAR
+     * (the host's stores cross PCIe as posted writes, the chunk and LPC
+     * kernels then read local HBM: 80 KB at 1024 streams, the chunk kernel's
+     * input phase ~24 K -> ~12 K cycles against reads of mapped host memory),
+     * else mapped pinned host memory.  LPCNET_FEAT_VRAM=0: always the latter. */
+    int large_bar = 0;
+    (void)hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, b->device);
+    const char *ev = getenv("LPCNET_FEAT_VRAM");
+    if (large_bar && !(ev && atoi(ev) == 0) &&
+        hipExtMallocWithFlags((void **)&b->h_io_feat, sizeof(float) * NF * (size_t)b->B, hipDeviceMallocFinegrained) ==
+            hipSuccess) {
+      b->io_feat_vram = true;
+      b->d_io_feat = b->h_io_feat;
+    } else {
+      b->h_io_feat = nullptr;
+      HIPCHK(hipHostMalloc(&b->h_io_feat, sizeof(float) * NF * (size_t)b->B, hipHostMallocMapped));
+      HIPCHK(hipHostGetDevicePointer((void **)&b->d_io_feat, b->h_io_feat, 0));
+    }
   }
   if (!b->h_io_pcm) {
     HIPCHK(hipHostMalloc(&b->h_io_pcm, sizeof(short) * FRAME * (size_t)b->B, hipHostMallocMapped));
@@ -2390,6 +2408,9 @@ static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm
   if (N < 0 || N > FRAME || !features || (N > 0 && !pcm) || preload < 0) { set_err("bad arguments"); return -1; }
   if (b->set_device()) return -1;
   if (ensure_trace(b, N)) return -1;
+  /* the caller's stores into the VRAM feature buffer are write-combined:
+   * drained before any command of this call can read them */
+  if (features == b->h_io_feat && b->io_feat_vram) __builtin_ia32_sfence();
   if (!staged && !pre && single_frame_chunked(b, nB, N, preload)) {
     /* the caller's buffers through pinned staging: both copies truly
      * asynchronous, one synchronisation per frame.  Features already in the
@@ -2404,7 +2425,7 @@ static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm
      * batches take one DMA copy; the caller's buffers: host copy into the
      * cached pinned staging, one DMA copy each way */
     const bool own_feat = features == b->h_io_feat, own_pcm = pcm == b->h_io_pcm;
-    const bool zc_feat = own_feat && nB <= ZC_FEAT_MAX && !getenv("LPCNET_FEAT_DMA");
+    const bool zc_feat = own_feat && (nB <= ZC_FEAT_MAX || b->io_feat_vram) && !getenv("LPCNET_FEAT_DMA");
     if (!own_feat) memcpy(b->h_stg_feat, features, sizeof(float) * NF * nB);
     if (!zc_feat)
       HIPCHK(hipMemcpyAsync(b->d_feat, own_feat ? b->h_io_feat : b->h_stg_feat, sizeof(float) * NF * nB,

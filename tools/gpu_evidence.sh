@@ -21,9 +21,13 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps $STEPS --warmup 2 --no-cpu --no-latency --no-capacity > "$R/gpurun_out/prof.log" 2>&1 || { echo "rocprof trace rc=$?"; exit 1; }
 echo "trace ok"
 # PMC passes: one counter group per run (slot limits, MI355X_MICROARCH.md)
-for cfg in "b1024:--streams 1024" "b256:--streams 256" "b1:--streams 1" "b1_fp32:--streams 1 --variant fp32"; do
+# (b8192 / b32768: the wide kernel, mfw_kernel, that carries the capacity
+# figures; its LDS bank conflicts and wave states as two more passes)
+for cfg in "b1024:--streams 1024" "b256:--streams 256" "b1:--streams 1" "b1_fp32:--streams 1 --variant fp32" "b8192:--streams 8192" "b32768:--streams 32768"; do
   name=${cfg%%:*}; args=${cfg#*:}
-  for pass in "fetch:FETCH_SIZE" "write:WRITE_SIZE" "l2:TCC_HIT_sum TCC_MISS_sum" "mfma:SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" "valu:SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE"; do
+  passes=("fetch:FETCH_SIZE" "write:WRITE_SIZE" "l2:TCC_HIT_sum TCC_MISS_sum" "mfma:SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" "valu:SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE")
+  case $name in b1024|b8192|b32768) passes+=("lds:SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS" "waves:SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU");; esac
+  for pass in "${passes[@]}"; do
     pn=${pass%%:*}; ctr=${pass#*:}
     timeout -s KILL 120 rocprofv3 --pmc $ctr -d "$R/gpurun_out/pmc_${pn}_${name}" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 2 $args --no-cpu --no-batch1 --no-latency --no-capacity > "$R/gpurun_out/pmc_${pn}_${name}.log" 2>&1 || { echo "pmc $pn $name rc=$?"; exit 1; }
   done

@@ -122,6 +122,15 @@ def main(outdir, out):
                 r["valu_issue_frac"] = r["SQ_INSTS_VALU"] / max(1.0, gui / 8 * 256 * 2)
                 if "frames_per_launch" in r:
                     r["valu_insts_per_frame"] = r["SQ_INSTS_VALU"] / r["frames_per_launch"]
+            # LDS bank conflicts per LDS-busy cycle; wave states per wave-cycle
+            if "SQ_LDS_BANK_CONFLICT" in r and r.get("SQ_ACTIVE_INST_LDS"):
+                r["lds_bank_conflict_frac"] = r["SQ_LDS_BANK_CONFLICT"] / r["SQ_ACTIVE_INST_LDS"]
+            if r.get("SQ_WAVE_CYCLES"):
+                wc = r["SQ_WAVE_CYCLES"]
+                r["wave_states"] = {k: r[c] / wc for k, c in (("issuing", "SQ_ACTIVE_INST_ANY"),
+                                                             ("valu", "SQ_ACTIVE_INST_VALU"),
+                                                             ("waiting", "SQ_WAIT_ANY"),
+                                                             ("issue_stalled", "SQ_WAIT_INST_ANY")) if c in r}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
