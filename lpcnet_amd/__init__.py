@@ -473,6 +473,9 @@ class LPCNetBatch:
             if not q:
                 raise LPCNetError(last_error())
             self._hp = _owned_view(self._owner, C.cast(q, C.c_void_p).value, C.c_int16, np.int16, (self.B * FRAME_SIZE,))
+            # the live tick's arguments, resolved once (ctypes attribute
+            # lookups per call are microseconds of host turn-around)
+            self._hf_addr, self._hp_addr = self._hf.ctypes.data, self._hp.ctypes.data
         return self._hf
 
     def synthesize_host(self, n: int = FRAME_SIZE) -> np.ndarray:
@@ -482,11 +485,10 @@ class LPCNetBatch:
         Returns a [B, n] view of that buffer, overwritten by the next call
         (copy it to keep it); the view keeps the batch's pinned memory alive
         past close()."""
-        f = self.host_features()
-        pcm = self._hp[:self.B * n]
-        if lib.lpcnet_batch_synthesize(self._b, f.ctypes.data, pcm.ctypes.data, n) != 0:
+        self.host_features()
+        if lib.lpcnet_batch_synthesize(self._b, self._hf_addr, self._hp_addr, n) != 0:
             raise LPCNetError(last_error())
-        return pcm.reshape(self.B, n)
+        return self._hp[:self.B * n].reshape(self.B, n)
 
     def synthesize_impl(self, features: np.ndarray, pcm: np.ndarray, preload: int) -> np.ndarray:
         """lpcnet_synthesize_impl: pcm [B, N] int16, first ``preload`` samples teacher-forced."""

@@ -3,6 +3,7 @@
  *
  *   dropin_bench <threads> <frames> [pool]
  *   dropin_bench <threads> <frames> rt [burst|spread]
+ *   dropin_bench <streams> <frames> live
  *
  * T pthreads, one LPCNetState each (include/lpcnet.h: lpcnet_create,
  * lpcnet_load_model, lpcnet_synthesize -- the reference's own calling
@@ -22,6 +23,11 @@
  * it returned after its tick's end (a missed deadline: the stream's next
  * frame is late).  One JSON object: latency p50 / p99 / max, misses,
  * coalesced launches.
+ *
+ * "live": the batch API's live tick from C (no Python in the loop): one
+ * LPCNetBatch of <streams>, each frame's features copied into the batch's
+ * own feature buffer (lpcnet_batch_host_features), lpcnet_batch_synthesize
+ * into its own PCM buffer; per-tick wall time mean / p50 / p99.
  */
 #define _POSIX_C_SOURCE 200809L
 #include <pthread.h>
@@ -86,6 +92,51 @@ static int cmpf(const void *x, const void *y)
   return (a > b) - (a < b);
 }
 
+static int live_ticks(int B, int nf)
+{
+  const int len = lpcnet_mi355x_synthetic_model(1, LPCNET_VARIANT_INT8, 0, NULL, 0);
+  unsigned char *m = malloc(len);
+  lpcnet_mi355x_synthetic_model(1, LPCNET_VARIANT_INT8, 0, m, len);
+  LPCNetBatch *b = lpcnet_batch_create(B, 0);
+  if (!b || lpcnet_batch_load_model(b, m, len)) {
+    fprintf(stderr, "batch failed: %s\n", lpcnet_mi355x_last_error());
+    return 1;
+  }
+  const int ND = 16; /* distinct feature frames, cycled */
+  float *all = malloc(sizeof(float) * (size_t)ND * B * NB_FEATURES);
+  float *tmp = malloc(sizeof(float) * (size_t)ND * NB_TOTAL_FEATURES);
+  for (int s = 0; s < B; s++) {
+    lpcnet_mi355x_synthetic_features(s, ND, tmp);
+    for (int f = 0; f < ND; f++)
+      memcpy(&all[((size_t)f * B + s) * NB_FEATURES], &tmp[(size_t)f * NB_TOTAL_FEATURES], sizeof(float) * NB_FEATURES);
+  }
+  float *hf = lpcnet_batch_host_features(b);
+  short *hp = lpcnet_batch_host_pcm(b);
+  const int warm = 20;
+  float *lat = malloc(sizeof(float) * nf);
+  long sum = 0;
+  for (int f = 0; f < warm + nf; f++) {
+    const double a = now();
+    memcpy(hf, &all[(size_t)(f % ND) * B * NB_FEATURES], sizeof(float) * (size_t)B * NB_FEATURES);
+    if (lpcnet_batch_synthesize(b, hf, hp, LPCNET_FRAME_SIZE)) {
+      fprintf(stderr, "synthesize failed: %s\n", lpcnet_mi355x_last_error());
+      return 1;
+    }
+    const double e = now();
+    if (f >= warm) lat[f - warm] = (float)((e - a) * 1e3);
+    sum += hp[0];
+  }
+  double mean = 0;
+  for (int f = 0; f < nf; f++) mean += lat[f];
+  mean /= nf;
+  qsort(lat, nf, sizeof(float), cmpf);
+  printf("{\"streams\": %d, \"ticks\": %d, \"ms_per_tick_mean\": %.5f, \"ms_per_tick_p50\": %.5f, "
+         "\"ms_per_tick_p99\": %.5f, \"samples_per_s\": %.1f, \"check\": %ld}\n",
+         B, nf, mean, lat[nf / 2], lat[(int)(0.99 * (nf - 1))], B * 160.0 / (mean * 1e-3), sum);
+  lpcnet_batch_destroy(b);
+  return 0;
+}
+
 static void *run(void *arg)
 {
   const int t = (int)(size_t)arg;
@@ -105,6 +156,7 @@ int main(int argc, char **argv)
   T = atoi(argv[1]);
   F = atoi(argv[2]);
   if (T < 1 || F < 1) return 2;
+  if (argc > 3 && !strcmp(argv[3], "live")) return live_ticks(T, F);
   blob_len = lpcnet_mi355x_synthetic_model(1, LPCNET_VARIANT_INT8, 0, NULL, 0);
   blob = malloc(blob_len);
   lpcnet_mi355x_synthetic_model(1, LPCNET_VARIANT_INT8, 0, blob, blob_len);
