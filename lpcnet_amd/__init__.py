@@ -152,7 +152,7 @@ class ModelInfo(C.Structure):
         if self.quad_path == 6:
             return f"mf2_kernel<4, {lr}, {hw}>"
         if self.quad_path == 7:
-            return f"mfw_kernel<true, {self.streams_per_workgroup // 4}>"
+            return f"mfw_kernel<true, {self.streams_per_workgroup // 4}, {lr}>"
         if self.quad_path == 5:
             return f"fp_kernel<0, {lr}, {hw}>"
         quad = "true" if self.quad_path == 1 else "false"

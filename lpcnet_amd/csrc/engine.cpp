@@ -520,7 +520,9 @@ void choose_kernel(LPCNetBatch *b)
      * LPCNET_MFW_G=2/3 forces the group count) */
     b->cus = current_device_cus();
     const int gauto = mfw_groups(b->B, b->cus);
-    const bool mfw_ok = !b->sa.mf_split && b->sa.rcp_hw;
+    /* split models: the wide kernel's own split form where its tables exist
+     * (mfw_split_tables), two groups only (LDS) */
+    const bool mfw_ok = (!b->sa.mf_split || b->sa.mfw_split) && b->sa.rcp_hw;
     const char *ew = getenv("LPCNET_MFW");
     const bool wantw = ew ? atoi(ew) != 0 : gauto > 0;
     b->mfw_forced = ew && atoi(ew) != 0;
@@ -533,12 +535,12 @@ void choose_kernel(LPCNetBatch *b)
       b->info.lds_bytes = mf2_lds_bytes(4, b->sa.mf_split);
       b->info.quad_path = 6;
       const char *eg = getenv("LPCNET_MFW_G");
-      b->mfw_g = eg ? (atoi(eg) == 2 ? 2 : 3) : (gauto ? gauto : 2);
-      if (wantw && mfw_ok && mfw_lds_bytes(b->mfw_g) <= 160 * 1024) {
+      b->mfw_g = b->sa.mf_split ? 2 : eg ? (atoi(eg) == 2 ? 2 : 3) : (gauto ? gauto : 2);
+      if (wantw && mfw_ok && mfw_lds_bytes(b->mfw_g, b->sa.mf_split) <= 160 * 1024) {
         b->mfw = true;
         b->info.mfma_ops_per_group_sample = b->mfw_g * (b->mf_ga_ops + b->mf_gb_ops);
         b->info.streams_per_workgroup = 4 * b->mfw_g;
-        b->info.lds_bytes = mfw_lds_bytes(b->mfw_g);
+        b->info.lds_bytes = mfw_lds_bytes(b->mfw_g, b->sa.mf_split);
         b->info.quad_path = 7;
       }
     }
@@ -847,6 +849,112 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
     if (4 * (P.nzr[w] + P.nfzr[w]) > MF_ZMAX || 4 * (P.nh[w] + P.nfh[w]) > MF_HMAX) return -1;
   }
   return best;
+}
+
+/* mfw_kernel's split form (trained Sparsify masks on the wide kernel): the
+ * six R waves keep the unit blocks of `perm` (the batch's main plan, so the
+ * E waves' lane-ordered tables stay valid) up to the full register caps
+ * (16 z/r, 32 h blocks: the unsplit kernel's largest tables), and every
+ * block beyond goes, in pieces of at most those caps, to the 16 lane groups
+ * of two host waves (MFW_H_WAVES): one piece per host lane group and gate,
+ * longest pieces first, dealt alternately to the two waves.  A host lane's
+ * int32 partial sums reach its row's owner through LDS adds into a compact
+ * part area: per gate, the unit blocks with pieces (at most 16) take part
+ * rows 8 slot .. 8 slot + 7.  Exact int32 sums in any order: bit-identical
+ * to the unsplit product.  Tables: [MFW_TAB_WAVES][MF_LANE_U32][64] as the
+ * mf tables (host waves: their piece at slot 0 of each gate), frow
+ * [3][SAMPLE_THREADS + 128]: an E thread's part row | 1 << 16 when its unit
+ * has pieces (else MFW_NOROW), a host lane's target part row (else
+ * MFW_NOROW).  False when a gate needs more than 16 pieces. */
+struct MfwSplitTab {
+  int nzr[MFW_TAB_WAVES] = {}, nh[MFW_TAB_WAVES] = {};
+  std::vector<uint32_t> tab;
+  std::vector<int> frow;
+};
+
+static bool mfw_split_tables(const std::vector<std::vector<int>> &ga, const std::vector<int> &perm,
+                             const std::vector<int> &ga_first, const int8_t *wa, MfwSplitTab &T)
+{
+  constexpr int NUB = NA / 8, NHL = 8 * MFW_H_WAVES;
+  const int cap[3] = {MF_ZMAX, MF_ZMAX, MF_HMAX};
+  std::vector<MfPiece> pcs[3];
+  std::vector<int> host[3]; /* host lane group (0..15) -> piece index */
+  std::vector<int> slot_of_ub[3];
+  for (int g = 0; g < 3; g++) {
+    for (int u = 0; u < NUB; u++) {
+      const int K = (int)ga[g * NUB + u].size();
+      for (int t0 = cap[g]; t0 < K; t0 += cap[g]) pcs[g].push_back(MfPiece{u, t0, std::min(K, t0 + cap[g])});
+    }
+    if ((int)pcs[g].size() > NHL) return false;
+    std::stable_sort(pcs[g].begin(), pcs[g].end(), [](const MfPiece &a, const MfPiece &b) { return a.t1 - a.t0 > b.t1 - b.t0; });
+    host[g].assign(NHL, -1);
+    for (int k = 0; k < (int)pcs[g].size(); k++) host[g][(k % MFW_H_WAVES) * 8 + k / MFW_H_WAVES] = k;
+    slot_of_ub[g].assign(NUB, -1);
+    int ns = 0;
+    for (const MfPiece &pc : pcs[g])
+      if (slot_of_ub[g][pc.unit] < 0) slot_of_ub[g][pc.unit] = ns++;
+    if (ns > 16) return false;
+  }
+  T.tab.assign((size_t)MFW_TAB_WAVES * MF_LANE_U32 * 64, 0);
+  T.frow.assign((size_t)3 * (SAMPLE_THREADS + NHL), MFW_NOROW);
+  for (int w = 0; w < MFW_TAB_WAVES; w++) {
+    const bool hw = w >= SAMPLE_WAVES;
+    /* this wave's rows per lane group and gate: (row block, first, end) */
+    int rb[8][3], t0[8][3], t1[8][3];
+    int kz = 1, kh = 1; /* at least one slot group (zero weights: exact) */
+    for (int j = 0; j < 8; j++)
+      for (int g = 0; g < 3; g++) {
+        rb[j][g] = -1;
+        t0[j][g] = t1[j][g] = 0;
+        if (!hw) {
+          const int u = perm[w * 8 + j];
+          rb[j][g] = g * NUB + u;
+          t1[j][g] = std::min((int)ga[rb[j][g]].size(), cap[g]);
+        } else if (host[g][(w - SAMPLE_WAVES) * 8 + j] >= 0) {
+          const MfPiece &pc = pcs[g][host[g][(w - SAMPLE_WAVES) * 8 + j]];
+          rb[j][g] = g * NUB + pc.unit;
+          t0[j][g] = pc.t0;
+          t1[j][g] = pc.t1;
+          for (int r = 0; r < 8; r++)
+            T.frow[(size_t)g * (SAMPLE_THREADS + NHL) + SAMPLE_THREADS + (w - SAMPLE_WAVES) * 64 + 8 * j + r] =
+                8 * slot_of_ub[g][pc.unit] + r;
+        }
+        (g < 2 ? kz : kh) = std::max(g < 2 ? kz : kh, t1[j][g] - t0[j][g]);
+      }
+    T.nzr[w] = (kz + 3) / 4;
+    T.nh[w] = (kh + 3) / 4;
+    auto word = [&](int k, int l) -> uint32_t & { return T.tab[((size_t)w * MF_LANE_U32 + k) * 64 + l]; };
+    for (int g = 0; g < 3; g++) {
+      const int base = g == 0 ? 0 : (g == 1 ? MF_ZMAX : 2 * MF_ZMAX);
+      const int nslot = 4 * (g < 2 ? T.nzr[w] : T.nh[w]);
+      for (int half = 0; half < 2; half++) {
+        std::vector<int> lists[4];
+        for (int k = 0; k < 4; k++) {
+          const int j = 4 * half + k;
+          if (rb[j][g] >= 0) lists[k].assign(ga[rb[j][g]].begin() + t0[j][g], ga[rb[j][g]].begin() + t1[j][g]);
+        }
+        const std::vector<int> *rows4[4] = {&lists[0], &lists[1], &lists[2], &lists[3]};
+        int slot_of[4][MF_HMAX], cb_at[4][MF_HMAX];
+        mf_bank_slots(rows4, nslot, slot_of, cb_at);
+        for (int k = 0; k < 4; k++) {
+          const int j = 4 * half + k;
+          for (int r = 0; r < 8; r++) {
+            const int l = 8 * j + r;
+            for (int t = 0; t < (int)lists[k].size(); t++)
+              memcpy(&word(base + slot_of[k][t], l), wa + 32 * (ga_first[rb[j][g]] + t0[j][g] + t) + 4 * r, 4);
+            for (int t = 0; t < nslot; t++) word(MF_GA + (base + t) / 4, l) |= (uint32_t)cb_at[k][t] << (8 * ((base + t) & 3));
+          }
+        }
+      }
+    }
+  }
+  /* the E threads' merge entries: thread t owns unit 8 perm[t / 8] + t % 8 */
+  for (int g = 0; g < 3; g++)
+    for (int t = 0; t < SAMPLE_THREADS; t++) {
+      const int u = perm[t / 8], sl = slot_of_ub[g][u];
+      if (sl >= 0) T.frow[(size_t)g * (SAMPLE_THREADS + NHL) + t] = (8 * sl + (t % 8)) | 1 << 16;
+    }
+  return true;
 }
 
 /* cls: the kernel the plan serves.  1: mf_kernel at 4 streams per
@@ -1273,6 +1381,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     fprintf(stderr, "\n");
   }
   std::vector<int> mf_units, mf_frow;
+  MfwSplitTab mfw_tabs;
   if (mf_ok) {
     const int8_t *wa = (const int8_t *)gaw->data, *wb = (const int8_t *)gbw, *wr = (const int8_t *)gbrec;
     /* GRU_A: lane l of wave w = row l%8 of unit block perm[8w + l/8] of each
@@ -1344,6 +1453,16 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
       for (const MfPiece &pc : plan.pieces[g]) has[pc.unit] = 1;
       for (int t = 0; t < SAMPLE_WAVES * 64; t++)
         if (has[mf_units[t] / 8]) mf_frow[(size_t)g * SAMPLE_WAVES * 64 + t] |= 1 << 16;
+    }
+    /* the wide kernel's split form (wide batches of split models) */
+    sa.mfw_split = 0;
+    if (plan.split && b->plan_wide && !getenv("LPCNET_NO_MFW_SPLIT") &&
+        mfw_split_tables(ga_blocks, perm, ga_first, wa, mfw_tabs)) {
+      sa.mfw_split = 1;
+      for (int w = 0; w < MFW_TAB_WAVES; w++) {
+        sa.mfw_nzr[w] = mfw_tabs.nzr[w];
+        sa.mfw_nh[w] = mfw_tabs.nh[w];
+      }
     }
     /* GRU_B: dense A tiles, lane l = row 16g + l%16, k = 64kt + 16(l/16) + byte */
     std::vector<int8_t> dense((size_t)GB_ROWS * NA, 0), drec((size_t)GB_ROWS * NB, 0);
@@ -1601,6 +1720,10 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     UP(sa.mf, mft.data(), mft.size() * 4);
     UP(sa.mf_unit, mf_units.data(), mf_units.size() * 4);
     UP(sa.mf_frow, mf_frow.data(), mf_frow.size() * 4);
+    if (sa.mfw_split) {
+      UP(sa.mfw_tab, mfw_tabs.tab.data(), mfw_tabs.tab.size() * 4);
+      UP(sa.mfw_frow, mfw_tabs.frow.data(), mfw_tabs.frow.size() * 4);
+    }
     {
       /* Range of the GRU_A gates' inputs for the elementwise fast path:
        * z/r: cvt_rne((bias + diag st + ((cond + Esig) + Epred) + Eexc) * 16256)

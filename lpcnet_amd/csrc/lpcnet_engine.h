@@ -51,6 +51,12 @@ constexpr int MF_ZMAX = 16;         /* z / r slots per lane */
 constexpr int MF_HMAX = 32;         /* h slots per lane */
 constexpr int MF_GA = 2 * MF_ZMAX + MF_HMAX;
 constexpr int MF_LANE_U32 = MF_GA + MF_GA / 4; /* 80 */
+/* mfw_kernel split form (engine.cpp mfw_split_tables): two host waves after
+ * the six R waves carry the pieces of block rows beyond the register caps */
+constexpr int MFW_H_WAVES = 2;
+constexpr int MFW_TAB_WAVES = 6 + MFW_H_WAVES; /* SAMPLE_WAVES R waves + the host waves */
+constexpr int MFW_NOROW = 0x1FF;               /* frow entry: no part row */
+constexpr int MFW_PART_ROWS = 128;             /* part rows per gate: 16 unit blocks x 8 */
 constexpr int MF_GB_IN = 3 * 6;                 /* GRU_B input tiles (3 gates x 6 K tiles) */
 constexpr int MF_GB_TILES = MF_GB_IN + 3;        /* + the 3 recurrent tiles */
 constexpr int MF_XSTR = 416;        /* LDS bytes per stream of the quantized GRU_A state (stream-major):
@@ -242,6 +248,14 @@ struct SampleArgs {
   int mf_nfzr[SAMPLE_WAVES];
   int mf_nfh[SAMPLE_WAVES];
   const int *mf_frow;
+  /* mfw_kernel's split form: [MFW_TAB_WAVES][MF_LANE_U32][64] tables (R
+   * waves own rows to the full caps, host waves the pieces), group counts,
+   * frow [3][SAMPLE_THREADS + 64 MFW_H_WAVES] (see mfw_split_tables) */
+  int mfw_split;
+  const uint32_t *mfw_tab;
+  const int *mfw_frow;
+  int mfw_nzr[MFW_TAB_WAVES];
+  int mfw_nh[MFW_TAB_WAVES];
   const uint4 *mf_gb;
   const float4 *fp_zr, *fp_h, *fp_gb; /* fp_kernel tables (see FP_ZF) */
   const uint32_t *fp_off;
@@ -361,7 +375,7 @@ int launch_mf2(const SampleArgs &a, int S, void *stream);
 constexpr double MFW_G3_PHASE = 1.08; /* 1.04 before two groups took the LDS rcpps table (-3.4 %) */
 /* 0 (batch within one mf_kernel<4> round), 2 or 3 */
 int mfw_groups(int B, int cus);
-int mfw_lds_bytes(int groups);
+int mfw_lds_bytes(int groups, int split = 0);
 int launch_mfw(const SampleArgs &a, int groups, void *stream);
 /* fp32 latency kernel: one stream per workgroup, LDS flags instead of
  * workgroup barriers (fp32 models within the FP_* limits, dense GRU_B). */

@@ -49,6 +49,9 @@ namespace lpcnet_mi355x {
 
 constexpr int MFW_S = 4;                 /* streams per group */
 constexpr int MFW_THREADS = 64 * 14;     /* 6 E + 2 S + 6 R waves */
+constexpr int MFW_THREADS_SPLIT = 64 * 16; /* split form: + 2 host waves (MFW_H_WAVES) */
+/* split form: the host waves' partial sums [phase parity][gate][MFW_PART_ROWS][S] */
+constexpr int MFW_PRT = 2 * 3 * MFW_PART_ROWS * MFW_S * 4;
 constexpr int MFW_S_WAVE0 = 6, MFW_R_WAVE0 = 8;
 
 /* MFW_G groups of MFW_S streams per workgroup (2 or 3, see the header) */
@@ -80,7 +83,14 @@ static_assert(MfwLds<3>::total + MFW_IMG <= 160 * 1024, "mfw_kernel LDS");
  * streams per lane) instead of the hardware reciprocal */
 static_assert(MfwLds<2>::total + IMG_VAR <= 160 * 1024, "mfw_kernel LDS (two groups, table)");
 
-int mfw_lds_bytes(int groups) { return groups == 2 ? MfwLds<2>::total + IMG_VAR : MfwLds<3>::total + MFW_IMG; }
+/* split form (two groups): the part area instead of the rcpps table */
+static_assert(MfwLds<2>::total + MFW_PRT + MFW_IMG <= 160 * 1024, "mfw_kernel LDS (two groups, split)");
+
+int mfw_lds_bytes(int groups, int split)
+{
+  if (split) return groups == 2 ? MfwLds<2>::total + MFW_PRT : 1 << 30;
+  return groups == 2 ? MfwLds<2>::total + IMG_VAR : MfwLds<3>::total + MFW_IMG;
+}
 
 template <int G>
 __device__ __forceinline__ int modg(int p) { return (p % G + G) % G; }
@@ -229,13 +239,17 @@ __device__ __forceinline__ void mfw_zr(const unsigned char *xg, const uint32_t (
 }
 
 /* ---- R role: GRU_A recurrent products (nnet.c:441) ------------------------ */
-template <int MFW_G, int Z, int H>
-__device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *xa, int *trm, int r, int lane, int total)
+/* HOST (split form, r = 6, 7: the host waves): the lane's piece of another
+ * unit's row, accumulated from 0, its int32 partial sums added into that
+ * row's part words (prt) instead of stored to trm */
+template <int MFW_G, int Z, int H, bool SPLIT = false, bool HOST = false>
+__device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *xa, int *trm, int r, int lane, int total,
+                                           int *prt = nullptr)
 {
   /* this lane's weight words and packed column quads (engine.cpp mf tables:
    * z slots 0..15, r 16..31, h 32..63, quads 4 per word after them) */
   uint32_t wz[4 * Z], wr[4 * Z], wh[4 * H], cz[Z], cr[Z], ch[H];
-  const uint32_t *mt = A.mf + (size_t)r * MF_LANE_U32 * 64 + lane;
+  const uint32_t *mt = (SPLIT ? A.mfw_tab : A.mf) + (size_t)r * MF_LANE_U32 * 64 + lane;
 #pragma unroll
   for (int t = 0; t < 4 * Z; t++) {
     wz[t] = mt[t * 64];
@@ -250,8 +264,18 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
   }
 #pragma unroll
   for (int k = 0; k < H; k++) ch[k] = mt[(MF_GA + 2 * MF_ZMAX / 4 + k) * 64];
-  const int i = A.mf_unit[r * 64 + lane];
-  const int wsz = A.ga_wsum[i], wsr = A.ga_wsum[NA + i], wsh = A.ga_wsum[2 * NA + i];
+  int wsz = 0, wsr = 0, wsh = 0;
+  uint32_t tgt = 0; /* HOST: part rows of the lane's pieces, 9 bits per gate */
+  if constexpr (HOST) {
+    const int *fr = A.mfw_frow + SAMPLE_THREADS + (r - SAMPLE_WAVES) * 64 + lane;
+    constexpr int FS = SAMPLE_THREADS + 64 * MFW_H_WAVES;
+    tgt = (uint32_t)fr[0] | (uint32_t)fr[FS] << 9 | (uint32_t)fr[2 * FS] << 18;
+  } else {
+    const int i = A.mf_unit[r * 64 + lane];
+    wsz = A.ga_wsum[i];
+    wsr = A.ga_wsum[NA + i];
+    wsh = A.ga_wsum[2 * NA + i];
+  }
   /* A operand of lane 4b+m = stream m of the group */
   const uint32_t mo = (uint32_t)(lane & 3) * MF_XSTR;
   const int row = r * 64 + lane;
@@ -280,23 +304,41 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
     v4i vz = {wsz, wsz, wsz, wsz}, vr = {wsr, wsr, wsr, wsr}, vh[1] = {{wsh, wsh, wsh, wsh}};
     mfw_zr<Z>(xg, wz, wr, cz, cr, mo, vz, vr);
     mfw_gate<H, 1>(xg, wh, ch, mo, vh);
-    /* the sums' LDS address from an opaque row (not hoisted per parity) */
-    int rq = row;
-    asm volatile("" : "+v"(rq));
-    int *tp = trm + (p & 1) * 3 * SAMPLE_THREADS * MFW_S + rq * MFW_S;
-    *(int4 *)&tp[0 * SAMPLE_THREADS * MFW_S] = make_int4(vz[0], vz[1], vz[2], vz[3]);
-    *(int4 *)&tp[1 * SAMPLE_THREADS * MFW_S] = make_int4(vr[0], vr[1], vr[2], vr[3]);
-    *(int4 *)&tp[2 * SAMPLE_THREADS * MFW_S] = make_int4(vh[0][0], vh[0][1], vh[0][2], vh[0][3]);
+    if constexpr (HOST) {
+      /* exact int32 LDS adds into the owners' part words (one piece per
+       * lane and gate; lanes without a piece skip) */
+      uint32_t tq = tgt;
+      asm volatile("" : "+v"(tq));
+      int *pp = prt + (p & 1) * 3 * MFW_PART_ROWS * MFW_S;
+      const int t3[3] = {(int)(tq & 0x1FF), (int)((tq >> 9) & 0x1FF), (int)((tq >> 18) & 0x1FF)};
+      const v4i vv[3] = {vz, vr, vh[0]};
+#pragma unroll
+      for (int q = 0; q < 3; q++)
+        if (t3[q] != MFW_NOROW)
+#pragma unroll
+          for (int s = 0; s < MFW_S; s++) atomicAdd(&pp[(q * MFW_PART_ROWS + t3[q]) * MFW_S + s], vv[q][s]);
+    } else {
+      /* the sums' LDS address from an opaque row (not hoisted per parity) */
+      int rq = row;
+      asm volatile("" : "+v"(rq));
+      int *tp = trm + (p & 1) * 3 * SAMPLE_THREADS * MFW_S + rq * MFW_S;
+      *(int4 *)&tp[0 * SAMPLE_THREADS * MFW_S] = make_int4(vz[0], vz[1], vz[2], vz[3]);
+      *(int4 *)&tp[1 * SAMPLE_THREADS * MFW_S] = make_int4(vr[0], vr[1], vr[2], vr[3]);
+      *(int4 *)&tp[2 * SAMPLE_THREADS * MFW_S] = make_int4(vh[0][0], vh[0][1], vh[0][2], vh[0][3]);
+    }
   }
   __syncthreads(); /* final */
   MFW_STAMP_PRINT("R");
 }
 
-template <bool HWR, int MFW_G>
-__global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
+template <bool HWR, int MFW_G, bool SPLIT = false>
+__global__ __launch_bounds__(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS) void mfw_kernel(SampleArgs A)
 {
-  /* the rcpps table in LDS for the E waves (two groups; see mfw_lds_bytes) */
-  constexpr bool TAB = MFW_G == 2 && MFW_TAB;
+  /* the rcpps table in LDS for the E waves (two groups, unsplit; see
+   * mfw_lds_bytes: the split form's part area takes its room) */
+  constexpr bool TAB = MFW_G == 2 && MFW_TAB && !SPLIT;
+  constexpr int NT = SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS;
+  static_assert(!SPLIT || MFW_G == 2, "split form: two groups");
   static_assert(HWR, "mfw_kernel: hardware reciprocal only (no rcpps table in LDS)");
   static_assert(MFW_G == 2 || MFW_G == 3, "two or three groups");
   extern __shared__ uint4 lds4[];
@@ -318,6 +360,7 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
   v4i *gbw = (v4i *)(okw + 2 * MFW_G * 8);
   uint32_t *sst = (uint32_t *)(gbw + MF_GB_TILES * 64);
   short *pcms = (short *)(sst + MFW_GS * 8);
+  int *prt = (int *)((unsigned char *)pcms + L::pcm); /* split form only (MFW_PRT bytes) */
   constexpr int IMG0 = TAB ? 0 : IMG_ULAW; /* first image byte held in LDS */
   __shared__ uint4 img_s[(IMG_VAR - IMG0) / 16];
   const unsigned char *img = (const unsigned char *)img_s - IMG0; /* section offsets as in the full image */
@@ -354,20 +397,39 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
     if (bad && tid == 0 && A.status) A.status[0] = STATUS_ACTIVITY; /* plain vector store to the pinned host word */
   }
   if (!any || bad) {
-    for (int e = tid; e < MFW_GS * total; e += MFW_THREADS) {
+    for (int e = tid; e < MFW_GS * total; e += NT) {
       const int s = e / total, fn = e % total, f = fn / A.N, n = fn % A.N;
       if (s0 + s < A.nstreams) A.pcm[((size_t)f * A.nstreams + s0 + s) * A.N + n] = 0;
     }
     return;
   }
-  for (int o = tid; o < (IMG_VAR - IMG0) / 16; o += MFW_THREADS) img_s[o] = A.image[IMG0 / 16 + o];
+  for (int o = tid; o < (IMG_VAR - IMG0) / 16; o += NT) img_s[o] = A.image[IMG0 / 16 + o];
 
   if (wv >= MFW_R_WAVE0) {
     /* ======================= R role ====================================== */
     const int r = wv - MFW_R_WAVE0;
-    switch (A.mf_nzr[r] * 16 + A.mf_nh[r]) {
+    if constexpr (SPLIT) {
+      if (r >= SAMPLE_WAVES) {
+        /* ===================== host waves (split form) ===================== */
+        switch (A.mfw_nzr[r] * 16 + A.mfw_nh[r]) {
+#define MFW_HCASE(Z, H) \
+  case Z * 16 + H: mfw_r_role<MFW_G, Z, H, true, true>(A, xa, trm, r, lane, total, prt); break;
+#define MFW_HCASES(Z) MFW_HCASE(Z, 1) MFW_HCASE(Z, 2) MFW_HCASE(Z, 3) MFW_HCASE(Z, 4) MFW_HCASE(Z, 5) MFW_HCASE(Z, 6) MFW_HCASE(Z, 7) MFW_HCASE(Z, 8)
+          MFW_HCASES(1)
+          MFW_HCASES(2)
+          MFW_HCASES(3)
+          MFW_HCASES(4)
+#undef MFW_HCASES
+#undef MFW_HCASE
+          default: mfw_r_role<MFW_G, MF_ZMAX / 4, MF_HMAX / 4, true, true>(A, xa, trm, r, lane, total, prt); break;
+        }
+        return;
+      }
+    }
+    const int *nzr_ = SPLIT ? A.mfw_nzr : A.mf_nzr, *nh_ = SPLIT ? A.mfw_nh : A.mf_nh;
+    switch (nzr_[r] * 16 + nh_[r]) {
 #define MFW_CASE(Z, H) \
-  case Z * 16 + H: mfw_r_role<MFW_G, Z, H>(A, xa, trm, r, lane, total); break;
+  case Z * 16 + H: mfw_r_role<MFW_G, Z, H, SPLIT>(A, xa, trm, r, lane, total); break;
 #define MFW_CASES(Z) MFW_CASE(Z, 1) MFW_CASE(Z, 2) MFW_CASE(Z, 3) MFW_CASE(Z, 4) MFW_CASE(Z, 5) MFW_CASE(Z, 6) MFW_CASE(Z, 7) MFW_CASE(Z, 8)
       MFW_CASES(1)
       MFW_CASES(2)
@@ -375,7 +437,7 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
       MFW_CASES(4)
 #undef MFW_CASES
 #undef MFW_CASE
-      default: mfw_r_role<MFW_G, MF_ZMAX / 4, MF_HMAX / 4>(A, xa, trm, r, lane, total); break;
+      default: mfw_r_role<MFW_G, MF_ZMAX / 4, MF_HMAX / 4, SPLIT>(A, xa, trm, r, lane, total); break;
     }
     return;
   }
@@ -410,6 +472,17 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
     };
 #pragma unroll
     for (int g = 0; g < MFW_G; g++) stage(g, A.cond, 0);
+    /* split form: this thread's part rows (9 bits per gate) and whether its
+     * unit has pieces there (bits 27..29), one register for the launch */
+    uint32_t frow = 0;
+    if constexpr (SPLIT) {
+      constexpr int FS = SAMPLE_THREADS + 64 * MFW_H_WAVES;
+      const int *fro = A.mfw_frow + tid;
+      const uint32_t e0 = fro[0], e1 = fro[FS], e2 = fro[2 * FS];
+      frow = (e0 & 0x1FF) | (e1 & 0x1FF) << 9 | (e2 & 0x1FF) << 18 | (e0 >> 16 & 1) << 27 | (e1 >> 16 & 1) << 28 |
+             (e2 >> 16 & 1) << 29;
+      for (int e = tid; e < MFW_PRT / 4; e += SAMPLE_THREADS) prt[e] = 0;
+    }
     __syncthreads(); /* image in LDS */
 #pragma unroll
     for (int g = 0; g < MFW_G; g++)
@@ -457,7 +530,27 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
       const int4 iz = *(const int4 *)&tp[(0 * SAMPLE_THREADS + tid) * S];
       const int4 ir = *(const int4 *)&tp[(1 * SAMPLE_THREADS + tid) * S];
       const int4 ih = *(const int4 *)&tp[(2 * SAMPLE_THREADS + tid) * S];
-      const int vz[4] = {iz.x, iz.y, iz.z, iz.w}, vr[4] = {ir.x, ir.y, ir.z, ir.w}, vh[4] = {ih.x, ih.y, ih.z, ih.w};
+      int vz[4] = {iz.x, iz.y, iz.z, iz.w}, vr[4] = {ir.x, ir.y, ir.z, ir.w}, vh[4] = {ih.x, ih.y, ih.z, ih.w};
+      if constexpr (SPLIT) {
+        /* the host waves' partial sums of this unit's rows (same phase
+         * parity as the R waves' sums), read then cleared for the next use
+         * of the parity; exact int32 adds */
+        uint32_t fp = frow;
+        asm volatile("" : "+v"(fp));
+        int *pp = prt + ((p - 1) & 1) * 3 * MFW_PART_ROWS * S;
+        int *vg[3] = {vz, vr, vh};
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+          if (fp >> (27 + q) & 1) {
+            int *w4 = pp + (q * MFW_PART_ROWS + (int)((fp >> (9 * q)) & 0x1FF)) * S;
+            const int4 t = *(const int4 *)w4;
+            vg[q][0] += t.x;
+            vg[q][1] += t.y;
+            vg[q][2] += t.z;
+            vg[q][3] += t.w;
+            *(int4 *)w4 = make_int4(0, 0, 0, 0);
+          }
+      }
       float az[S], ar[S], tz[S], tr[S], hpre[S];
 #pragma unroll
       for (int s = 0; s < S; s++) {
@@ -757,19 +850,26 @@ __global__ __launch_bounds__(MFW_THREADS) void mfw_kernel(SampleArgs A)
   }
 }
 
-template <int G>
+template <int G, bool SPLIT = false>
 static int launch_mfw_g(const SampleArgs &a, void *stream)
 {
   using L = MfwLds<G>;
-  if (ensure_dyn_lds((const void *)mfw_kernel<true, G>, L::total)) return -1;
+  const int bytes = L::total + (SPLIT ? MFW_PRT : 0);
+  if (ensure_dyn_lds((const void *)mfw_kernel<true, G, SPLIT>, bytes)) return -1;
   const int grid = (a.nstreams + L::MFW_GS - 1) / L::MFW_GS;
-  hipLaunchKernelGGL((mfw_kernel<true, G>), dim3(grid), dim3(MFW_THREADS), L::total, (hipStream_t)stream, a);
+  hipLaunchKernelGGL((mfw_kernel<true, G, SPLIT>), dim3(grid), dim3(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS), bytes,
+                     (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_mfw(const SampleArgs &a, int groups, void *stream)
 {
-  if (!a.rcp_hw || a.mf_split || a.preload || a.trace_logits || a.stamps) return -1;
+  if (!a.rcp_hw || a.preload || a.trace_logits || a.stamps) return -1;
+  if (a.mf_split) {
+    /* split models: the host-wave form, two groups, where its tables exist */
+    if (!a.mfw_split || groups != 2) return -1;
+    return launch_mfw_g<2, true>(a, stream);
+  }
   if (groups == 2) return launch_mfw_g<2>(a, stream);
   if (groups == 3) return launch_mfw_g<3>(a, stream);
   return -1;

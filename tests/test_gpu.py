@@ -791,7 +791,7 @@ def test_wide_kernel_matches_oracle(require_gpu, monkeypatch, groups, B, F):
     monkeypatch.setenv("LPCNET_MFW", "1")
     monkeypatch.setenv("LPCNET_MFW_G", str(groups))
     b = L.LPCNetBatch(B, 0, blob)
-    assert b.info().quad_path == 7 and b.info().kernel_name == f"mfw_kernel<true, {groups}>"
+    assert b.info().quad_path == 7 and b.info().kernel_name == f"mfw_kernel<true, {groups}, false>"
     got = np.stack([b.synthesize(allf[f]) for f in range(F)], 1)
     b.reset()
     d_f = b.device_alloc(allf.nbytes)
@@ -880,3 +880,49 @@ def test_host_views_outlive_close(require_gpu):
     del pcm, hf
     gc.collect()
     assert owner() is None  # destroyed with the last view
+
+
+@pytest.mark.parametrize("B,F", [(8, 3), (2049, 3), (4100, 4), (8192, 2)])
+def test_wide_kernel_split_form_matches_oracle(require_gpu, monkeypatch, B, F):
+    """Trained-like (Sparsify, skewed) masks on the wide kernel: mfw_kernel's
+    split form (block rows beyond the register caps in pieces on two host
+    waves, their int32 partial sums merged through LDS adds) -- every stream
+    equals mf2_kernel's split form (LPCNET_NO_MFW_SPLIT=1), host-I/O and
+    device-resident multi-frame launches agree, sampled streams equal the
+    oracle; one workgroup (forced), ragged (2049, 4100) and 8192 streams."""
+    blob = L.synthetic_model(1, 0, skewed=True)
+    allf = np.stack([feats(s, F) for s in range(B)], 1)
+    if B < 1024:
+        monkeypatch.setenv("LPCNET_MF2", "1")
+        monkeypatch.setenv("LPCNET_MFW", "1")
+    b = L.LPCNetBatch(B, 0, blob)
+    info = b.info()
+    assert info.quad_path == 7 and info.long_rows == 1 and info.kernel_name == "mfw_kernel<true, 2, true>"
+    got = np.stack([b.synthesize(allf[f]) for f in range(F)], 1)
+    b.reset()
+    d_f = b.device_alloc(allf.nbytes)
+    d_p = b.device_alloc(F * B * 160 * 2)
+    b.h2d(d_f, np.ascontiguousarray(allf))
+    b.synthesize_frames(None, d_f, d_p, F)
+    b.sync()
+    dev = np.zeros((F, B, 160), np.int16)
+    b.d2h(dev, d_p)
+    b.device_free(d_f)
+    b.device_free(d_p)
+    st = b.get_state(B - 1)
+    b.close()
+    assert np.array_equal(dev.transpose(1, 0, 2), got)
+    monkeypatch.setenv("LPCNET_NO_MFW_SPLIT", "1")
+    b2 = L.LPCNetBatch(B, 0, blob)
+    assert b2.info().quad_path in (4, 6)
+    ref = np.stack([b2.synthesize(allf[f]) for f in range(F)], 1)
+    b2.reset()
+    for f in range(F):
+        b2.synthesize(allf[f])
+    st2 = b2.get_state(B - 1)
+    b2.close()
+    assert np.array_equal(got, ref)
+    assert np.array_equal(st["gru_a_state"].view(np.uint32), st2["gru_a_state"].view(np.uint32))
+    for s in sorted(x for x in {0, 5, B // 2, B - 1} if x < B):
+        o = O.Oracle(blob, 0)
+        assert np.array_equal(got[s], np.stack([o.synthesize(allf[f, s]) for f in range(F)])), s
