@@ -875,7 +875,7 @@ struct MfwSplitTab {
 static bool mfw_split_tables(const std::vector<std::vector<int>> &ga, const std::vector<int> &perm,
                              const std::vector<int> &ga_first, const int8_t *wa, MfwSplitTab &T)
 {
-  constexpr int NUB = NA / 8, NHL = 8 * MFW_H_WAVES;
+  constexpr int NUB = NA / 8, NHL = 8 * MFW_H_WAVES, FS = SAMPLE_THREADS + 64 * MFW_H_WAVES;
   const int cap[3] = {MF_ZMAX, MF_ZMAX, MF_HMAX};
   std::vector<MfPiece> pcs[3];
   std::vector<int> host[3]; /* host lane group (0..15) -> piece index */
@@ -896,7 +896,7 @@ static bool mfw_split_tables(const std::vector<std::vector<int>> &ga, const std:
     if (ns > 16) return false;
   }
   T.tab.assign((size_t)MFW_TAB_WAVES * MF_LANE_U32 * 64, 0);
-  T.frow.assign((size_t)3 * (SAMPLE_THREADS + NHL), MFW_NOROW);
+  T.frow.assign((size_t)3 * FS, MFW_NOROW);
   for (int w = 0; w < MFW_TAB_WAVES; w++) {
     const bool hw = w >= SAMPLE_WAVES;
     /* this wave's rows per lane group and gate: (row block, first, end) */
@@ -916,7 +916,7 @@ static bool mfw_split_tables(const std::vector<std::vector<int>> &ga, const std:
           t0[j][g] = pc.t0;
           t1[j][g] = pc.t1;
           for (int r = 0; r < 8; r++)
-            T.frow[(size_t)g * (SAMPLE_THREADS + NHL) + SAMPLE_THREADS + (w - SAMPLE_WAVES) * 64 + 8 * j + r] =
+            T.frow[(size_t)g * FS + SAMPLE_THREADS + (w - SAMPLE_WAVES) * 64 + 8 * j + r] =
                 8 * slot_of_ub[g][pc.unit] + r;
         }
         (g < 2 ? kz : kh) = std::max(g < 2 ? kz : kh, t1[j][g] - t0[j][g]);
@@ -952,7 +952,7 @@ static bool mfw_split_tables(const std::vector<std::vector<int>> &ga, const std:
   for (int g = 0; g < 3; g++)
     for (int t = 0; t < SAMPLE_THREADS; t++) {
       const int u = perm[t / 8], sl = slot_of_ub[g][u];
-      if (sl >= 0) T.frow[(size_t)g * (SAMPLE_THREADS + NHL) + t] = (8 * sl + (t % 8)) | 1 << 16;
+      if (sl >= 0) T.frow[(size_t)g * FS + t] = (8 * sl + (t % 8)) | 1 << 16;
     }
   return true;
 }
@@ -2118,6 +2118,43 @@ int check_status(LPCNetBatch *b)
 extern "C" {
 
 LPCNET_EXPORT const char *lpcnet_mi355x_last_error(void) { return g_err.c_str(); }
+
+/* Host-only view of the GRU_A plans a blob gets on a wide batch (no
+ * device): the main plan (mf_plan, wide class) and, for split models, the
+ * wide kernel's split tables.  out[0] = split (0/1), out[1] = mfw split form
+ * available (0/1), out[2..17] = the split form's z/r and h 4-slot groups per
+ * table wave (R waves 0..5, host waves 6..7), out[18..20] = pieces per gate.
+ * 0 / -1 (malformed blob or no int8 matrix-core plan). */
+LPCNET_EXPORT int lpcnet_mi355x_wide_plan(const unsigned char *data, int len, int *out)
+{
+  std::vector<Arr> L;
+  if (!data || len <= 0 || !out || !parse_blob(L, data, len)) return -1;
+  std::vector<std::vector<int>> ga;
+  if (!parse_idx(L, "sparse_gru_a_recurrent_weights_idx", NA, GA_ROWS, ga)) return -1;
+  const Arr *gaw = find(L, "sparse_gru_a_recurrent_weights");
+  if (!gaw || gaw->size != 32 * total_blocks(ga)) return -1;
+  std::vector<int> first(ga.size() + 1, 0);
+  for (size_t r = 0; r < ga.size(); r++) first[r + 1] = first[r] + (int)ga[r].size();
+  MfPlan plan;
+  if (!mf_plan(ga, plan, 3, 2)) return -1;
+  MfwSplitTab T;
+  const bool ok = plan.split && mfw_split_tables(ga, plan.perm, first, (const int8_t *)gaw->data, T);
+  out[0] = plan.split ? 1 : 0;
+  out[1] = ok ? 1 : 0;
+  for (int w = 0; w < MFW_TAB_WAVES; w++) {
+    out[2 + 2 * w] = T.nzr[w];
+    out[3 + 2 * w] = T.nh[w];
+  }
+  for (int g = 0; g < 3; g++) {
+    int n = 0;
+    for (int u = 0; u < NA / 8; u++) {
+      const int K = (int)ga[g * (NA / 8) + u].size(), c = g < 2 ? MF_ZMAX : MF_HMAX;
+      if (K > c) n += (K - c + c - 1) / c;
+    }
+    out[18 + g] = n;
+  }
+  return 0;
+}
 
 LPCNET_EXPORT int lpcnet_mi355x_device_count(void)
 {
