@@ -870,10 +870,11 @@ struct MfwSplitTab {
   int nzr[MFW_TAB_WAVES] = {}, nh[MFW_TAB_WAVES] = {};
   std::vector<uint32_t> tab;
   std::vector<int> frow;
+  std::vector<int> units; /* [SAMPLE_THREADS] own unit of each lane (perm below) */
 };
 
-static bool mfw_split_tables(const std::vector<std::vector<int>> &ga, const std::vector<int> &perm,
-                             const std::vector<int> &ga_first, const int8_t *wa, MfwSplitTab &T)
+static bool mfw_split_tables(const std::vector<std::vector<int>> &ga, const std::vector<int> &ga_first,
+                             const int8_t *wa, MfwSplitTab &T)
 {
   constexpr int NUB = NA / 8, NHL = 8 * MFW_H_WAVES, FS = SAMPLE_THREADS + 64 * MFW_H_WAVES;
   const int cap[3] = {MF_ZMAX, MF_ZMAX, MF_HMAX};
@@ -895,6 +896,18 @@ static bool mfw_split_tables(const std::vector<std::vector<int>> &ga, const std:
       if (slot_of_ub[g][pc.unit] < 0) slot_of_ub[g][pc.unit] = ns++;
     if (ns > 16) return false;
   }
+  /* own unit blocks over the six R waves for the capped rows (the wide
+   * kernel's SIMD weight, mf_plan class 3); the E waves' lane order follows */
+  std::vector<std::vector<int>> own(ga.size());
+  for (int g = 0; g < 3; g++)
+    for (int u = 0; u < NUB; u++) {
+      const std::vector<int> &v = ga[g * NUB + u];
+      own[g * NUB + u].assign(v.begin(), v.begin() + std::min((int)v.size(), cap[g]));
+    }
+  g_mf_simd_weight = getenv("LPCNET_MF_SIMD_W") ? atoi(getenv("LPCNET_MF_SIMD_W")) : 25;
+  const std::vector<int> perm = mf_assign_unit_blocks(own, nullptr, 40000);
+  T.units.assign(SAMPLE_THREADS, 0);
+  for (int t = 0; t < SAMPLE_THREADS; t++) T.units[t] = 8 * perm[t / 8] + (t & 7);
   T.tab.assign((size_t)MFW_TAB_WAVES * MF_LANE_U32 * 64, 0);
   T.frow.assign((size_t)3 * FS, MFW_NOROW);
   for (int w = 0; w < MFW_TAB_WAVES; w++) {
@@ -1457,7 +1470,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     /* the wide kernel's split form (wide batches of split models) */
     sa.mfw_split = 0;
     if (plan.split && b->plan_wide && !getenv("LPCNET_NO_MFW_SPLIT") &&
-        mfw_split_tables(ga_blocks, perm, ga_first, wa, mfw_tabs)) {
+        mfw_split_tables(ga_blocks, ga_first, wa, mfw_tabs)) {
       sa.mfw_split = 1;
       for (int w = 0; w < MFW_TAB_WAVES; w++) {
         sa.mfw_nzr[w] = mfw_tabs.nzr[w];
@@ -1723,6 +1736,7 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     if (sa.mfw_split) {
       UP(sa.mfw_tab, mfw_tabs.tab.data(), mfw_tabs.tab.size() * 4);
       UP(sa.mfw_frow, mfw_tabs.frow.data(), mfw_tabs.frow.size() * 4);
+      UP(sa.mfw_unit, mfw_tabs.units.data(), mfw_tabs.units.size() * 4);
     }
     {
       /* Range of the GRU_A gates' inputs for the elementwise fast path:
@@ -1776,6 +1790,16 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
         const float *d = nullptr;
         UP(d, pt.data(), pt.size() * 4);
         sa.mf_emb[t] = d;
+        if (sa.mfw_split) {
+          /* the same in the wide split form's lane order */
+          for (int row = 0; row < 256; row++)
+            for (int g = 0; g < 3; g++)
+              for (int p = 0; p < NA; p++)
+                pt[(size_t)row * GA_ROWS + g * NA + p] = src[t][(size_t)row * GA_ROWS + g * NA + mfw_tabs.units[p]];
+          const float *dw = nullptr;
+          UP(dw, pt.data(), pt.size() * 4);
+          sa.mfw_emb[t] = dw;
+        }
       }
     }
     UP(sa.mf_gb, mfgb.data(), mfgb.size() * 4);
@@ -2138,7 +2162,7 @@ LPCNET_EXPORT int lpcnet_mi355x_wide_plan(const unsigned char *data, int len, in
   MfPlan plan;
   if (!mf_plan(ga, plan, 3, 2)) return -1;
   MfwSplitTab T;
-  const bool ok = plan.split && mfw_split_tables(ga, plan.perm, first, (const int8_t *)gaw->data, T);
+  const bool ok = plan.split && mfw_split_tables(ga, first, (const int8_t *)gaw->data, T);
   out[0] = plan.split ? 1 : 0;
   out[1] = ok ? 1 : 0;
   for (int w = 0; w < MFW_TAB_WAVES; w++) {

@@ -254,6 +254,8 @@ struct SampleArgs {
   int mfw_split;
   const uint32_t *mfw_tab;
   const int *mfw_frow;
+  const int *mfw_unit;      /* [SAMPLE_THREADS]: the split form's own unit of each E / R lane */
+  const float *mfw_emb[3];  /* embedding tables in the split form's lane order (as mf_emb) */
   int mfw_nzr[MFW_TAB_WAVES];
   int mfw_nh[MFW_TAB_WAVES];
   const uint4 *mf_gb;

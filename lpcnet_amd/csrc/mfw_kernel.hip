@@ -271,7 +271,7 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
     constexpr int FS = SAMPLE_THREADS + 64 * MFW_H_WAVES;
     tgt = (uint32_t)fr[0] | (uint32_t)fr[FS] << 9 | (uint32_t)fr[2 * FS] << 18;
   } else {
-    const int i = A.mf_unit[r * 64 + lane];
+    const int i = (SPLIT ? A.mfw_unit : A.mf_unit)[r * 64 + lane];
     wsz = A.ga_wsum[i];
     wsr = A.ga_wsum[NA + i];
     wsh = A.ga_wsum[2 * NA + i];
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS) void mfw_k
 
   if (wv < MFW_S_WAVE0) {
     /* ======================= E role ====================================== */
-    const int i = A.mf_unit[tid];
+    const int i = (SPLIT ? A.mfw_unit : A.mf_unit)[tid];
     const float bz = A.ga_par[i], br = A.ga_par[NA + i], bh = A.ga_par[2 * NA + i];
     const float dz = A.ga_par[3 * NA + i], dr = A.ga_par[4 * NA + i], dh = A.ga_par[5 * NA + i];
     float st[MFW_G][S];
@@ -517,7 +517,8 @@ __global__ __launch_bounds__(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS) void mfw_k
         uint32_t o2 = (uint32_t)tid * 4u + (uint32_t)v.y;
         uint32_t o3 = (uint32_t)tid * 4u + (uint32_t)v.z;
         asm volatile("" : "+v"(o1), "+v"(o2), "+v"(o3));
-        const char *b1 = (const char *)A.mf_emb[0], *b2 = (const char *)A.mf_emb[1], *b3 = (const char *)A.mf_emb[2];
+        const float *const *emb = SPLIT ? A.mfw_emb : A.mf_emb;
+        const char *b1 = (const char *)emb[0], *b2 = (const char *)emb[1], *b3 = (const char *)emb[2];
 #pragma unroll
         for (uint32_t q = 0; q < 3; q++) {
           e[s][q] = *(const float *)(b1 + o1 + q * NA * 4u);
