@@ -50,7 +50,8 @@ namespace lpcnet_mi355x {
 constexpr int MFW_S = 4;                 /* streams per group */
 constexpr int MFW_THREADS = 64 * 14;     /* 6 E + 2 S + 6 R waves */
 constexpr int MFW_THREADS_SPLIT = 64 * 16; /* split form: + 2 host waves (MFW_H_WAVES) */
-/* split form: the host waves' partial sums [phase parity][gate][MFW_PART_ROWS][S] */
+/* split form: the host waves' partial sums [phase parity][gate][MFW_PART_ROWS][S / 2]
+ * 64-bit words (two streams each, see mfw_r_role) */
 constexpr int MFW_PRT = 2 * 3 * MFW_PART_ROWS * MFW_S * 4;
 constexpr int MFW_S_WAVE0 = 6, MFW_R_WAVE0 = 8;
 
@@ -168,6 +169,10 @@ __device__ __forceinline__ uint32_t mfw_x(const unsigned char *xg, const uint32_
  * the hardware reciprocal (0) */
 #ifndef MFW_TAB
 #define MFW_TAB 1
+#endif
+/* split form: host waves on SIMDs 0 / 1 instead of 2 / 3 (A/B) */
+#ifndef MFW_H_LOW
+#define MFW_H_LOW 0
 #endif
 /* issue priority of the S waves */
 #ifndef MFW_S_PRIO
@@ -303,20 +308,30 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
      * whether its accumulator chains or not (tools/probes/mfma_timing.hip) */
     v4i vz = {wsz, wsz, wsz, wsz}, vr = {wsr, wsr, wsr, wsr}, vh[1] = {{wsh, wsh, wsh, wsh}};
     mfw_zr<Z>(xg, wz, wr, cz, cr, mo, vz, vr);
-    mfw_gate<H, 1>(xg, wh, ch, mo, vh);
     if constexpr (HOST) {
-      /* exact int32 LDS adds into the owners' part words (one piece per
-       * lane and gate; lanes without a piece skip) */
+      /* exact LDS adds into the owners' part words, two streams per 64-bit
+       * add (hi 2^32 + lo, lo sign-extended: mf_common.h part_add PACK); one
+       * piece per lane and gate, lanes without one skip.  z / r go out
+       * before the h product, so their adds complete under its MFMAs */
       uint32_t tq = tgt;
       asm volatile("" : "+v"(tq));
-      int *pp = prt + (p & 1) * 3 * MFW_PART_ROWS * MFW_S;
-      const int t3[3] = {(int)(tq & 0x1FF), (int)((tq >> 9) & 0x1FF), (int)((tq >> 18) & 0x1FF)};
-      const v4i vv[3] = {vz, vr, vh[0]};
+      unsigned long long *pp = (unsigned long long *)prt + (p & 1) * 3 * MFW_PART_ROWS * (MFW_S / 2);
+      auto padd = [&](int q, const v4i &v) {
+        const int t = (int)((tq >> (9 * q)) & 0x1FF);
+        if (t != MFW_NOROW)
 #pragma unroll
-      for (int q = 0; q < 3; q++)
-        if (t3[q] != MFW_NOROW)
-#pragma unroll
-          for (int s = 0; s < MFW_S; s++) atomicAdd(&pp[(q * MFW_PART_ROWS + t3[q]) * MFW_S + s], vv[q][s]);
+          for (int k = 0; k < MFW_S / 2; k++)
+            atomicAdd(&pp[(q * MFW_PART_ROWS + t) * (MFW_S / 2) + k],
+                      ((unsigned long long)(uint32_t)v[2 * k + 1] << 32) + (unsigned long long)(long long)v[2 * k]);
+      };
+      padd(0, vz);
+      padd(1, vr);
+      mfw_gate<H, 1>(xg, wh, ch, mo, vh);
+      padd(2, vh[0]);
+    } else {
+      mfw_gate<H, 1>(xg, wh, ch, mo, vh);
+    }
+    if constexpr (HOST) {
     } else {
       /* the sums' LDS address from an opaque row (not hoisted per parity) */
       int rq = row;
@@ -407,7 +422,13 @@ __global__ __launch_bounds__(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS) void mfw_k
 
   if (wv >= MFW_R_WAVE0) {
     /* ======================= R role ====================================== */
-    const int r = wv - MFW_R_WAVE0;
+    int r = wv - MFW_R_WAVE0;
+#if MFW_H_LOW
+    /* A/B: the host waves on hardware waves 12 / 13 (SIMDs 0 / 1, beside R
+     * waves 0 / 1), R waves 4 / 5 on 14 / 15 (SIMDs 2 / 3, beside the
+     * samplers) */
+    if (SPLIT && r >= 4) r = r < 6 ? r + 2 : r - 2;
+#endif
     if constexpr (SPLIT) {
       if (r >= SAMPLE_WAVES) {
         /* ===================== host waves (split form) ===================== */
@@ -538,18 +559,22 @@ __global__ __launch_bounds__(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS) void mfw_k
          * of the parity; exact int32 adds */
         uint32_t fp = frow;
         asm volatile("" : "+v"(fp));
-        int *pp = prt + ((p - 1) & 1) * 3 * MFW_PART_ROWS * S;
+        unsigned long long *pp = (unsigned long long *)prt + ((p - 1) & 1) * 3 * MFW_PART_ROWS * (S / 2);
         int *vg[3] = {vz, vr, vh};
 #pragma unroll
         for (int q = 0; q < 3; q++)
           if (fp >> (27 + q) & 1) {
-            int *w4 = pp + (q * MFW_PART_ROWS + (int)((fp >> (9 * q)) & 0x1FF)) * S;
-            const int4 t = *(const int4 *)w4;
-            vg[q][0] += t.x;
-            vg[q][1] += t.y;
-            vg[q][2] += t.z;
-            vg[q][3] += t.w;
-            *(int4 *)w4 = make_int4(0, 0, 0, 0);
+            unsigned long long *w2 = pp + (q * MFW_PART_ROWS + (int)((fp >> (9 * q)) & 0x1FF)) * (S / 2);
+#pragma unroll
+            for (int k = 0; k < S / 2; k++) {
+              /* sum over pieces of hi 2^32 + lo: lo is the low word, the
+               * rest hi (|row sums| < 2^24) */
+              const unsigned long long t = w2[k];
+              const int lo = (int)(uint32_t)t;
+              vg[q][2 * k] += lo;
+              vg[q][2 * k + 1] += (int)((long long)(t - (unsigned long long)(long long)lo) >> 32);
+              w2[k] = 0ull;
+            }
           }
       }
       float az[S], ar[S], tz[S], tr[S], hpre[S];

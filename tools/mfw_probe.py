@@ -15,7 +15,7 @@ import lpcnet_amd as L  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 3072
 F = int(sys.argv[2]) if len(sys.argv) > 2 else 6
-blob = L.synthetic_model(1, 0)
+blob = L.synthetic_model(1, 0, skewed=os.environ.get("PROBE_SKEWED") == "1")
 feats = np.ascontiguousarray(np.stack([L.synthetic_features(s, F)[:, :20] for s in range(B)], 1), np.float32)
 b = L.LPCNetBatch(B, 0, blob)
 d_f = b.device_alloc(feats.nbytes)
