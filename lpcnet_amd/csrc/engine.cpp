@@ -330,6 +330,7 @@ struct LPCNetBatch {
                             recurrent / sampler waves) for the same launches, non-split models with the
                             default rcpps */
   bool plan_wide = false; /* the register tables were planned for mfw_kernel (plan class 3) */
+  L2Warm ck_warm{};       /* the chunk kernel's re-tiled weights (deferred LPC warms them) */
   std::vector<unsigned char> blob; /* the loaded model's blob: replanned when the kernel choice moves */
   double mf_ga_ops = 0;  /* int8 matrix-core ops per workgroup per sample: the GRU_A recurrent pass */
   double mf_gb_ops = 0;  /* the GRU_B tiles of both sampler waves */
@@ -426,6 +427,7 @@ void free_model(LPCNetBatch *b)
   for (void *p : b->model_bufs) (void)hipFree(p);
   b->model_bufs.clear();
   b->have_model = false;
+  b->ck_warm = L2Warm{};
 }
 
 hipEvent_t get_event(LPCNetBatch *b)
@@ -1718,6 +1720,12 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     UP(fa.ck_dense1, t3.data(), t3.size() * 4);
     UP(fa.ck_dense2, t4.data(), t4.size() * 4);
     UP(fa.ck_proj, t5.data(), t5.size() * 4);
+    const float4 *wm[5] = {fa.ck_conv1, fa.ck_conv2, fa.ck_dense1, fa.ck_dense2, fa.ck_proj};
+    const size_t wn[5] = {t1.size(), t2.size(), t3.size(), t4.size(), t5.size()};
+    for (int t = 0; t < 5; t++) {
+      b->ck_warm.m[t] = (const uint32_t *)wm[t];
+      b->ck_warm.lines[t] = (int)(wn[t] * 4 / 128);
+    }
   }
   UP(fa.embed_pitch, embed_pitch, 256 * EP * 4);
   UP(fa.rcp, rcp_dev.data(), RCP_ENTRIES * 4);
@@ -2623,7 +2631,12 @@ static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm
       HIPCHK(hipMemcpyAsync(own_pcm ? b->h_io_pcm : b->h_stg_pcm, b->d_pcm, sizeof(short) * N * nB,
                             hipMemcpyDeviceToHost, b->stream));
     auto lpc_after = [&]() -> int {
-      if (launch_lpc(b->d_feat, nullptr, nB, b->d_lpc_tab, b->stream, b->d_state, b->mc.delay)) {
+      /* ... and warms every XCD's L2 with the chunk kernel's weights for the
+       * next tick (the sample kernel's tables evict them; LPCNET_CK_WARM=0 off) */
+      const char *cw = getenv("LPCNET_CK_WARM");
+      const bool warm = !(cw && atoi(cw) == 0) && b->ck_warm.m[0];
+      if (launch_lpc(b->d_feat, nullptr, nB, b->d_lpc_tab, b->stream, b->d_state, b->mc.delay,
+                     warm ? &b->ck_warm : nullptr)) {
         set_err("deferred lpc kernel launch failed");
         return -1;
       }

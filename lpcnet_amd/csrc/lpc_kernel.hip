@@ -97,9 +97,25 @@ __device__ __forceinline__ void bfly5(C2 *f, int u, const C2 *tw)
 
 }  // namespace
 
-__global__ __launch_bounds__(64 * LPC_STREAMS) void lpc_kernel(const float *features, float *lpc_out, int nstreams,
-                                                               const LpcTables *T, StreamState *ring, int ring_depth)
+/* the warm-up of the next tick's chunk kernel weights (deferred form): the
+ * workgroups of an XCD (workgroup b runs on XCD b % 8) split every line of
+ * the matrices and touch it once; the XOR only keeps the loads alive */
+__device__ __forceinline__ void l2_warm_lines(const L2Warm &W)
 {
+  const int x = blockIdx.x % 8, nx = ((int)gridDim.x - 1 - x) / 8 + 1, k = blockIdx.x / 8;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int t = 0; t < 5; t++)
+    for (int o = k * (int)blockDim.x + (int)threadIdx.x; o < W.lines[t]; o += nx * (int)blockDim.x)
+      acc ^= W.m[t][(size_t)o * 32];
+  asm volatile("" ::"v"(acc));
+}
+
+__global__ __launch_bounds__(64 * LPC_STREAMS) void lpc_kernel(const float *features, float *lpc_out, int nstreams,
+                                                               const LpcTables *T, StreamState *ring, int ring_depth,
+                                                               L2Warm warm)
+{
+  if (warm.m[0]) l2_warm_lines(warm); /* issued first, in flight under the LPC work */
   __shared__ C2 ybuf[LPC_STREAMS][WIN];
   __shared__ C2 tw[WIN];
   __shared__ float dct[NBANDS * NBANDS];
@@ -226,12 +242,14 @@ __global__ __launch_bounds__(64 * LPC_STREAMS) void lpc_kernel(const float *feat
 }
 
 int launch_lpc(const float *features, float *lpc_out, int nstreams, const LpcTables *tables, void *stream,
-               StreamState *ring, int ring_depth)
+               StreamState *ring, int ring_depth, const L2Warm *warm)
 {
   if (ring && (ring_depth < 1 || ring_depth > MAX_FEATURES_DELAY)) return -1;
   const int grid = (nstreams + LPC_STREAMS - 1) / LPC_STREAMS;
+  L2Warm w{};
+  if (warm) w = *warm;
   hipLaunchKernelGGL(lpc_kernel, dim3(grid), dim3(64 * LPC_STREAMS), 0, (hipStream_t)stream, features, lpc_out, nstreams,
-                     tables, ring, ring_depth);
+                     tables, ring, ring_depth, w);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

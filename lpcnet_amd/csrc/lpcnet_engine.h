@@ -410,8 +410,15 @@ struct LpcTables {
   LpcSlot slot[LPC_WIN];
 };
 /* features [nstreams][NF] -> lpc_out [nstreams][NLPC] */
+/* read-only matrices an idle-time kernel touches once per 128-byte line in
+ * every XCD's L2 (the deferred lpc_kernel warms the one-frame chunk
+ * kernel's weights for the next tick) */
+struct L2Warm {
+  const uint32_t *m[5];
+  int lines[5];
+};
 int launch_lpc(const float *features, float *lpc_out, int nstreams, const LpcTables *tables, void *stream,
-               StreamState *ring = nullptr, int ring_depth = 0);
+               StreamState *ring = nullptr, int ring_depth = 0, const L2Warm *warm = nullptr);
 
 /* decode_packet (lpcnet_dec.c:81-156) on the device (decode_kernel.hip):
  * packets [npackets][nstreams][8] -> features [4 npackets][nstreams][NF],
