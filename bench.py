@@ -623,6 +623,38 @@ def capacity_live(L, blob, ticks=100, warmup=10,
             "ticks_per_point": ticks, "ladder": {str(k): v for k, v in sorted(rows.items())}}
 
 
+def dropin_rt(threads=(256, 960), frames=300):
+    """The drop-in API (include/lpcnet.h, one LPCNetState per stream,
+    lpcnet.c:213-219, 279-281) paced in real time from C threads
+    (tools/dropin_bench rt): each thread calls lpcnet_synthesize once per 10
+    ms tick, phases spread over the tick and all on one phase ("burst");
+    per-call latency p50 / p99 / max and deadline misses.  Runs as a child
+    process before this process touches the GPU; None when the binary is
+    absent (make dropin).  The thread counts stop at 960: one thread per
+    stream is the reference's calling pattern, and the GPU box limits a
+    job's tasks."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "dropin_bench")
+    if not os.path.exists(exe):
+        return None
+    pts = []
+    for T in threads:
+        for mode in ("spread", "burst"):
+            try:
+                r = subprocess.run([exe, str(T), str(frames), "rt", mode], capture_output=True, text=True, timeout=120)
+                pts.append(json.loads(r.stdout.strip().splitlines()[-1]))
+            except (subprocess.SubprocessError, ValueError, IndexError, OSError) as e:
+                pts.append({"threads": T, "mode": mode, "error": str(e)[:200]})
+    ok = [p["threads"] for p in pts if p.get("realtime_p99") is True]
+    worst = {m: max((p for p in pts if p.get("mode") == m and "latency_ms_p99" in p), key=lambda p: p["threads"],
+                    default=None) for m in ("spread", "burst")}
+    return {"max_threads_realtime_p99": max(ok) if ok else 0, "max_threads_measured": max(threads),
+            "criterion": "p99 per-call latency of lpcnet_synthesize <= 10 ms, one C thread per stream paced at one "
+                         "frame per 10 ms", "points": pts,
+            "at_max": {m: {k: w[k] for k in ("latency_ms_p50", "latency_ms_p99", "latency_ms_max", "deadline_misses",
+                                             "calls", "mean_coalesced_streams")} for m, w in worst.items() if w}}
+
+
 def skewed_lines(L, args):
     """A trained-model-like sparsity pattern (Sparsify's global per-gate
     threshold over skewed block energies, training_tf2/lpcnet.py:140-160:
@@ -774,8 +806,13 @@ def compact_line(out, detail_path):
                     "samples_per_s_at_max": _r(top.get("samples_per_s")), "criterion": cp["criterion"]}
     if "skewed_int8" in out:
         c["skewed_int8"] = {k: _r(v["samples_per_s"]) for k, v in out["skewed_int8"].items()}
-    if "dropin_rt" in out:
-        c["dropin_rt"] = out["dropin_rt"]
+    if out.get("dropin_rt"):
+        d = out["dropin_rt"]
+        c["dropin_rt"] = {"max_threads_realtime_p99": d["max_threads_realtime_p99"],
+                          "max_threads_measured": d["max_threads_measured"],
+                          "at_max": {m: {k: _r(v) if isinstance(v, float) else v for k, v in w.items()}
+                                     for m, w in d.get("at_max", {}).items()},
+                          "criterion": d["criterion"]}
     if "latency" in out:
         c["latency_cycles_per_sample"] = _r(out["latency"].get("cycles_per_sample_at_measured"))
     c["pcm_checksum"] = out.get("pcm_checksum")
@@ -785,6 +822,11 @@ def compact_line(out, detail_path):
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank0 = int(os.environ.get("RANK", "0")) == 0
+    # the drop-in real-time check runs as a child process, before this
+    # process initialises the GPU
+    drt = dropin_rt() if rank0 and world == 1 and not args.no_batch1 and not args.live_only else None
     world, rank, local, dist = dist_setup(args)
     import lpcnet_amd as L
     variant = L.VARIANT_INT8 if args.variant == "int8" else L.VARIANT_FP32
@@ -852,6 +894,8 @@ def main():
         out["capacity_live"] = capacity_live(L, blob)
         # the same ladder on the trained-like (Sparsify) sparsity pattern
         out["capacity_skewed"] = capacity(L, L.synthetic_model(1, L.VARIANT_INT8, skewed=True), args)
+    if drt is not None:
+        out["dropin_rt"] = drt
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         # beside batch1_fp32 (configs[1]): the reference's fp32 build on the same cores

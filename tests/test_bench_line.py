@@ -16,7 +16,7 @@ CANNED = os.path.join(ROOT, "tests", "golden", "bench_full_canned.json")
 REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
             "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "cpu_baseline_fp32",
             "realtime_streams_per_gpu", "batch1", "batch1_fp32", "batch256", "batch8192", "live", "capacity",
-            "capacity_live", "capacity_skewed", "detail")
+            "capacity_live", "capacity_skewed", "dropin_rt", "detail")
 ROOF = ("bound", "achieved", "peak", "unit", "frac", "traffic", "roofline_l2", "valu", "binding")
 CPU = ("value", "unit", "cores", "kind")
 
