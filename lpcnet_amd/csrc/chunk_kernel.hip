@@ -350,10 +350,11 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
    * (one ring), then its projection tiles wave, wave + 8, ... TP at a time */
   const int l64 = tid & 63;
   constexpr int XL = ck_xl(NCT), PQ = ck_pq(NCT), TP = ck_tp(NCT), PQP = ck_pqp(TP, NCT);
-  const float4 *t_c1 = A.ck_conv1 + (size_t)wave * ck_tq(3 * FIN) * 64 + l64;
-  const float4 *t_c2 = A.ck_conv2 + (size_t)wave * ck_tq(3 * COND) * 64 + l64;
-  const float4 *t_d1 = A.ck_dense1 + (size_t)wave * ck_tq(COND) * 64 + l64;
-  const float4 *t_d2 = A.ck_dense2 + (size_t)wave * ck_tq(COND) * 64 + l64;
+  /* sliced: this slice's copy of the layer weights (same values) */
+  const float4 *t_c1 = A.ck_conv1 + (size_t)slice * A.ck_rep[0] + (size_t)wave * ck_tq(3 * FIN) * 64 + l64;
+  const float4 *t_c2 = A.ck_conv2 + (size_t)slice * A.ck_rep[1] + (size_t)wave * ck_tq(3 * COND) * 64 + l64;
+  const float4 *t_d1 = A.ck_dense1 + (size_t)slice * A.ck_rep[2] + (size_t)wave * ck_tq(COND) * 64 + l64;
+  const float4 *t_d2 = A.ck_dense2 + (size_t)slice * A.ck_rep[3] + (size_t)wave * ck_tq(COND) * 64 + l64;
   auto t_pj = [&](int rt) { return A.ck_proj + (size_t)rt * ck_tq(COND) * 64 + l64; };
   const int bo = 16 * wave + 4 * g; /* this lane's bias quad in a 128-row layer */
   CkRing<1, PQ> R;
@@ -614,6 +615,7 @@ static int launch_chunk_h(const FrameArgs &a, void *stream)
     const int ps = !a.ck_sync || !a.status || a.cond ? 1
                    : ps_env >= 1 ? ps_env
                    : 4 * groups <= cus ? 4 : 2 * groups <= cus ? 2 : 1;
+    static_assert(CK_SLICES_MAX >= 4, "weight copies per slice");
     if (ps >= 4) return launch_chunk_t<1, 16, HWR, 4>(a, stream);
     if (ps == 2) return launch_chunk_t<1, 16, HWR, 2>(a, stream);
     return groups <= 2 * cus ? launch_chunk_t<1, 16, HWR>(a, stream) : launch_chunk_t<1, 32, HWR>(a, stream);

@@ -1715,10 +1715,25 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     std::vector<float> t1 = tiled(conv1_w, 3 * FIN, COND), t2 = tiled(conv2_w, 3 * COND, COND);
     std::vector<float> t3 = tiled(dense1_w, COND, COND), t4 = tiled(dense2_w, COND, COND);
     std::vector<float> t5 = tiled(pwf.data(), COND, GA_ROWS + GB_ROWS);
-    UP(fa.ck_conv1, t1.data(), t1.size() * 4);
-    UP(fa.ck_conv2, t2.data(), t2.size() * 4);
-    UP(fa.ck_dense1, t3.data(), t3.size() * 4);
-    UP(fa.ck_dense2, t4.data(), t4.size() * 4);
+    /* conv1 .. dense2 once per projection slice of the one-frame kernel
+     * (CK_SLICES_MAX copies): the slices of all 16-stream groups of an XCD
+     * stream these rows in near lockstep, and one copy per slice spreads
+     * their same-line L2 reads over four times the lines */
+    auto rep = [](const std::vector<float> &t) {
+      std::vector<float> r;
+      r.reserve(t.size() * CK_SLICES_MAX);
+      for (int k = 0; k < CK_SLICES_MAX; k++) r.insert(r.end(), t.begin(), t.end());
+      return r;
+    };
+    const std::vector<float> r1 = rep(t1), r2 = rep(t2), r3 = rep(t3), r4 = rep(t4);
+    UP(fa.ck_conv1, r1.data(), r1.size() * 4);
+    UP(fa.ck_conv2, r2.data(), r2.size() * 4);
+    UP(fa.ck_dense1, r3.data(), r3.size() * 4);
+    UP(fa.ck_dense2, r4.data(), r4.size() * 4);
+    fa.ck_rep[0] = (int)(t1.size() / 4);
+    fa.ck_rep[1] = (int)(t2.size() / 4);
+    fa.ck_rep[2] = (int)(t3.size() / 4);
+    fa.ck_rep[3] = (int)(t4.size() / 4);
     UP(fa.ck_proj, t5.data(), t5.size() * 4);
     const float4 *wm[5] = {fa.ck_conv1, fa.ck_conv2, fa.ck_dense1, fa.ck_dense2, fa.ck_proj};
     const size_t wn[5] = {t1.size(), t2.size(), t3.size(), t4.size(), t5.size()};
@@ -2631,10 +2646,10 @@ static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm
       HIPCHK(hipMemcpyAsync(own_pcm ? b->h_io_pcm : b->h_stg_pcm, b->d_pcm, sizeof(short) * N * nB,
                             hipMemcpyDeviceToHost, b->stream));
     auto lpc_after = [&]() -> int {
-      /* ... and warms every XCD's L2 with the chunk kernel's weights for the
-       * next tick (the sample kernel's tables evict them; LPCNET_CK_WARM=0 off) */
+      /* LPCNET_CK_WARM=1 (A/B, measured: no gain at 1024 streams): it also
+       * warms every XCD's L2 with the chunk kernel's weights for the next tick */
       const char *cw = getenv("LPCNET_CK_WARM");
-      const bool warm = !(cw && atoi(cw) == 0) && b->ck_warm.m[0];
+      const bool warm = cw && atoi(cw) != 0 && b->ck_warm.m[0];
       if (launch_lpc(b->d_feat, nullptr, nB, b->d_lpc_tab, b->stream, b->d_state, b->mc.delay,
                      warm ? &b->ck_warm : nullptr)) {
         set_err("deferred lpc kernel launch failed");

@@ -175,6 +175,9 @@ struct FrameArgs {
    * lane l = (g, r) = (l / 16, l % 16), element j of quad q = W[4 (4q + j) +
    * g][16 rt + r] (0 past K), CK_WPAD zero quads after each row tile's last */
   const float4 *ck_conv1, *ck_conv2, *ck_dense1, *ck_dense2, *ck_proj;
+  /* conv1 .. dense2 are stored CK_SLICES_MAX times: copy k at + k ck_rep[i]
+   * float4s (projection slice k of the one-frame kernel reads copy k) */
+  int ck_rep[4];
   /* one-frame chunk_kernel, deferred LPC (FEATURES_DELAY >= 1): the frame's
    * LPC comes from the ring only, the ring is advanced later by lpc_kernel
    * (launch_lpc with a ring), and the frame's features are copied to
@@ -188,6 +191,7 @@ struct FrameArgs {
   int *ck_sync;
   int *status;
 };
+constexpr int CK_SLICES_MAX = 4; /* projection slices of the one-frame chunk kernel */
 constexpr int CK_WPAD = 8; /* chunk_kernel: k quads in flight per wave (zero padding of each row tile) */
 
 struct SampleArgs {
