@@ -30,6 +30,9 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "device_math.h"
 #include "lpcnet_engine.h"
 
@@ -586,7 +589,12 @@ template <int NFR, int SC, bool HWR, int PS = 1>
 static int launch_chunk_t(const FrameArgs &a, void *stream)
 {
   using G = CkGeom<NFR, SC>;
-  const int bytes = G::FLOATS * 4;
+  /* sliced launches (one workgroup per CU at most 4 x 64 groups): more than
+   * half the CU's LDS, so the dispatcher cannot pack two workgroups on one
+   * CU -- two would share each SIMD's f32 matrix pipe, whose issue rate
+   * bounds the layers (LPCNET_CK_PACK=1: the plain size, A/B) */
+  static const bool pack = getenv("LPCNET_CK_PACK") && atoi(getenv("LPCNET_CK_PACK")) != 0;
+  const int bytes = PS > 1 && !pack ? std::max(G::FLOATS * 4, 81 * 1024) : G::FLOATS * 4;
   if (ensure_dyn_lds((const void *)chunk_kernel<NFR, SC, HWR, PS>, bytes)) return -1;
   const int grid = (a.nstreams + G::SC - 1) / G::SC * PS;
   hipLaunchKernelGGL((chunk_kernel<NFR, SC, HWR, PS>), dim3(grid), dim3(CK_THREADS), bytes, (hipStream_t)stream, a);
