@@ -335,10 +335,9 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
   CK_T(1);
   if constexpr (PS > 1) {
     /* every state read of this slice has landed (LDS / registers) */
-    if (!writer && tid == 0) {
-      __threadfence();
-      atomicAdd(&A.ck_sync[grp], 1);
-    }
+    /* relaxed: the reads completed (their values are in LDS past the
+     * barrier); a release fence here (buffer_wbl2) cost wave 0 ~10 K cycles */
+    if (!writer && tid == 0) __hip_atomic_fetch_add(&A.ck_sync[grp], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
   /* this lane's column of each column tile */
@@ -395,14 +394,15 @@ __global__ __launch_bounds__(CK_THREADS) void chunk_kernel(FrameArgs A)
     if (writer) {
       if (tid == 0) {
         int polls = 0;
-        while (__hip_atomic_load(&A.ck_sync[grp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < PS - 1) {
+        /* relaxed polls: the state stores below issue after the loop exits */
+        while (__hip_atomic_load(&A.ck_sync[grp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < PS - 1) {
           if (++polls > (1 << 22)) {
             A.status[0] = STATUS_SLICE_TIMEOUT; /* plain vector store to the pinned host word */
             break;
           }
           __builtin_amdgcn_s_sleep(2);
         }
-        atomicExch(&A.ck_sync[grp], 0);
+        __hip_atomic_exchange(&A.ck_sync[grp], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
     }
