@@ -382,8 +382,6 @@ struct LPCNetBatch {
   int *h_status = nullptr;
   int *d_status = nullptr;
   int *d_ck_sync = nullptr; /* [ceil(B / 16)] arrival counters of the sliced one-frame chunk kernel */
-  unsigned *d_tick_cnt = nullptr; /* mf_kernel's workgroup arrivals of a flagged tick (SampleArgs::tick_cnt) */
-  int tick_seq = 0;               /* the last flagged tick's number (h_status[8] receives it) */
   int spin_limit = FLAG_SPIN_LIMIT_DEFAULT;
   /* 1.6 kb/s decoder (decode_kernel.hip): the model's ceps codebooks (optional
    * blob records), packets and decoded features of up to DEC_MAX_PACKETS
@@ -2255,11 +2253,9 @@ LPCNET_EXPORT LPCNetBatch *lpcnet_batch_create(int nb_streams, int device)
   ok = ok && hipMalloc(&b->d_pcm, sizeof(short) * FRAME * (size_t)nb_streams) == hipSuccess;
   ok = ok && hipHostMalloc(&b->h_status, 64, hipHostMallocMapped) == hipSuccess;
   ok = ok && hipHostGetDevicePointer((void **)&b->d_status, b->h_status, 0) == hipSuccess;
-  if (ok) memset(b->h_status, 0, 64); /* [0] status bits, [8] tick flag */
+  if (ok) *b->h_status = 0;
   ok = ok && hipMalloc(&b->d_lpc, sizeof(float) * NLPC * (size_t)nb_streams * LPC_CHUNK) == hipSuccess;
   ok = ok && hipMalloc(&b->d_ck_sync, sizeof(int) * (size_t)((nb_streams + 15) / 16)) == hipSuccess;
-  ok = ok && hipMalloc(&b->d_tick_cnt, sizeof(unsigned)) == hipSuccess;
-  ok = ok && hipMemset(b->d_tick_cnt, 0, sizeof(unsigned)) == hipSuccess;
   ok = ok && hipMemset(b->d_ck_sync, 0, sizeof(int) * (size_t)((nb_streams + 15) / 16)) == hipSuccess;
   ok = ok && hipMalloc(&b->d_lpc_tab, sizeof(LpcTables)) == hipSuccess;
   /* d_chunk (the chunked path's frame outputs, LPC_CHUNK x 4.9 KB per
@@ -2297,7 +2293,6 @@ LPCNET_EXPORT void lpcnet_batch_destroy(LPCNetBatch *b)
   free_model(b);
   (void)hipFree(b->d_state);
   (void)hipFree(b->d_ck_sync);
-  (void)hipFree(b->d_tick_cnt);
   (void)hipFree(b->d_feat);
   (void)hipFree(b->d_pcm);
   (void)hipFree(b->d_trace_logits);
@@ -2463,7 +2458,7 @@ static bool lpc_deferred(const LPCNetBatch *b)
 /* d_features: device memory, or the mapped host buffer (mapped = true: a
  * deferred LPC then reads the chunk kernel's copy in b->d_feat) */
 static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_features, short *d_pcm, int N,
-                                       bool defer = false, bool mapped = false, int tick_seq = 0)
+                                       bool defer = false, bool mapped = false)
 {
   if (!b->mc.end2end && !defer && launch_lpc(d_features, b->d_lpc, nB, b->d_lpc_tab, b->stream)) {
     set_err("lpc kernel launch failed");
@@ -2506,10 +2501,6 @@ static int launch_single_frame_chunked(LPCNetBatch *b, int nB, const float *d_fe
   sa.stamps = nullptr;
   sa.status = b->d_status;
   sa.spin_limit = b->spin_limit;
-  /* a flagged tick (mf_kernel only): the kernel itself reports its end */
-  sa.tick_cnt = tick_seq ? b->d_tick_cnt : nullptr;
-  sa.tick_flag = tick_seq ? b->d_status + 8 : nullptr;
-  sa.tick_seq = tick_seq;
   if (e[1]) HIPCHK(hipEventRecord(e[1], b->stream));
   const int lrc = b->fp ? launch_fp(sa, b->stream)
                   : wide_for(b, nB) ? launch_mfw(sa, b->mfw_g, b->stream)
@@ -2605,30 +2596,6 @@ static int tick_sync(LPCNetBatch *b, bool poll, const std::function<int()> &afte
   return 0;
 }
 
-/* the end of a flagged tick: poll the pinned word the sample kernel stores
- * seq into (x86 load; no runtime call per poll).  An event after the work
- * queued behind it (the deferred LPC) bounds the wait: once that completes
- * the word must hold seq, else the launch failed. */
-static int tick_wait_flag(LPCNetBatch *b, int seq)
-{
-  if (!b->ev_tick) HIPCHK(hipEventCreateWithFlags(&b->ev_tick, hipEventDisableTiming));
-  HIPCHK(hipEventRecord(b->ev_tick, b->stream));
-  volatile int *w = b->h_status + 8;
-  for (unsigned k = 1;; k++) {
-    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return 0;
-    __builtin_ia32_pause();
-    if ((k & 1023) == 0) {
-      const hipError_t q = hipEventQuery(b->ev_tick);
-      if (q == hipSuccess) {
-        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return 0;
-        set_err("flagged tick: the stream completed without the sample kernel's end flag");
-        return -1;
-      }
-      if (q != hipErrorNotReady) HIPCHK(q);
-    }
-  }
-}
-
 /* sample kernels whose PCM write-out is wide (a frame's samples, or 16 of
  * them, per stream in consecutive lanes): mf_kernel at the end of the
  * launch, mfw_kernel every 16 samples, fp_kernel at the end.  mf2_kernel
@@ -2672,15 +2639,8 @@ static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm
                             hipMemcpyHostToDevice, b->stream));
     const bool direct = own_pcm && pcm_store_coalesced(b);
     const bool defer = lpc_deferred(b);
-    /* the tick's end as a flag the sample kernel stores into pinned memory
-     * (no queue event between it and the deferred LPC; the host polls a
-     * word instead of the runtime): mf_kernel storing the PCM itself, the
-     * timers off.  LPCNET_TICK_FLAG=0 off */
-    const char *tf = getenv("LPCNET_TICK_FLAG");
-    const bool flag = direct && !(tf && atoi(tf) == 0) && !b->fp && !wide_for(b, nB) && !mf2_for(b, nB) && !b->timing;
-    const int seq = flag ? (b->tick_seq = b->tick_seq % 0x3FFFFFFF + 1) : 0;
     if (launch_single_frame_chunked(b, nB, zc_feat ? b->d_io_feat : b->d_feat, direct ? b->d_io_pcm : b->d_pcm, N,
-                                    defer, zc_feat, seq))
+                                    defer, zc_feat))
       return -1;
     if (!direct)
       HIPCHK(hipMemcpyAsync(own_pcm ? b->h_io_pcm : b->h_stg_pcm, b->d_pcm, sizeof(short) * N * nB,
@@ -2697,12 +2657,7 @@ static int synth_first(LPCNetBatch *b, int nB, const float *features, short *pcm
       }
       return 0;
     };
-    if (flag) {
-      if (defer && lpc_after()) return -1;
-      if (tick_wait_flag(b, seq)) return -1;
-    } else if (tick_sync(b, false, defer ? std::function<int()>(lpc_after) : std::function<int()>())) {
-      return -1;
-    }
+    if (tick_sync(b, false, defer ? std::function<int()>(lpc_after) : std::function<int()>())) return -1;
     if (check_status(b)) return -1;
     if (!own_pcm) memcpy(pcm, b->h_stg_pcm, sizeof(short) * N * nB);
     return 0;

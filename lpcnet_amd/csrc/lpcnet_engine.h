@@ -287,32 +287,7 @@ struct SampleArgs {
                             kernel that aborts sets bits (STATUS_*), the host
                             checks after every sync */
   int spin_limit;        /* polls before an LDS flag wait aborts (FLAG_SPIN_LIMIT_DEFAULT) */
-  /* live tick end without a queue event (mf_kernel): every workgroup counts
-   * its arrival in *tick_cnt (device, zero between launches) after a
-   * system-scope release of its PCM stores; the last one resets the count
-   * and stores tick_seq into *tick_flag (the batch's pinned word), which the
-   * host polls.  Null: no flag (the host waits on an event). */
-  unsigned *tick_cnt;
-  int *tick_flag;
-  int tick_seq;
 };
-
-#if defined(__HIP__) || defined(__HIPCC__)
-__device__ __forceinline__ void tick_arrive(const SampleArgs &A)
-{
-  if (!A.tick_flag) return;
-  __threadfence_system(); /* this wave's PCM stores (host memory) performed */
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned n = __hip_atomic_fetch_add(A.tick_cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (n == gridDim.x - 1) {
-      __hip_atomic_store(A.tick_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence_system();
-      __hip_atomic_store(A.tick_flag, A.tick_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-#endif
 
 constexpr int FLAG_SPIN_LIMIT_DEFAULT = 1 << 20; /* lpcnet_batch_set_spin_limit */
 constexpr int FLAG_SPIN_LIMIT_MAX = 1 << 30;     /* larger requests are clamped (int poll counters) */

@@ -86,10 +86,7 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
   __shared__ uint4 img_s[IMG_VAR / 16];
   unsigned char *img = (unsigned char *)img_s;
 
-  if (l2_warm_role(A.mf_emb, (A.nstreams + S - 1) / S)) {
-    tick_arrive(A);
-    return;
-  }
+  if (l2_warm_role(A.mf_emb, (A.nstreams + S - 1) / S)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = blockIdx.x * S;
   const uint32_t *rcp = (const uint32_t *)(img + IMG_RCP);
@@ -129,7 +126,6 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
       const int s = e / total, fn = e % total, f = fn / A.N, n = fn % A.N;
       if (s0 + s < A.nstreams) A.pcm[((size_t)f * A.nstreams + s0 + s) * A.N + n] = 0;
     }
-    tick_arrive(A);
     return;
   }
   for (int o = tid; o < IMG_VAR / 16; o += MF_THREADS) img_s[o] = A.image[o];
@@ -732,7 +728,6 @@ __global__ __launch_bounds__(MF_THREADS) void mf_kernel(SampleArgs A)
     const int s = e / A.N, n = e % A.N;
     if (s0 + s < A.nstreams) pcm_last[(size_t)(s0 + s) * A.N + n] = active[s] ? pcmbuf[s * FRAME + n] : (short)0;
   }
-  tick_arrive(A);
 }
 
 template <int S, int DIAG, bool SPLIT, bool HWR = true>
