@@ -102,13 +102,15 @@ def test_skewed_fp32_on_fp_kernel(require_gpu, B):
 @pytest.mark.parametrize("B,check", [(1, (0,)), (70, (0, 69)), (256, (0, 255)), (1030, (0, 517, 1029))])
 def test_skewed_int8_on_matrix_cores(require_gpu, B, check):
     """Skewed (Sparsify-like) int8 model: the automatic kernel is mf_kernel
-    (split rows), at 1, 2 (70 streams: 1 per workgroup; 1030: 4 per
-    workgroup, ragged); host frames then the multi-frame device path,
-    against the oracle."""
+    (split rows), at 1, 2 (70 streams: 1 per workgroup) and 4 streams per
+    workgroup; above one mf_kernel<4> round (1030 streams, ragged) the wide
+    kernel's split form (round 6); host frames then the multi-frame device
+    path, against the oracle."""
     F = 8
     blob = L.synthetic_model(1, 0, skewed=True)
     b = L.LPCNetBatch(B, 0, blob)
-    assert b.info().quad_path == 4 and b.info().long_rows == 1, b.info().quad_path
+    want = 7 if B > 1024 else 4
+    assert b.info().quad_path == want and b.info().long_rows == 1, b.info().quad_path
     allf = np.ascontiguousarray(np.stack([feats(s, F) for s in range(B)], 1))
     out = np.concatenate([np.stack([b.synthesize(allf[f]) for f in range(3)]), _frames(b, allf, 3, F)], 0)
     assert np.abs(out[3:].astype(np.float64)).mean() > 100
@@ -160,11 +162,13 @@ def test_forced_split_mf2_matches_golden(require_gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("B,check", [(2048, (0, 1031, 2047)), (8192, (0, 4099, 8191))])
-def test_skewed_int8_on_mf2(require_gpu, B, check):
-    """Skewed (trained-like) int8 model at mf2_kernel's batch sizes: the
-    automatic kernel is mf2_kernel's split form; host frames then the
-    chunked multi-frame device path, PCM and final states against the
-    oracle."""
+def test_skewed_int8_on_mf2(require_gpu, monkeypatch, B, check):
+    """Skewed (trained-like) int8 model at mf2_kernel's batch sizes with the
+    wide kernel's split form off (LPCNET_NO_MFW_SPLIT=1; the automatic
+    choice is covered by test_wide_kernel_split_form_matches_oracle):
+    mf2_kernel's split form; host frames then the chunked multi-frame device
+    path, PCM and final states against the oracle."""
+    monkeypatch.setenv("LPCNET_NO_MFW_SPLIT", "1")
     F = 7
     blob = L.synthetic_model(1, 0, skewed=True)
     b = L.LPCNetBatch(B, 0, blob)
