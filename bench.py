@@ -86,6 +86,7 @@ def parse():
     p.add_argument("--variant", choices=["int8", "fp32"], default="int8")
     p.add_argument("--no-batch1", action="store_true", help="skip the batch1 / batch1_fp32 / batch256 lines")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-dropin", action="store_true", help="skip the drop-in API real-time check (dropin_rt)")
     p.add_argument("--no-latency", action="store_true", help="skip the stamped latency run")
     p.add_argument("--no-capacity", action="store_true", help="skip the measured real-time capacity ladder")
     p.add_argument("--live-only", action="store_true",
@@ -826,7 +827,7 @@ def main():
     rank0 = int(os.environ.get("RANK", "0")) == 0
     # the drop-in real-time check runs as a child process, before this
     # process initialises the GPU
-    drt = dropin_rt() if rank0 and world == 1 and not args.no_batch1 and not args.live_only else None
+    drt = dropin_rt() if rank0 and world == 1 and not (args.no_batch1 or args.live_only or args.no_dropin) else None
     world, rank, local, dist = dist_setup(args)
     import lpcnet_amd as L
     variant = L.VARIANT_INT8 if args.variant == "int8" else L.VARIANT_FP32
