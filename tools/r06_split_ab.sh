@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "wide" > gpurun_out/split_pytest.log 2>&1 || { echo "pytest failed"; tail -20 gpurun_out/split_pytest.log; exit 1; }
 tail -1 gpurun_out/split_pytest.log
-for v in default ${VARIANTS:-hlow}; do
+for v in default ${VARIANTS-hlow}; do
   if [ $v = default ]; then unset LPCNET_LIB_VARIANT; else export LPCNET_LIB_VARIANT=$v; fi
   timeout -k 10 200 python tools/skew_tput.py ${BS:-8192} > gpurun_out/skew_$v.log 2>&1 || { echo "skew $v rc=$?"; tail -3 gpurun_out/skew_$v.log; exit 1; }
   echo "$v: $(tail -1 gpurun_out/skew_$v.log)"
