@@ -853,128 +853,49 @@ static long mf_layout(const std::vector<std::vector<int>> &ga, MfPlan &P, const 
   return best;
 }
 
-/* mfw_kernel's split form (trained Sparsify masks on the wide kernel).  The
- * six R waves own their unit blocks' rows up to own caps (Tz for z / r, Th
- * for h); every row's blocks beyond the cap (its remainder) are packed, in
- * row order of decreasing remainder, into 16 bins -- the lane groups of the
- * two host waves (MFW_H_WAVES) -- of Zc (z / r) and Hc (h) 4-slot groups:
- * a bin takes consecutive pieces, a remainder longer than a bin's free
- * slots is cut there, so a bin holds pieces of several rows, each starting
- * at a slot group.  A host lane accumulates its bin slot group by slot
- * group and, after the last group of each piece, adds the int32 partial
- * sums into that row's part words and restarts from zero (htab: per gate
- * and group, the part row a piece ending there goes to, 0xFF none).  Part
- * rows: per gate the unit blocks with a remainder (at most 16) take rows 8
- * slot .. 8 slot + 7.  The caps are chosen to minimise the larger of the
- * busiest R wave's and the host waves' slot groups (the host's weighted
- * 1.15 for their adds), over Tz in {8, 12, 16} and Th in {16, ..., 32}.
- * Exact int32 sums in any order: bit-identical to the unsplit product.
- * Tables: [MFW_TAB_WAVES][MF_LANE_U32][64] as the mf tables, frow
- * [3][SAMPLE_THREADS] (an E thread's part row | 1 << 16 where its unit has
- * a remainder, else MFW_NOROW), htab [4][64 MFW_H_WAVES].  False when no
- * caps fit (more than 16 rows with remainders in a gate, or bins past the
- * register caps). */
+/* mfw_kernel's split form (trained Sparsify masks on the wide kernel): the
+ * six R waves keep the unit blocks of `perm` (the batch's main plan, so the
+ * E waves' lane-ordered tables stay valid) up to the full register caps
+ * (16 z/r, 32 h blocks: the unsplit kernel's largest tables), and every
+ * block beyond goes, in pieces of at most those caps, to the 16 lane groups
+ * of two host waves (MFW_H_WAVES): one piece per host lane group and gate,
+ * longest pieces first, dealt alternately to the two waves.  A host lane's
+ * int32 partial sums reach its row's owner through LDS adds into a compact
+ * part area: per gate, the unit blocks with pieces (at most 16) take part
+ * rows 8 slot .. 8 slot + 7.  Exact int32 sums in any order: bit-identical
+ * to the unsplit product.  Tables: [MFW_TAB_WAVES][MF_LANE_U32][64] as the
+ * mf tables (host waves: their piece at slot 0 of each gate), frow
+ * [3][SAMPLE_THREADS + 128]: an E thread's part row | 1 << 16 when its unit
+ * has pieces (else MFW_NOROW), a host lane's target part row (else
+ * MFW_NOROW).  False when a gate needs more than 16 pieces. */
 struct MfwSplitTab {
   int nzr[MFW_TAB_WAVES] = {}, nh[MFW_TAB_WAVES] = {};
-  int tz = 0, th = 0, zc = 0, hc = 0;
   std::vector<uint32_t> tab;
   std::vector<int> frow;
-  std::vector<uint32_t> htab;
   std::vector<int> units; /* [SAMPLE_THREADS] own unit of each lane (perm below) */
 };
-
-namespace {
-struct MfwBinPiece {
-  int unit, t0, t1, slot; /* blocks [t0, t1) of the unit block's row, from bin slot `slot` */
-};
-
-/* packs one gate's remainders beyond `cap` into 16 bins of `c` slots; false
- * when they do not fit */
-bool mfw_pack(const std::vector<std::vector<int>> &ga, int g, int cap, int c, std::vector<MfwBinPiece> (&bins)[16])
-{
-  constexpr int NUB = NA / 8;
-  std::vector<int> us;
-  for (int u = 0; u < NUB; u++)
-    if ((int)ga[g * NUB + u].size() > cap) us.push_back(u);
-  std::stable_sort(us.begin(), us.end(), [&](int x, int y) { return ga[g * NUB + x].size() > ga[g * NUB + y].size(); });
-  for (auto &v : bins) v.clear();
-  int b = 0, used = 0;
-  for (int u : us) {
-    const int K = (int)ga[g * NUB + u].size();
-    for (int t0 = cap; t0 < K;) {
-      if (used >= c) {
-        if (++b >= 16) return false;
-        used = 0;
-      }
-      const int len = std::min(K - t0, c - used);
-      bins[b].push_back(MfwBinPiece{u, t0, t0 + len, used});
-      used += (len + 3) / 4 * 4;
-      t0 += len;
-    }
-  }
-  return true;
-}
-}  // namespace
 
 static bool mfw_split_tables(const std::vector<std::vector<int>> &ga, const std::vector<int> &ga_first,
                              const int8_t *wa, MfwSplitTab &T)
 {
-  constexpr int NUB = NA / 8, NHL = 64 * MFW_H_WAVES;
-  g_mf_simd_weight = getenv("LPCNET_MF_SIMD_W") ? atoi(getenv("LPCNET_MF_SIMD_W")) : 25;
-  /* caps search: R cost from a short unit-block search, host cost from the packing */
-  long best = -1;
-  int bt[2] = {0, 0}, bc[2] = {0, 0};
-  const char *capenv = getenv("LPCNET_MFW_CAPS"); /* tuning hook "Tz,Th" */
-  int fz = 0, fh = 0;
-  if (capenv && sscanf(capenv, "%d,%d", &fz, &fh) != 2) fz = fh = 0;
-  for (int tz = 8; tz <= MF_ZMAX; tz += 4)
-    for (int th = 16; th <= MF_HMAX; th += 4) {
-      if (fz && (tz != fz || th != fh)) continue;
-      int nrem[3] = {0, 0, 0};
-      for (int g = 0; g < 3; g++)
-        for (int u = 0; u < NUB; u++) nrem[g] += (int)ga[g * NUB + u].size() > (g < 2 ? tz : th);
-      if (nrem[0] > 16 || nrem[1] > 16 || nrem[2] > 16) continue;
-      std::vector<MfwBinPiece> bins[16];
-      int zc = 1, hc = 1;
-      while (zc <= MF_ZMAX / 4 && !(mfw_pack(ga, 0, tz, 4 * zc, bins) && mfw_pack(ga, 1, tz, 4 * zc, bins))) zc++;
-      while (hc <= MF_HMAX / 4 && !mfw_pack(ga, 2, th, 4 * hc, bins)) hc++;
-      if (zc > MF_ZMAX / 4 || hc > MF_HMAX / 4) continue;
-      std::vector<std::vector<int>> own(ga.size());
-      for (int g = 0; g < 3; g++)
-        for (int u = 0; u < NUB; u++) {
-          const std::vector<int> &v = ga[g * NUB + u];
-          own[g * NUB + u].assign(v.begin(), v.begin() + std::min((int)v.size(), g < 2 ? tz : th));
-        }
-      const std::vector<int> perm = mf_assign_unit_blocks(own, nullptr, 3000);
-      int rmax = 0;
-      for (int w = 0; w < SAMPLE_WAVES; w++) rmax = std::max(rmax, mf_wave_cost(own, &perm[8 * w]));
-      const long hcost = (115L * (8 * zc + 4 * hc)) / 100;
-      const long sc = std::max((long)rmax, hcost) * 64 + (8 * zc + 4 * hc);
-      if (best < 0 || sc < best) {
-        best = sc;
-        bt[0] = tz;
-        bt[1] = th;
-        bc[0] = zc;
-        bc[1] = hc;
-      }
-    }
-  if (best < 0) return false;
-  T.tz = bt[0];
-  T.th = bt[1];
-  T.zc = bc[0];
-  T.hc = bc[1];
-  const int cap[3] = {bt[0], bt[0], bt[1]};
-  std::vector<MfwBinPiece> bins[3][16];
-  for (int g = 0; g < 3; g++)
-    if (!mfw_pack(ga, g, cap[g], 4 * (g < 2 ? bc[0] : bc[1]), bins[g])) return false;
-  /* part rows: per gate the unit blocks with remainders */
+  constexpr int NUB = NA / 8, NHL = 8 * MFW_H_WAVES, FS = SAMPLE_THREADS + 64 * MFW_H_WAVES;
+  const int cap[3] = {MF_ZMAX, MF_ZMAX, MF_HMAX};
+  std::vector<MfPiece> pcs[3];
+  std::vector<int> host[3]; /* host lane group (0..15) -> piece index */
   std::vector<int> slot_of_ub[3];
   for (int g = 0; g < 3; g++) {
+    for (int u = 0; u < NUB; u++) {
+      const int K = (int)ga[g * NUB + u].size();
+      for (int t0 = cap[g]; t0 < K; t0 += cap[g]) pcs[g].push_back(MfPiece{u, t0, std::min(K, t0 + cap[g])});
+    }
+    if ((int)pcs[g].size() > NHL) return false;
+    std::stable_sort(pcs[g].begin(), pcs[g].end(), [](const MfPiece &a, const MfPiece &b) { return a.t1 - a.t0 > b.t1 - b.t0; });
+    host[g].assign(NHL, -1);
+    for (int k = 0; k < (int)pcs[g].size(); k++) host[g][(k % MFW_H_WAVES) * 8 + k / MFW_H_WAVES] = k;
     slot_of_ub[g].assign(NUB, -1);
     int ns = 0;
-    for (auto &bv : bins[g])
-      for (const MfwBinPiece &pc : bv)
-        if (slot_of_ub[g][pc.unit] < 0) slot_of_ub[g][pc.unit] = ns++;
+    for (const MfPiece &pc : pcs[g])
+      if (slot_of_ub[g][pc.unit] < 0) slot_of_ub[g][pc.unit] = ns++;
     if (ns > 16) return false;
   }
   /* own unit blocks over the six R waves for the capped rows (the wide
@@ -985,95 +906,68 @@ static bool mfw_split_tables(const std::vector<std::vector<int>> &ga, const std:
       const std::vector<int> &v = ga[g * NUB + u];
       own[g * NUB + u].assign(v.begin(), v.begin() + std::min((int)v.size(), cap[g]));
     }
+  g_mf_simd_weight = getenv("LPCNET_MF_SIMD_W") ? atoi(getenv("LPCNET_MF_SIMD_W")) : 25;
   const std::vector<int> perm = mf_assign_unit_blocks(own, nullptr, 40000);
   T.units.assign(SAMPLE_THREADS, 0);
   for (int t = 0; t < SAMPLE_THREADS; t++) T.units[t] = 8 * perm[t / 8] + (t & 7);
   T.tab.assign((size_t)MFW_TAB_WAVES * MF_LANE_U32 * 64, 0);
-  T.frow.assign((size_t)3 * SAMPLE_THREADS, MFW_NOROW);
-  T.htab.assign((size_t)4 * NHL, 0xFFFFFFFFu);
+  T.frow.assign((size_t)3 * FS, MFW_NOROW);
   for (int w = 0; w < MFW_TAB_WAVES; w++) {
     const bool hw = w >= SAMPLE_WAVES;
-    auto word = [&](int k, int l) -> uint32_t & { return T.tab[((size_t)w * MF_LANE_U32 + k) * 64 + l]; };
-    if (!hw) {
-      /* R wave: its own rows, bank-disjoint slot order (mf_bank_slots) */
-      int kz = 1, kh = 1;
-      for (int j = 0; j < 8; j++) {
-        const int u = perm[w * 8 + j];
-        kz = std::max(kz, (int)std::max(own[u].size(), own[NUB + u].size()));
-        kh = std::max(kh, (int)own[2 * NUB + u].size());
-      }
-      T.nzr[w] = (kz + 3) / 4;
-      T.nh[w] = (kh + 3) / 4;
-      for (int g = 0; g < 3; g++) {
-        const int base = g == 0 ? 0 : (g == 1 ? MF_ZMAX : 2 * MF_ZMAX);
-        const int nslot = 4 * (g < 2 ? T.nzr[w] : T.nh[w]);
-        for (int half = 0; half < 2; half++) {
-          const std::vector<int> *rows4[4];
-          for (int k = 0; k < 4; k++) rows4[k] = &own[g * NUB + perm[w * 8 + 4 * half + k]];
-          int slot_of[4][MF_HMAX], cb_at[4][MF_HMAX];
-          mf_bank_slots(rows4, nslot, slot_of, cb_at);
-          for (int k = 0; k < 4; k++) {
-            const int j = 4 * half + k, rb = g * NUB + perm[w * 8 + j];
-            for (int r = 0; r < 8; r++) {
-              const int l = 8 * j + r;
-              for (int t = 0; t < (int)rows4[k]->size(); t++)
-                memcpy(&word(base + slot_of[k][t], l), wa + 32 * (ga_first[rb] + t) + 4 * r, 4);
-              for (int t = 0; t < nslot; t++) word(MF_GA + (base + t) / 4, l) |= (uint32_t)cb_at[k][t] << (8 * ((base + t) & 3));
-            }
-          }
-        }
-      }
-      continue;
-    }
-    /* host wave: bins (w - 6) * 8 + j in slot order; an empty slot reads a
-     * quad the half's first lane group reads there (broadcast, zero weight) */
-    const int hw0 = w - SAMPLE_WAVES;
-    int uz = 1, uh = 1;
+    /* this wave's rows per lane group and gate: (row block, first, end) */
+    int rb[8][3], t0[8][3], t1[8][3];
+    int kz = 1, kh = 1; /* at least one slot group (zero weights: exact) */
     for (int j = 0; j < 8; j++)
-      for (int g = 0; g < 3; g++)
-        for (const MfwBinPiece &pc : bins[g][hw0 * 8 + j])
-          (g < 2 ? uz : uh) = std::max(g < 2 ? uz : uh, pc.slot + (pc.t1 - pc.t0 + 3) / 4 * 4);
-    T.nzr[w] = (uz + 3) / 4;
-    T.nh[w] = (uh + 3) / 4;
+      for (int g = 0; g < 3; g++) {
+        rb[j][g] = -1;
+        t0[j][g] = t1[j][g] = 0;
+        if (!hw) {
+          const int u = perm[w * 8 + j];
+          rb[j][g] = g * NUB + u;
+          t1[j][g] = std::min((int)ga[rb[j][g]].size(), cap[g]);
+        } else if (host[g][(w - SAMPLE_WAVES) * 8 + j] >= 0) {
+          const MfPiece &pc = pcs[g][host[g][(w - SAMPLE_WAVES) * 8 + j]];
+          rb[j][g] = g * NUB + pc.unit;
+          t0[j][g] = pc.t0;
+          t1[j][g] = pc.t1;
+          for (int r = 0; r < 8; r++)
+            T.frow[(size_t)g * FS + SAMPLE_THREADS + (w - SAMPLE_WAVES) * 64 + 8 * j + r] =
+                8 * slot_of_ub[g][pc.unit] + r;
+        }
+        (g < 2 ? kz : kh) = std::max(g < 2 ? kz : kh, t1[j][g] - t0[j][g]);
+      }
+    T.nzr[w] = (kz + 3) / 4;
+    T.nh[w] = (kh + 3) / 4;
+    auto word = [&](int k, int l) -> uint32_t & { return T.tab[((size_t)w * MF_LANE_U32 + k) * 64 + l]; };
     for (int g = 0; g < 3; g++) {
       const int base = g == 0 ? 0 : (g == 1 ? MF_ZMAX : 2 * MF_ZMAX);
       const int nslot = 4 * (g < 2 ? T.nzr[w] : T.nh[w]);
-      int quad[8][MF_HMAX];
-      for (int j = 0; j < 8; j++)
-        for (int t = 0; t < MF_HMAX; t++) quad[j][t] = -1;
-      for (int j = 0; j < 8; j++)
-        for (const MfwBinPiece &pc : bins[g][hw0 * 8 + j]) {
-          const int rb = g * NUB + pc.unit;
-          for (int t = pc.t0; t < pc.t1; t++) {
-            const int sl = pc.slot + (t - pc.t0);
-            quad[j][sl] = ga[rb][t] / 4;
-            for (int r = 0; r < 8; r++) memcpy(&word(base + sl, 8 * j + r), wa + 32 * (ga_first[rb] + t) + 4 * r, 4);
-          }
-          /* the part row this piece's last slot group adds into */
-          const int lastg = (pc.slot + pc.t1 - pc.t0 - 1) / 4, hw_ = g < 2 ? g : (lastg < 4 ? 2 : 3);
-          const int sh = 8 * (g < 2 ? lastg : lastg & 3);
+      for (int half = 0; half < 2; half++) {
+        std::vector<int> lists[4];
+        for (int k = 0; k < 4; k++) {
+          const int j = 4 * half + k;
+          if (rb[j][g] >= 0) lists[k].assign(ga[rb[j][g]].begin() + t0[j][g], ga[rb[j][g]].begin() + t1[j][g]);
+        }
+        const std::vector<int> *rows4[4] = {&lists[0], &lists[1], &lists[2], &lists[3]};
+        int slot_of[4][MF_HMAX], cb_at[4][MF_HMAX];
+        mf_bank_slots(rows4, nslot, slot_of, cb_at);
+        for (int k = 0; k < 4; k++) {
+          const int j = 4 * half + k;
           for (int r = 0; r < 8; r++) {
-            uint32_t &e = T.htab[(size_t)hw_ * NHL + hw0 * 64 + 8 * j + r];
-            e = (e & ~(0xFFu << sh)) | (uint32_t)(8 * slot_of_ub[g][pc.unit] + r) << sh;
+            const int l = 8 * j + r;
+            for (int t = 0; t < (int)lists[k].size(); t++)
+              memcpy(&word(base + slot_of[k][t], l), wa + 32 * (ga_first[rb[j][g]] + t0[j][g] + t) + 4 * r, 4);
+            for (int t = 0; t < nslot; t++) word(MF_GA + (base + t) / 4, l) |= (uint32_t)cb_at[k][t] << (8 * ((base + t) & 3));
           }
         }
-      for (int half = 0; half < 2; half++)
-        for (int t = 0; t < nslot; t++) {
-          int fill = 0;
-          for (int k = 0; k < 4; k++)
-            if (quad[4 * half + k][t] >= 0) { fill = quad[4 * half + k][t]; break; }
-          for (int k = 0; k < 4; k++) {
-            const int j = 4 * half + k, cb = quad[j][t] >= 0 ? quad[j][t] : fill;
-            for (int r = 0; r < 8; r++) word(MF_GA + (base + t) / 4, 8 * j + r) |= (uint32_t)cb << (8 * ((base + t) & 3));
-          }
-        }
+      }
     }
   }
   /* the E threads' merge entries: thread t owns unit 8 perm[t / 8] + t % 8 */
   for (int g = 0; g < 3; g++)
     for (int t = 0; t < SAMPLE_THREADS; t++) {
-      const int sl = slot_of_ub[g][perm[t / 8]];
-      if (sl >= 0) T.frow[(size_t)g * SAMPLE_THREADS + t] = (8 * sl + (t % 8)) | 1 << 16;
+      const int u = perm[t / 8], sl = slot_of_ub[g][u];
+      if (sl >= 0) T.frow[(size_t)g * FS + t] = (8 * sl + (t % 8)) | 1 << 16;
     }
   return true;
 }
@@ -1866,7 +1760,6 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
       UP(sa.mfw_tab, mfw_tabs.tab.data(), mfw_tabs.tab.size() * 4);
       UP(sa.mfw_frow, mfw_tabs.frow.data(), mfw_tabs.frow.size() * 4);
       UP(sa.mfw_unit, mfw_tabs.units.data(), mfw_tabs.units.size() * 4);
-      UP(sa.mfw_htab, mfw_tabs.htab.data(), mfw_tabs.htab.size() * 4);
     }
     {
       /* Range of the GRU_A gates' inputs for the elementwise fast path:
@@ -2277,8 +2170,7 @@ LPCNET_EXPORT const char *lpcnet_mi355x_last_error(void) { return g_err.c_str();
  * device): the main plan (mf_plan, wide class) and, for split models, the
  * wide kernel's split tables.  out[0] = split (0/1), out[1] = mfw split form
  * available (0/1), out[2..17] = the split form's z/r and h 4-slot groups per
- * table wave (R waves 0..5, host waves 6..7), out[18..21] = its own caps
- * (z/r, h) and host bin groups (z/r, h).
+ * table wave (R waves 0..5, host waves 6..7), out[18..20] = pieces per gate.
  * 0 / -1 (malformed blob or no int8 matrix-core plan). */
 LPCNET_EXPORT int lpcnet_mi355x_wide_plan(const unsigned char *data, int len, int *out)
 {
@@ -2300,10 +2192,14 @@ LPCNET_EXPORT int lpcnet_mi355x_wide_plan(const unsigned char *data, int len, in
     out[2 + 2 * w] = T.nzr[w];
     out[3 + 2 * w] = T.nh[w];
   }
-  out[18] = T.tz;
-  out[19] = T.th;
-  out[20] = T.zc;
-  out[21] = T.hc;
+  for (int g = 0; g < 3; g++) {
+    int n = 0;
+    for (int u = 0; u < NA / 8; u++) {
+      const int K = (int)ga[g * (NA / 8) + u].size(), c = g < 2 ? MF_ZMAX : MF_HMAX;
+      if (K > c) n += (K - c + c - 1) / c;
+    }
+    out[18 + g] = n;
+  }
   return 0;
 }
 

@@ -253,13 +253,12 @@ struct SampleArgs {
   int mf_nfh[SAMPLE_WAVES];
   const int *mf_frow;
   /* mfw_kernel's split form: [MFW_TAB_WAVES][MF_LANE_U32][64] tables (R
-   * waves own rows to the caps, host waves the packed remainders), group
-   * counts, frow [3][SAMPLE_THREADS] (see mfw_split_tables) */
+   * waves own rows to the full caps, host waves the pieces), group counts,
+   * frow [3][SAMPLE_THREADS + 64 MFW_H_WAVES] (see mfw_split_tables) */
   int mfw_split;
   const uint32_t *mfw_tab;
   const int *mfw_frow;
   const int *mfw_unit;      /* [SAMPLE_THREADS]: the split form's own unit of each E / R lane */
-  const uint32_t *mfw_htab; /* [4][64 MFW_H_WAVES]: host lanes' part rows by slot group (z, r, h 0-3, h 4-7) */
   const float *mfw_emb[3];  /* embedding tables in the split form's lane order (as mf_emb) */
   int mfw_nzr[MFW_TAB_WAVES];
   int mfw_nh[MFW_TAB_WAVES];

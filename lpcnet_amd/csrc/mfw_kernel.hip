@@ -243,64 +243,6 @@ __device__ __forceinline__ void mfw_zr(const unsigned char *xg, const uint32_t (
   }
 }
 
-/* the host waves' forms of mfw_zr / mfw_gate: after each 4-slot group's
- * MFMAs, end(group) (flush the pieces ending there) */
-template <int NG, typename End>
-__device__ __forceinline__ void mfw_zr_host(const unsigned char *xg, const uint32_t (&wz)[4 * NG], const uint32_t (&wr)[4 * NG],
-                                            const uint32_t (&cz)[NG], const uint32_t (&cr)[NG], uint32_t mo, v4i &az, v4i &ar,
-                                            End end)
-{
-  uint32_t xz[NG][4], xr[NG][4];
-#pragma unroll
-  for (int d = 0; d < MFW_XD && d < NG; d++)
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      xz[d][k] = mfw_x(xg, cz, 4 * d + k, mo);
-      xr[d][k] = mfw_x(xg, cr, 4 * d + k, mo);
-    }
-#pragma unroll
-  for (int g = 0; g < NG; g++) {
-    if (g + MFW_XD < NG) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        xz[g + MFW_XD][k] = mfw_x(xg, cz, 4 * (g + MFW_XD) + k, mo);
-        xr[g + MFW_XD][k] = mfw_x(xg, cr, 4 * (g + MFW_XD) + k, mo);
-      }
-    }
-    MFW_FENCE();
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      az = mfma4(xz[g][k], wz[4 * g + k], az);
-      ar = mfma4(xr[g][k], wr[4 * g + k], ar);
-    }
-    end(g);
-    MFW_FENCE();
-  }
-}
-
-template <int NG, typename End>
-__device__ __forceinline__ void mfw_gate_host(const unsigned char *xg, const uint32_t (&w)[4 * NG], const uint32_t (&cw)[NG],
-                                              uint32_t mo, v4i &a, End end)
-{
-  uint32_t x[NG][4];
-#pragma unroll
-  for (int d = 0; d < MFW_XD && d < NG; d++)
-#pragma unroll
-    for (int k = 0; k < 4; k++) x[d][k] = mfw_x(xg, cw, 4 * d + k, mo);
-#pragma unroll
-  for (int g = 0; g < NG; g++) {
-    if (g + MFW_XD < NG) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) x[g + MFW_XD][k] = mfw_x(xg, cw, 4 * (g + MFW_XD) + k, mo);
-    }
-    MFW_FENCE();
-#pragma unroll
-    for (int k = 0; k < 4; k++) a = mfma4(x[g][k], w[4 * g + k], a);
-    end(g);
-    MFW_FENCE();
-  }
-}
-
 /* ---- R role: GRU_A recurrent products (nnet.c:441) ------------------------ */
 /* HOST (split form, r = 6, 7: the host waves): the lane's piece of another
  * unit's row, accumulated from 0, its int32 partial sums added into that
@@ -328,16 +270,11 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
 #pragma unroll
   for (int k = 0; k < H; k++) ch[k] = mt[(MF_GA + 2 * MF_ZMAX / 4 + k) * 64];
   int wsz = 0, wsr = 0, wsh = 0;
-  /* HOST: per gate and slot group, the part row a piece ending at that
-   * group adds into (8 bits each, 0xFF none): z, r, h groups 0-3, 4-7 */
-  uint32_t hz = 0, hr = 0, hh0 = 0, hh1 = 0;
+  uint32_t tgt = 0; /* HOST: part rows of the lane's pieces, 9 bits per gate */
   if constexpr (HOST) {
-    constexpr int NHL = 64 * MFW_H_WAVES;
-    const uint32_t *ht = A.mfw_htab + (r - SAMPLE_WAVES) * 64 + lane;
-    hz = ht[0];
-    hr = ht[NHL];
-    hh0 = ht[2 * NHL];
-    hh1 = ht[3 * NHL];
+    const int *fr = A.mfw_frow + SAMPLE_THREADS + (r - SAMPLE_WAVES) * 64 + lane;
+    constexpr int FS = SAMPLE_THREADS + 64 * MFW_H_WAVES;
+    tgt = (uint32_t)fr[0] | (uint32_t)fr[FS] << 9 | (uint32_t)fr[2 * FS] << 18;
   } else {
     const int i = (SPLIT ? A.mfw_unit : A.mf_unit)[r * 64 + lane];
     wsz = A.ga_wsum[i];
@@ -370,30 +307,28 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
     /* one accumulator per gate: a 4x4x4 MFMA issues every ~13 cycles
      * whether its accumulator chains or not (tools/probes/mfma_timing.hip) */
     v4i vz = {wsz, wsz, wsz, wsz}, vr = {wsr, wsr, wsr, wsr}, vh[1] = {{wsh, wsh, wsh, wsh}};
+    mfw_zr<Z>(xg, wz, wr, cz, cr, mo, vz, vr);
     if constexpr (HOST) {
-      /* the lane's bin, slot group by slot group; after the last group of
-       * each piece its int32 partial sums go into the row's part words
-       * (two streams per 64-bit add: hi 2^32 + lo, lo sign-extended, as
-       * mf_common.h part_add PACK) and the accumulator restarts */
-      uint32_t tq[4] = {hz, hr, hh0, hh1};
-      asm volatile("" : "+v"(tq[0]), "+v"(tq[1]), "+v"(tq[2]), "+v"(tq[3]));
+      /* exact LDS adds into the owners' part words, two streams per 64-bit
+       * add (hi 2^32 + lo, lo sign-extended: mf_common.h part_add PACK); one
+       * piece per lane and gate, lanes without one skip.  z / r go out
+       * before the h product, so their adds complete under its MFMAs */
+      uint32_t tq = tgt;
+      asm volatile("" : "+v"(tq));
       unsigned long long *pp = (unsigned long long *)prt + (p & 1) * 3 * MFW_PART_ROWS * (MFW_S / 2);
-      auto flush = [&](int q, uint32_t t, v4i &v) {
-        if (t != 0xFFu) {
+      auto padd = [&](int q, const v4i &v) {
+        const int t = (int)((tq >> (9 * q)) & 0x1FF);
+        if (t != MFW_NOROW)
 #pragma unroll
           for (int k = 0; k < MFW_S / 2; k++)
-            atomicAdd(&pp[(q * MFW_PART_ROWS + (int)t) * (MFW_S / 2) + k],
+            atomicAdd(&pp[(q * MFW_PART_ROWS + t) * (MFW_S / 2) + k],
                       ((unsigned long long)(uint32_t)v[2 * k + 1] << 32) + (unsigned long long)(long long)v[2 * k]);
-          v = v4i{0, 0, 0, 0};
-        }
       };
-      mfw_zr_host<Z>(xg, wz, wr, cz, cr, mo, vz, vr, [&](int gi) {
-        flush(0, (tq[0] >> (8 * gi)) & 0xFFu, vz);
-        flush(1, (tq[1] >> (8 * gi)) & 0xFFu, vr);
-      });
-      mfw_gate_host<H>(xg, wh, ch, mo, vh[0], [&](int gi) { flush(2, (tq[2 + (gi >> 2)] >> (8 * (gi & 3))) & 0xFFu, vh[0]); });
+      padd(0, vz);
+      padd(1, vr);
+      mfw_gate<H, 1>(xg, wh, ch, mo, vh);
+      padd(2, vh[0]);
     } else {
-      mfw_zr<Z>(xg, wz, wr, cz, cr, mo, vz, vr);
       mfw_gate<H, 1>(xg, wh, ch, mo, vh);
     }
     if constexpr (HOST) {
@@ -562,7 +497,7 @@ __global__ __launch_bounds__(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS) void mfw_k
      * unit has pieces there (bits 27..29), one register for the launch */
     uint32_t frow = 0;
     if constexpr (SPLIT) {
-      constexpr int FS = SAMPLE_THREADS;
+      constexpr int FS = SAMPLE_THREADS + 64 * MFW_H_WAVES;
       const int *fro = A.mfw_frow + tid;
       const uint32_t e0 = fro[0], e1 = fro[FS], e2 = fro[2 * FS];
       frow = (e0 & 0x1FF) | (e1 & 0x1FF) << 9 | (e2 & 0x1FF) << 18 | (e0 >> 16 & 1) << 27 | (e1 >> 16 & 1) << 28 |

@@ -293,9 +293,8 @@ def test_wide_split_plan_host_only():
     """lpcnet_mi355x_wide_plan (host only): the default synthetic model needs
     no split; the trained-like skewed one (Sparsify masks, block rows up to
     76 / 59 / 96 blocks) gets the wide kernel's split form -- R waves within
-    the register caps (<= 4 z/r and 8 h slot groups), own caps within them,
-    the remainders packed into the two host waves' bins of at most 4 / 8
-    slot groups."""
+    the register caps (<= 4 z/r and 8 h slot groups), its pieces (one per
+    host lane group and gate, <= 16 per gate) on the two host waves."""
     import ctypes as C
     f = L.lib.lpcnet_mi355x_wide_plan
     f.restype = C.c_int
@@ -306,6 +305,4 @@ def test_wide_split_plan_host_only():
     assert f(blob, len(blob), out) == 0 and out[0] == 1 and out[1] == 1
     groups = [(out[2 + 2 * w], out[3 + 2 * w]) for w in range(8)]
     assert all(1 <= z <= 4 and 1 <= h <= 8 for z, h in groups), groups
-    tz, th, zc, hc = out[18:22]
-    assert 4 <= tz <= 16 and 4 <= th <= 32 and 1 <= zc <= 4 and 1 <= hc <= 8, (tz, th, zc, hc)
-    assert all(groups[6 + h][0] <= zc and groups[6 + h][1] <= hc for h in range(2)), (groups, zc, hc)
+    assert all(0 < n <= 16 for n in out[18:21]), list(out[18:21])
