@@ -105,13 +105,16 @@ LPCNET_EXPORT int lpcnet_batch_nb_streams(const LPCNetBatch *b);
  * Returns 0, or -1 on error (no model, bad N). */
 LPCNET_EXPORT int lpcnet_batch_synthesize(LPCNetBatch *b, const float *features, short *pcm, int N);
 
-/* The batch's own pinned host buffers for a live server's tick (features
- * [B][NB_FEATURES], PCM [B][160]; allocated on first use, freed with the
- * batch, NULL on error).  lpcnet_batch_synthesize with these pointers skips
- * its host staging copies: the features go to the device in one DMA copy,
- * and the sample kernel stores the PCM into the (mapped) PCM buffer itself
- * where its write-out is coalesced -- no device-to-host copy.  The PCM
- * buffer holds a frame's output until the next synthesis call. */
+/* The batch's own host-addressable buffers for a live server's tick
+ * (features [B][NB_FEATURES], PCM [B][160]; allocated on first use, freed
+ * with the batch, NULL on error).  lpcnet_batch_synthesize with these
+ * pointers skips its host staging copies: the kernels read the features
+ * where they are, and the sample kernel stores the PCM into the (mapped,
+ * pinned) PCM buffer itself where its write-out is coalesced -- no
+ * device-to-host copy.  The feature buffer is host-visible device memory on
+ * a large-BAR device (write it from the host; reads back are slow uncached
+ * PCIe reads; LPCNET_FEAT_VRAM=0: mapped pinned host memory instead).  The
+ * PCM buffer holds a frame's output until the next synthesis call. */
 LPCNET_EXPORT float *lpcnet_batch_host_features(LPCNetBatch *b);
 LPCNET_EXPORT short *lpcnet_batch_host_pcm(LPCNetBatch *b);
 
