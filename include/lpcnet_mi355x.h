@@ -283,6 +283,12 @@ LPCNET_EXPORT int lpcnet_mi355x_device_numerics(int device, int op, const void *
 LPCNET_EXPORT int lpcnet_mi355x_validate_model(const unsigned char *data, int len);
 /* Number of visible HIP devices (0 on a machine without GPU). */
 LPCNET_EXPORT int lpcnet_mi355x_device_count(void);
+/* Host-only view of the GRU_A plans a blob (data, len) gets on a wide batch
+ * (no device touched): out[0] = split model (0/1), out[1] = mfw_kernel's
+ * split form available (0/1), out[2 + 2w], out[3 + 2w] = its z/r and h
+ * 4-slot groups of table wave w (R waves 0..5, host waves 6..7),
+ * out[18..20] = pieces per gate.  int out[24].  0 / -1. */
+LPCNET_EXPORT int lpcnet_mi355x_wide_plan(const unsigned char *data, int len, int *out);
 /* The drop-in handles (include/lpcnet.h) bound to the same model on the
  * same device share one device copy of it and one work batch; concurrent
  * lpcnet_synthesize calls on them coalesce into one launch.  Statistics of
