@@ -109,8 +109,12 @@ __device__ __forceinline__ float sigmoid_x86(float X, const uint32_t *tab)
 }
 
 /* N independent rcp_x86: all N table reads are issued before any is pinned,
- * so their LDS latencies overlap (rcp_x86's pin alone serialises a chain). */
-template <int N, bool HW = false>
+ * so their LDS latencies overlap (rcp_x86's pin alone serialises a chain).
+ * TB: the table's index bits.  11 reads a 2,048-entry table of the x86
+ * entries themselves (kRcpTable, 11-bit prefixes: mfw_kernel's split form,
+ * whose models run with that table only), the default 12 the device table
+ * of every other kernel (RCP_ENTRIES, any host's). */
+template <int N, bool HW = false, int TB = RCP_TABLE_BITS>
 __device__ __forceinline__ void rcp_x86_n(float (&x)[N], const uint32_t *tab)
 {
   if constexpr (HW) {
@@ -120,7 +124,7 @@ __device__ __forceinline__ void rcp_x86_n(float (&x)[N], const uint32_t *tab)
   }
   uint32_t t[N];
 #pragma unroll
-  for (int k = 0; k < N; k++) t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(x[k]), 23 - RCP_TABLE_BITS, RCP_TABLE_BITS)];
+  for (int k = 0; k < N; k++) t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(x[k]), 23 - TB, TB)];
 #pragma unroll
   for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
 #pragma unroll
@@ -152,7 +156,7 @@ __device__ __forceinline__ void sigmoid_x86_n(float (&X)[N], const uint32_t *tab
  * rcp_x86_fix) and no NaN can arise, so the result is rcp_x86 / clamp_x86
  * without the flush select and the NaN select: identical to sigmoid_x86_n
  * for every such input.  Used for the int8 products' z / r gates. */
-template <int N, bool HW = false>
+template <int N, bool HW = false, int TB = RCP_TABLE_BITS>
 __device__ __forceinline__ void sigmoid_x86_fin_n(float (&X)[N], const uint32_t *tab)
 {
   float num[N], den[N];
@@ -175,7 +179,7 @@ __device__ __forceinline__ void sigmoid_x86_fin_n(float (&X)[N], const uint32_t 
     num[k] = __builtin_fmaf(__builtin_fmaf(0.00950985f, X2, 6.02452230f), X2, 238.13200378f);
     den[k] = __builtin_fmaf(__builtin_fmaf(0.74287558f, X2, 103.34200287f), X2, 952.72399902f);
     num[k] = num[k] * X[k];
-    t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(den[k]), 23 - RCP_TABLE_BITS, RCP_TABLE_BITS)];
+    t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(den[k]), 23 - TB, TB)];
   }
 #pragma unroll
   for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
@@ -186,7 +190,7 @@ __device__ __forceinline__ void sigmoid_x86_fin_n(float (&X)[N], const uint32_t 
   }
 }
 
-template <int N, bool HW = false>
+template <int N, bool HW = false, int TB = RCP_TABLE_BITS>
 __device__ __forceinline__ void tanh_x86_n(float (&X)[N], const uint32_t *tab)
 {
   float num[N], den[N];
@@ -197,7 +201,7 @@ __device__ __forceinline__ void tanh_x86_n(float (&X)[N], const uint32_t *tab)
     den[k] = __builtin_fmaf(__builtin_fmaf(11.88600922f, X2, 413.36801147f), X2, 952.72399902f);
     num[k] = num[k] * X[k];
   }
-  rcp_x86_n<N, HW>(den, tab);
+  rcp_x86_n<N, HW, TB>(den, tab);
 #pragma unroll
   for (int k = 0; k < N; k++) X[k] = clamp_x86(num[k] * den[k], -1.f, 1.f);
 }
@@ -206,7 +210,7 @@ __device__ __forceinline__ void tanh_x86_n(float (&X)[N], const uint32_t *tab)
  * denominator lies in [952.72, 2^125), so rcpps never flushes and no NaN
  * arises: rcp_x86 / clamp_x86 without their flush and NaN selects, identical
  * to tanh_x86_n for every such input (mf_kernel's bounded-input path). */
-template <int N, bool HW = false>
+template <int N, bool HW = false, int TB = RCP_TABLE_BITS>
 __device__ __forceinline__ void tanh_x86_fin_n(float (&X)[N], const uint32_t *tab)
 {
   float num[N], den[N];
@@ -224,7 +228,7 @@ __device__ __forceinline__ void tanh_x86_fin_n(float (&X)[N], const uint32_t *ta
   }
   uint32_t t[N];
 #pragma unroll
-  for (int k = 0; k < N; k++) t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(den[k]), 23 - RCP_TABLE_BITS, RCP_TABLE_BITS)];
+  for (int k = 0; k < N; k++) t[k] = tab[__builtin_amdgcn_ubfe(__float_as_uint(den[k]), 23 - TB, TB)];
 #pragma unroll
   for (int k = 0; k < N; k++) asm volatile("" : "+v"(t[k]));
 #pragma unroll

@@ -326,9 +326,9 @@ struct LPCNetBatch {
   int mfw_g = 3;         /* mfw_kernel's four-stream groups per workgroup (2 or 3) */
   bool mfw_forced = false; /* LPCNET_MFW=1: mfw_kernel for every launch, however narrow */
   int cus = 256;           /* compute units of the batch's device */
-  bool mfw = false;      /* wider batches: mfw_kernel (three 4-stream groups, dedicated gather /
-                            recurrent / sampler waves) for the same launches, non-split models with the
-                            default rcpps */
+  bool mfw = false;      /* wider batches: mfw_kernel (two or three 4-stream groups, dedicated gather /
+                            recurrent / sampler waves; split models in its split form) for the same
+                            launches, models with the default rcpps */
   bool plan_wide = false; /* the register tables were planned for mfw_kernel (plan class 3) */
   L2Warm ck_warm{};       /* the chunk kernel's re-tiled weights (deferred LPC warms them) */
   std::vector<unsigned char> blob; /* the loaded model's blob: replanned when the kernel choice moves */
@@ -1378,7 +1378,9 @@ int load_model(LPCNetBatch *b, const unsigned char *data, int len, bool upload =
     const bool wide = mfw_planned(b, current_device_cus());
     b->plan_wide = wide;
     const int cls = b->B >= MF2_MIN_STREAMS ? 2 : b->B >= 1024 ? 1 : 0;
-    /* split plans never run the wide kernel */
+    /* a split plan's own tables serve mf_kernel / mf2_kernel (class cls);
+     * the wide kernel's split form gets tables of its own below
+     * (mfw_split_tables) */
     mf_ok = mf_plan(ga_blocks, plan, wide ? 3 : cls, cls);
   }
   if (getenv("LPCNET_VERBOSE")) {

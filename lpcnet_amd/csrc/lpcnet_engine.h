@@ -369,8 +369,9 @@ int mf2_lds_bytes(int S, int split);
 int launch_mf2(const SampleArgs &a, int S, void *stream);
 /* wide-batch kernel (mfw_kernel.hip): 2 or 3 four-stream groups per
  * 896-thread workgroup with dedicated gather/elementwise, recurrent and
- * sampler waves; non-split int8 models with the default (Intel) rcpps, no
- * preload / trace / stamps (-1 otherwise) */
+ * sampler waves (split models: two groups, 1,024 threads with two host
+ * waves); int8 models with the default (Intel) rcpps, no preload / trace /
+ * stamps (-1 otherwise) */
 /* mfw_kernel runs in rounds of one workgroup per CU.  Per stream at whole
  * rounds (24,576 streams, same box, profiles/r05): two groups 7.07 ms per
  * frame, three 7.36 (per-phase time 1.04x), mf2_kernel 8.02 -- so two

@@ -332,7 +332,7 @@ __device__ __forceinline__ void mf_h_split(const unsigned char *lds, const uint3
  * file is built with -fno-slp-vectorize) cost more SIMD issue cycles than
  * the scalar pairs, and waves 0/4 and 1/5 share one SIMD's VALU here
  * (measured: 7,450 -> 7,240 cycles per sample at 1024 streams). */
-template <int S, bool FAST, bool HW, typename Stamp>
+template <int S, bool FAST, bool HW, int TB = RCP_TABLE_BITS, typename Stamp>
 __device__ __forceinline__ void ga_elementwise(float (&st)[S], const float (&e)[S][9], const float *cnd, int tid,
                                                const float (&faz)[S], const float (&far)[S], const float (&tz)[S],
                                                const float (&tr)[S], const float (&hpre)[S], const uint32_t *rcp,
@@ -358,15 +358,15 @@ __device__ __forceinline__ void ga_elementwise(float (&st)[S], const float (&e)[
 #ifdef MF_FINE
   if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(11); }
 #endif
-  sigmoid_x86_fin_n<2 * S, HW>(zrv, rcp);
+  sigmoid_x86_fin_n<2 * S, HW, TB>(zrv, rcp);
 #ifdef MF_FINE
   if (stamping) { float g = 0.f; for (int k = 0; k < 2 * S; k++) g += zrv[k]; asm volatile("" ::"v"(g)); stamp(12); }
 #endif
   for (int s = 0; s < S; s++) hv[s] = hv[s] * zrv[S + s] + inh[s];
   if (FAST)
-    tanh_x86_fin_n<S, HW>(hv, rcp);
+    tanh_x86_fin_n<S, HW, TB>(hv, rcp);
   else
-    tanh_x86_n<S, HW>(hv, rcp);
+    tanh_x86_n<S, HW, TB>(hv, rcp);
   for (int s = 0; s < S; s++) st[s] = zrv[s] * st[s] + (1.f - zrv[s]) * hv[s];
 #ifdef MF_FINE
   if (stamping) { float g = 0.f; for (int k = 0; k < S; k++) g += st[k]; asm volatile("" ::"v"(g)); stamp(13); }

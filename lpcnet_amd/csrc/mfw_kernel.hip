@@ -84,12 +84,20 @@ static_assert(MfwLds<3>::total + MFW_IMG <= 160 * 1024, "mfw_kernel LDS");
  * streams per lane) instead of the hardware reciprocal */
 static_assert(MfwLds<2>::total + IMG_VAR <= 160 * 1024, "mfw_kernel LDS (two groups, table)");
 
-/* split form (two groups): the part area instead of the rcpps table */
-static_assert(MfwLds<2>::total + MFW_PRT + MFW_IMG <= 160 * 1024, "mfw_kernel LDS (two groups, split)");
+/* split form (two groups): the part area, and the rcpps table in its
+ * 2,048-entry form (the x86 entries of the 11-bit prefixes, MFW_RC11 bytes;
+ * the split form runs with that table only, see choose_kernel) instead of
+ * the device's 4,096 entries.  -DMFW_SPLIT_TAB=0 (A/B): the hardware
+ * reciprocal, no table */
+#ifndef MFW_SPLIT_TAB
+#define MFW_SPLIT_TAB 1
+#endif
+constexpr int MFW_RC11 = MFW_SPLIT_TAB ? 2048 * 4 : 0;
+static_assert(MfwLds<2>::total + MFW_PRT + MFW_IMG + MFW_RC11 <= 160 * 1024, "mfw_kernel LDS (two groups, split)");
 
 int mfw_lds_bytes(int groups, int split)
 {
-  if (split) return groups == 2 ? MfwLds<2>::total + MFW_PRT : 1 << 30;
+  if (split) return groups == 2 ? MfwLds<2>::total + MFW_PRT + MFW_IMG + MFW_RC11 : 1 << 30;
   return groups == 2 ? MfwLds<2>::total + IMG_VAR : MfwLds<3>::total + MFW_IMG;
 }
 
@@ -349,9 +357,12 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
 template <bool HWR, int MFW_G, bool SPLIT = false>
 __global__ __launch_bounds__(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS) void mfw_kernel(SampleArgs A)
 {
-  /* the rcpps table in LDS for the E waves (two groups, unsplit; see
-   * mfw_lds_bytes: the split form's part area takes its room) */
+  /* the rcpps table in LDS for the E waves: two groups, unsplit, the
+   * device table (TAB); the split form, its 2,048-entry form beside the part
+   * area (STAB, see mfw_lds_bytes) */
   constexpr bool TAB = MFW_G == 2 && MFW_TAB && !SPLIT;
+  constexpr bool STAB = SPLIT && MFW_SPLIT_TAB;
+  constexpr int TB = STAB ? 11 : RCP_TABLE_BITS;
   constexpr int NT = SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS;
   static_assert(!SPLIT || MFW_G == 2, "split form: two groups");
   static_assert(HWR, "mfw_kernel: hardware reciprocal only (no rcpps table in LDS)");
@@ -380,7 +391,8 @@ __global__ __launch_bounds__(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS) void mfw_k
   __shared__ uint4 img_s[(IMG_VAR - IMG0) / 16];
   const unsigned char *img = (const unsigned char *)img_s - IMG0; /* section offsets as in the full image */
   const float *ulaw = (const float *)(img + IMG_ULAW);
-  const uint32_t *rcpt = TAB ? (const uint32_t *)(img + IMG_RCP) : nullptr;
+  __shared__ uint32_t rc11[STAB ? 2048 : 1];
+  const uint32_t *rcpt = TAB ? (const uint32_t *)(img + IMG_RCP) : STAB ? rc11 : nullptr;
   const float *logit_tab = ulaw + 256;
   const float *fcw = logit_tab + 256;
   const float *fcb = fcw + 256 * 32;
@@ -419,6 +431,11 @@ __global__ __launch_bounds__(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS) void mfw_k
     return;
   }
   for (int o = tid; o < (IMG_VAR - IMG0) / 16; o += NT) img_s[o] = A.image[IMG0 / 16 + o];
+  if constexpr (STAB) {
+    /* entry i of the 11-bit table = the device table's entries 2i, 2i + 1 */
+    const uint32_t *dev = (const uint32_t *)A.image + IMG_RCP / 4;
+    for (int o = tid; o < 2048; o += NT) rc11[o] = dev[2 * o];
+  }
 
   if (wv >= MFW_R_WAVE0) {
     /* ======================= R role ====================================== */
@@ -590,9 +607,9 @@ __global__ __launch_bounds__(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS) void mfw_k
       auto nostamp = [&](int) { (void)stub; };
       const float *cg = cnd + g * GA_ROWS * S;
       if (__builtin_amdgcn_readfirstlane((int)fast[g]))
-        ga_elementwise<S, true, !TAB>(st[g], e, cg, tid, az, ar, tz, tr, hpre, rcpt, xa + g * S * MF_XSTR + i, false, nostamp);
+        ga_elementwise<S, true, !(TAB || STAB), TB>(st[g], e, cg, tid, az, ar, tz, tr, hpre, rcpt, xa + g * S * MF_XSTR + i, false, nostamp);
       else
-        ga_elementwise<S, false, !TAB>(st[g], e, cg, tid, az, ar, tz, tr, hpre, rcpt, xa + g * S * MF_XSTR + i, false, nostamp);
+        ga_elementwise<S, false, !(TAB || STAB), TB>(st[g], e, cg, tid, az, ar, tz, tr, hpre, rcpt, xa + g * S * MF_XSTR + i, false, nostamp);
     };
     using G0 = std::integral_constant<int, 0>;
     using G1 = std::integral_constant<int, 1>;
