@@ -186,9 +186,19 @@ __device__ __forceinline__ uint32_t mfw_x(const unsigned char *xg, const uint32_
 #ifndef MFW_S_PRIO
 #define MFW_S_PRIO 3
 #endif
-/* issue priority of the E waves */
+/* issue priority of the E waves (split form: MFW_E_PRIO_SPLIT, beside the
+ * host waves' 1: +0.8 %, profiles/r06/split_prio_ab_8192.json) */
 #ifndef MFW_E_PRIO
 #define MFW_E_PRIO 0
+#endif
+#ifndef MFW_E_PRIO_SPLIT
+#define MFW_E_PRIO_SPLIT 1
+#endif
+/* split form: issue priority of the host waves, the longest role (they
+ * share SIMDs 2 / 3 with the S waves at 3 and the R waves at 0): skewed
+ * 8,192 streams 464 -> 482 M at 1 or 2 (profiles/r06/split_prio_ab_8192.json) */
+#ifndef MFW_HOST_PRIO
+#define MFW_HOST_PRIO 1
 #endif
 
 /* one gate's product over NG 4-slot groups, NC accumulators (slot k -> k %
@@ -298,6 +308,9 @@ __device__ __forceinline__ void mfw_r_role(const SampleArgs &A, unsigned char *x
   /* the R waves' few VALU ops (x addresses) ahead of the E waves' stream on
    * the shared SIMDs: the MFMAs then run beside the elementwise step */
   __builtin_amdgcn_s_setprio(MFW_R_PRIO);
+#endif
+#if MFW_HOST_PRIO > 0
+  if constexpr (HOST) __builtin_amdgcn_s_setprio(MFW_HOST_PRIO);
 #endif
   MFW_STAMP_DECL;
   /* group (p - (G - 1)) mod G: three groups, the group E left two phases
@@ -527,9 +540,7 @@ __global__ __launch_bounds__(SPLIT ? MFW_THREADS_SPLIT : MFW_THREADS) void mfw_k
 #pragma unroll
       for (int s = 0; s < S; s++) xa[(g * S + s) * MF_XSTR + i] = (unsigned char)quant_s8_state(st[g][s]);
     __syncthreads(); /* initial q(h_A) of every group */
-#if MFW_E_PRIO > 0
-    __builtin_amdgcn_s_setprio(MFW_E_PRIO);
-#endif
+    if constexpr ((SPLIT ? MFW_E_PRIO_SPLIT : MFW_E_PRIO) > 0) __builtin_amdgcn_s_setprio(SPLIT ? MFW_E_PRIO_SPLIT : MFW_E_PRIO);
     bool fast[MFW_G];
 #pragma unroll
     for (int g = 0; g < MFW_G; g++) fast[g] = true;
