@@ -646,7 +646,9 @@ def dropin_rt(threads=(256, 960), frames=300):
                 pts.append(json.loads(r.stdout.strip().splitlines()[-1]))
             except (subprocess.SubprocessError, ValueError, IndexError, OSError) as e:
                 pts.append({"threads": T, "mode": mode, "error": str(e)[:200]})
-    ok = [p["threads"] for p in pts if p.get("realtime_p99") is True]
+    # a thread count is real-time when both pacings are (spread and burst)
+    ok = [T for T in threads if all(p.get("realtime_p99") is True for p in pts if p.get("threads") == T)
+          and any(p.get("threads") == T for p in pts)]
     worst = {m: max((p for p in pts if p.get("mode") == m and "latency_ms_p99" in p), key=lambda p: p["threads"],
                     default=None) for m in ("spread", "burst")}
     return {"max_threads_realtime_p99": max(ok) if ok else 0, "max_threads_measured": max(threads),

@@ -59,3 +59,24 @@ def test_rounding_helper():
     assert bench._r(None) is None
     assert bench._r(456426930.68781596) == 456400000.0
     assert bench._r(0.88216800) == 0.8822
+
+
+def test_dropin_rt_needs_both_pacings(monkeypatch):
+    """dropin_rt counts a thread count as real-time only when its spread and
+    burst runs both keep p99 <= 10 ms (canned child outputs, no GPU)."""
+    import subprocess
+    import types
+
+    def fake_run(cmd, **kw):
+        T, mode = int(cmd[1]), cmd[4]
+        rt = not (T == 960 and mode == "burst")
+        rec = {"threads": T, "frames": 300, "mode": mode, "latency_ms_p50": 1.0, "latency_ms_p99": 2.0 if rt else 12.0,
+               "latency_ms_max": 3.0, "deadline_misses": 0, "calls": T * 300, "mean_coalesced_streams": 10.0,
+               "realtime_p99": rt}
+        return types.SimpleNamespace(stdout=json.dumps(rec) + "\n", returncode=0)
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr(os.path, "exists", lambda p: True)
+    d = bench.dropin_rt(threads=(256, 960), frames=300)
+    assert d["max_threads_realtime_p99"] == 256
+    assert d["at_max"]["burst"]["latency_ms_p99"] == 12.0
