@@ -510,9 +510,10 @@ def run_live(L, blob, B, warmup, steps, preheat_ms=0.0, engine_buffers=True, dis
     (lpcnet_demo.c:208-219's loop for B streams at once; PCIe copies, the
     LPC, frame and sample kernels and the synchronisation all inside the
     timed region).  engine_buffers: the features are written into the
-    batch's pinned feature buffer and the PCM is read from its pinned PCM
-    buffer (lpcnet_batch_host_features / _pcm: no staging copies, the
-    sample kernel stores the PCM over PCIe itself); otherwise the caller's
+    batch's feature buffer (host-visible VRAM on large-BAR devices, else
+    pinned host memory) and the PCM is read from its pinned PCM buffer
+    (lpcnet_batch_host_features / _pcm: no staging copies, the sample
+    kernel stores the PCM over PCIe itself); otherwise the caller's
     own numpy arrays in and out.  distinct_frames: the streams' feature
     frames cycle with this period (long tick runs at large B without
     generating every frame).  Returns (seconds per frame for each timed
@@ -571,8 +572,9 @@ def live_line(L, blob, B, args, device_resident_value):
     res = dict(out["engine_buffers"])
     res["caller_buffers"] = out["caller_buffers"]
     res["what"] = ("host features in, host PCM out, one lpcnet_batch_synthesize per 10 ms frame (PCIe-inclusive; "
-                   "the headline `value` keeps the inputs resident in HBM); top level: features written into and "
-                   "PCM read from the batch's pinned buffers (lpcnet_batch_host_features / _pcm); caller_buffers: "
+                   "the headline `value` keeps the inputs resident in HBM); top level: features written into the "
+                   "batch's feature buffer (host-visible VRAM on large-BAR devices) and PCM read from its pinned PCM "
+                   "buffer (lpcnet_batch_host_features / _pcm); caller_buffers: "
                    "the caller's own arrays, staged through pinned memory by the engine")
     return res
 
