@@ -374,7 +374,7 @@ class _BatchOwner:
     """Owns the native batch: lpcnet_batch_destroy runs when the last
     reference goes -- the LPCNetBatch (until close()) or an array handed out
     by host_features() / synthesize_host(), whose buffer object holds this
-    owner, so such an array never outlives the pinned memory it views."""
+    owner, so such an array never outlives the host-visible memory it views."""
 
     def __init__(self, ptr):
         self.ptr = ptr
@@ -462,8 +462,10 @@ class LPCNetBatch:
         return out
 
     def host_features(self) -> np.ndarray:
-        """The batch's pinned feature buffer [B, 20] (lpcnet_batch_host_features):
-        fill it in place, then synthesize_host()."""
+        """The batch's feature buffer [B, 20] (lpcnet_batch_host_features:
+        host-visible VRAM on large-BAR devices, else pinned host memory;
+        write-combined there, so fill it in place and do not read it back
+        in a hot loop), then synthesize_host()."""
         if getattr(self, "_hf", None) is None:
             p = lib.lpcnet_batch_host_features(self._b)
             if not p:
@@ -483,7 +485,7 @@ class LPCNetBatch:
         (lpcnet_batch_synthesize on the batch's own buffers: no host staging
         copies; the sample kernel stores the PCM there itself where it can).
         Returns a [B, n] view of that buffer, overwritten by the next call
-        (copy it to keep it); the view keeps the batch's pinned memory alive
+        (copy it to keep it); the view keeps the batch's host buffers alive
         past close()."""
         self.host_features()
         if lib.lpcnet_batch_synthesize(self._b, self._hf_addr, self._hp_addr, n) != 0:
