@@ -898,15 +898,18 @@ static bool mfw_split_tables(const std::vector<std::vector<int>> &ga, const std:
       if (slot_of_ub[g][pc.unit] < 0) slot_of_ub[g][pc.unit] = ns++;
     if (ns > 16) return false;
   }
-  /* own unit blocks over the six R waves for the capped rows (the wide
-   * kernel's SIMD weight, mf_plan class 3); the E waves' lane order follows */
+  /* own unit blocks over the six R waves for the capped rows; the E waves'
+   * lane order follows.  The R waves on SIMDs 2 / 3 share them with a
+   * sampler, a host wave and an E wave, all at a higher issue priority:
+   * their rows are weighted 6x (the unsplit kernel's 2.5x: skewed 8,192
+   * streams 486 -> 494 M, 4x-10x alike, profiles/r06/split_simdw_8192.log) */
   std::vector<std::vector<int>> own(ga.size());
   for (int g = 0; g < 3; g++)
     for (int u = 0; u < NUB; u++) {
       const std::vector<int> &v = ga[g * NUB + u];
       own[g * NUB + u].assign(v.begin(), v.begin() + std::min((int)v.size(), cap[g]));
     }
-  g_mf_simd_weight = getenv("LPCNET_MF_SIMD_W") ? atoi(getenv("LPCNET_MF_SIMD_W")) : 25;
+  g_mf_simd_weight = getenv("LPCNET_MF_SIMD_W") ? atoi(getenv("LPCNET_MF_SIMD_W")) : 60;
   const std::vector<int> perm = mf_assign_unit_blocks(own, nullptr, 40000);
   T.units.assign(SAMPLE_THREADS, 0);
   for (int t = 0; t < SAMPLE_THREADS; t++) T.units[t] = 8 * perm[t / 8] + (t & 7);
